@@ -1,0 +1,14 @@
+"""MI355X-native geodesic ray-marcher: drop-in for the `Scene::render` hot path of
+jonathandw743/black_hole_ray_marching (src/black_hole_maybe.wgsl get_col / fs_main).
+
+The compute path is libbh_render.so (hand-written HIP for gfx950 behind the C ABI of
+include/bh_render.h); this package is the host-side mirror of the reference's Scene/Camera API.
+"""
+from ._abi import (BH_FATE_BLACKOUT, BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_LAYOUT_ROWMAJOR,
+                   BH_LAYOUT_TILES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_BGRA8_SRGB, BH_OUT_RGBA16F,
+                   BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BYTES_PER_PIXEL,
+                   BhError, load)
+from .scene import (MAX_ITERATIONS, Camera, CameraUniform, Scene, Uniforms, shard_tile_count, synthetic_sky,
+                    tiles_unpack)
+
+__version__ = "0.1.0"

@@ -1,0 +1,116 @@
+"""ctypes view of include/bh_render.h (the C ABI).  No torch types cross this boundary."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libbh_render.so"
+
+BH_OK = 0
+BH_ERR_INVALID_ARG = -1
+BH_ERR_UNSUPPORTED = -2
+BH_ERR_HIP = -3
+BH_ERR_NO_DEVICE = -4
+BH_ERR_OUT_OF_MEMORY = -5
+
+BH_OUT_RGBA32F, BH_OUT_RGBA16F, BH_OUT_BGRA8_SRGB = 0, 1, 2
+BH_MATH_EXACT, BH_MATH_FAST = 0, 1
+BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
+BH_SCENE_DEFAULT = 3
+BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES = 0, 1
+BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
+BH_TILE = 8
+
+BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
+
+
+class bh_camera_uniform(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("_pad0", C.c_float),
+                ("screen_tri", (C.c_float * 4) * 3), ("world_tri", (C.c_float * 4) * 3)]
+
+
+class bh_uniforms(C.Structure):
+    _fields_ = [("rs", C.c_float), ("delta_time_mult", C.c_float), ("bg_brightness", C.c_float),
+                ("blackout_eh", C.c_uint32), ("max_dist", C.c_float), ("distortion_power", C.c_float),
+                ("_pad", C.c_uint32 * 2)]
+
+
+class bh_camera(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("dir", C.c_float * 3), ("up", C.c_float * 3),
+                ("aspect", C.c_float), ("fovy", C.c_float), ("znear", C.c_float), ("zfar", C.c_float)]
+
+
+class bh_render_desc(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("max_iters", C.c_uint32),
+                ("scene_flags", C.c_uint32), ("format", C.c_uint32), ("math", C.c_uint32),
+                ("layout", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
+                ("_reserved", C.c_uint32), ("out_col", C.c_void_p), ("out_blackout", C.c_void_p),
+                ("dbg_n_rk", C.c_void_p), ("dbg_fate", C.c_void_p)]
+
+
+assert C.sizeof(bh_camera_uniform) == 112
+assert C.sizeof(bh_uniforms) == 32
+
+# name -> (restype, argtypes): every entry point declared in include/bh_render.h
+SIGNATURES = {
+    "bh_abi_version": (C.c_int, []),
+    "bh_status_string": (C.c_char_p, [C.c_int]),
+    "bh_last_error": (C.c_char_p, []),
+    "bh_uniforms_default": (C.c_int, [C.POINTER(bh_uniforms)]),
+    "bh_camera_default": (C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(bh_camera)]),
+    "bh_camera_uniform_update": (C.c_int, [C.POINTER(bh_camera), C.POINTER(bh_camera_uniform)]),
+    "bh_camera_look_at": (C.c_int, [C.c_float * 3, C.c_float * 3, C.c_uint32, C.c_uint32, C.POINTER(bh_camera)]),
+    "bh_synthetic_sky": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint64]),
+    "bh_create": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_void_p)]),
+    "bh_destroy": (C.c_int, [C.c_void_p]),
+    "bh_render": (C.c_int, [C.c_void_p, C.POINTER(bh_camera_uniform), C.POINTER(bh_uniforms),
+                            C.POINTER(bh_render_desc), C.c_void_p]),
+    "bh_shard_tile_count": (C.c_int64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.c_uint64, C.c_uint32, C.c_void_p]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libbh_render.so.  Fails loudly if it has not been built (there is no fallback path).
+
+    torch is imported first when available so that this library binds to the same HIP runtime
+    (SONAME libamdhip64.so.7) that torch already mapped; otherwise two runtimes would coexist.
+    """
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"{LIB_PATH} is missing: run `python -m black_hole_ray_marching_amd.build` "
+                           "(there is no CPU fallback for the render path)")
+    if os.environ.get("BH_NO_TORCH_PRELOAD") != "1":
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.bh_abi_version() != 1:
+        raise RuntimeError("libbh_render.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+class BhError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        lib = load()
+        msg = lib.bh_status_string(status).decode()
+        detail = lib.bh_last_error().decode()
+        super().__init__(f"{what}: {msg} ({status})" + (f": {detail}" if detail else ""))
+        self.status = status
+
+
+def check(status: int, what: str) -> None:
+    if status != BH_OK:
+        raise BhError(status, what)

@@ -1,0 +1,84 @@
+"""In-tree build of the native libraries (no cmake, no JIT cache — the .so files travel with the repo).
+
+  black_hole_ray_marching_amd/libbh_render.so   product: HIP kernels for gfx950 + C ABI (hipcc)
+  oracle/libbh_oracle.so                        test infrastructure: CPU oracle (gcc, OpenMP)
+
+Run `python -m black_hole_ray_marching_amd.build` or call build_all().
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+OBJ = PKG / "_build"
+LIB = PKG / "libbh_render.so"
+ORACLE_SRC = ROOT / "oracle" / "bh_oracle.c"
+ORACLE_LIB = ROOT / "oracle" / "libbh_oracle.so"
+
+ARCH = os.environ.get("BH_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
+
+COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+# per-translation-unit floating-point contracts (DESIGN.md "Math modes")
+TU_FLAGS = {
+    "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
+    "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
+    "bh_tiles.hip": [],
+    "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
+}
+
+
+def _run(cmd: list[str]) -> None:
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build step failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}")
+
+
+def _stale(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def build_product(force: bool = False) -> Path:
+    OBJ.mkdir(exist_ok=True)
+    headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "bh_render.h"]
+    objs = []
+    for src, flags in TU_FLAGS.items():
+        s = CSRC / src
+        o = OBJ / (s.stem + ".o")
+        if force or _stale(o, [s, *headers, Path(__file__)]):
+            _run([HIPCC, *COMMON, *flags, "-c", str(s), "-o", str(o)])
+        objs.append(o)
+    if force or _stale(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)])
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    if force or _stale(ORACLE_LIB, [ORACLE_SRC, ROOT / "include" / "bh_render.h", Path(__file__)]):
+        tmp = ORACLE_LIB.with_suffix(".so.tmp")
+        _run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC",
+              "-shared", "-o", str(tmp), str(ORACLE_SRC), "-lm"])
+        os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False) -> None:
+    build_product(force)
+    build_oracle(force)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv)
+    print(LIB)
+    print(ORACLE_LIB)

@@ -1,0 +1,82 @@
+// bh_common.hpp — host/device shared definitions for the geodesic ray-marcher (no math here).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/bh_render.h"
+
+namespace bh {
+
+// Everything one launch needs, passed by value as the kernel argument (lives in SGPRs / kernarg).
+struct MarchArgs {
+    // camera uniform (src/black_hole_maybe.wgsl:9-17): ro0 and the three interpolated corner rays
+    float pos[3];
+    float c0[3], c1[3], c2[3];
+    // Uniforms (src/black_hole_maybe.wgsl:58-69)
+    float rs, dtm, max_dist, dp;
+    uint32_t blackout_eh;
+    // frame
+    uint32_t width, height, max_iters, scene_flags;
+    uint32_t format, layout;
+    uint32_t shard_index, shard_count;
+    uint32_t tiles_x, tiles_y;
+    uint32_t n_tiles;          // tiles owned by this shard (= grid work items)
+    // sky (Rgba8UnormSrgb texels as packed u32, little endian: r | g<<8 | b<<16 | a<<24)
+    const uint32_t* sky;
+    const float* srgb_lut;     // 256 entries, sRGB byte -> linear
+    uint32_t sky_w, sky_h;
+    // outputs
+    void* out_col;
+    void* out_blackout;
+    uint16_t* dbg_n_rk;
+    uint8_t* dbg_fate;
+};
+
+// Shard ownership: tile (tx, ty) belongs to shard (tx + 3*ty) % S (SURVEY §8e diagonal interleave).
+// Row ty's first owned column for shard k.
+__host__ __device__ inline uint32_t shard_row_start(uint32_t ty, uint32_t k, uint32_t S) {
+    // (k - 3*ty) mod S, computed without negatives
+    uint32_t m = (3u * (ty % S)) % S;
+    return (k + S - m) % S;
+}
+__host__ __device__ inline uint32_t shard_row_count(uint32_t tiles_x, uint32_t ty, uint32_t k, uint32_t S) {
+    uint32_t st = shard_row_start(ty, k, S);
+    return st < tiles_x ? (tiles_x - st + S - 1u) / S : 0u;
+}
+// Tiles owned in one full period of rows.  Period P = S / gcd(S, 3).
+__host__ __device__ inline uint32_t shard_period(uint32_t S) { return (S % 3u == 0u) ? S / 3u : S; }
+
+__host__ __device__ inline uint64_t shard_tile_count(uint32_t tiles_x, uint32_t tiles_y, uint32_t k, uint32_t S) {
+    const uint32_t P = shard_period(S);
+    uint64_t per = 0;
+    for (uint32_t r = 0; r < P && r < tiles_y; ++r) per += shard_row_count(tiles_x, r, k, S);
+    uint64_t full = tiles_y / P, n = full * per;
+    for (uint32_t r = 0; r < tiles_y % P; ++r) n += shard_row_count(tiles_x, r, k, S);
+    return n;
+}
+
+// Shard-local tile index t -> global tile coordinates.  Walks at most one row period (P <= S rows).
+__host__ __device__ inline void shard_tile_coords(uint32_t t, uint32_t tiles_x, uint32_t k, uint32_t S,
+                                                  uint32_t* tx, uint32_t* ty) {
+    if (S == 1u) { *ty = t / tiles_x; *tx = t - *ty * tiles_x; return; }
+    const uint32_t P = shard_period(S);
+    uint32_t per = 0;
+    for (uint32_t r = 0; r < P; ++r) per += shard_row_count(tiles_x, r, k, S);
+    uint32_t period = t / per, rem = t - period * per, row = period * P;
+    for (uint32_t r = 0; r < P; ++r) {
+        uint32_t c = shard_row_count(tiles_x, r, k, S);
+        if (rem < c) { row += r; break; }
+        rem -= c;
+    }
+    *ty = row;
+    *tx = shard_row_start(row, k, S) + rem * S;
+}
+
+}  // namespace bh
+
+// Launchers (defined in the .hip translation units).
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_fast(const bh::MarchArgs& a, hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
+                                      uint32_t shard_count, uint64_t shard_stride_tiles,
+                                      uint32_t bytes_per_pixel, hipStream_t s);

@@ -1,0 +1,335 @@
+// bh_host.cpp — C ABI of include/bh_render.h: context, camera/uniform host math, synthetic sky,
+// render dispatch.  No CPU rendering path exists here by design: bh_render runs the HIP kernel or
+// fails with a status code.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bh_common.hpp"
+
+struct bh_ctx {
+    int device = 0;
+    uint32_t* sky = nullptr;   // device RGBA8 texels
+    float* lut = nullptr;      // device sRGB->linear table (256 floats)
+    uint32_t sky_w = 0, sky_h = 0;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int hip_fail(hipError_t e, const char* what) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return BH_ERR_HIP;
+}
+
+// ---- glam 0.24 Vec3 subset (scalar f32, left-to-right association as glam writes it) ----------
+struct V3 { float x, y, z; };
+V3 v_add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+V3 v_sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+V3 v_mul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+float v_dot(V3 a, V3 b) { return (a.x * b.x) + (a.y * b.y) + (a.z * b.z); }
+V3 v_cross(V3 a, V3 b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+V3 v_normalize(V3 a) { return v_mul(a, 1.0f / std::sqrt(v_dot(a, a))); }  // self * length_recip()
+V3 v_neg(V3 a) { return {-a.x, -a.y, -a.z}; }
+
+// sRGB byte -> linear, in double (the Rgba8UnormSrgb decode; DESIGN.md "Normative arithmetic").
+void srgb_lut(float lut[256]) {
+    for (int i = 0; i < 256; ++i) {
+        double c = (double)i / 255.0;
+        lut[i] = (float)(c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4));
+    }
+}
+
+bool screen_tri_default(const bh_camera_uniform* c) {
+    static const float st[3][2] = {{3.0f, 1.0f}, {-1.0f, 1.0f}, {-1.0f, -3.0f}};
+    for (int i = 0; i < 3; ++i)
+        if (c->screen_tri[i][0] != st[i][0] || c->screen_tri[i][1] != st[i][1]) return false;
+    return true;
+}
+
+uint64_t splitmix64(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+uint64_t hash3(uint64_t seed, int64_t a, int64_t b, int64_t c) {
+    uint64_t s = seed ^ ((uint64_t)a * 0x9E3779B185EBCA87ull) ^ ((uint64_t)b * 0xC2B2AE3D27D4EB4Full) ^
+                 ((uint64_t)c * 0x165667B19E3779F9ull);
+    return splitmix64(s);
+}
+float unit(uint64_t h) { return (float)(h >> 40) * (1.0f / 16777216.0f); }
+
+// periodic-in-x lattice value noise, smoothstep interpolation
+float value_noise(uint64_t seed, int oct, float x, float y, int period_x) {
+    float fx = std::floor(x), fy = std::floor(y);
+    int ix = (int)fx, iy = (int)fy;
+    float tx = x - fx, ty = y - fy;
+    tx = tx * tx * (3.0f - 2.0f * tx);
+    ty = ty * ty * (3.0f - 2.0f * ty);
+    auto L = [&](int cx, int cy) {
+        int wx = ((cx % period_x) + period_x) % period_x;
+        return unit(hash3(seed, oct, wx, cy));
+    };
+    float a = L(ix, iy), b = L(ix + 1, iy), c = L(ix, iy + 1), d = L(ix + 1, iy + 1);
+    return (a + (b - a) * tx) + ((c + (d - c) * tx) - (a + (b - a) * tx)) * ty;
+}
+
+uint8_t encode8(float lin) {
+    if (!(lin > 0.0f)) return 0;
+    if (lin >= 1.0f) return 255;
+    double v = lin, s = v <= 0.0031308 ? 12.92 * v : 1.055 * std::pow(v, 1.0 / 2.4) - 0.055;
+    return (uint8_t)std::floor(s * 255.0 + 0.5);
+}
+
+}  // namespace
+
+extern "C" {
+
+int bh_abi_version(void) { return BH_ABI_VERSION; }
+
+const char* bh_status_string(int st) {
+    switch (st) {
+        case BH_OK: return "ok";
+        case BH_ERR_INVALID_ARG: return "invalid argument";
+        case BH_ERR_UNSUPPORTED: return "unsupported";
+        case BH_ERR_HIP: return "HIP runtime error";
+        case BH_ERR_NO_DEVICE: return "no HIP device";
+        case BH_ERR_OUT_OF_MEMORY: return "out of device memory";
+        default: return "unknown status";
+    }
+}
+
+const char* bh_last_error(void) { return g_last_error.c_str(); }
+
+// Scene::new defaults, src/scene.rs:89-137 (RS 1.0, max dt 0.5, bg 0.5, blackout PodBool::r#false()
+// whose inner is 1 (src/podbool.rs:24-26), max dist 250, distortion 1.0); 24 B padded to 32.
+int bh_uniforms_default(bh_uniforms* out) {
+    if (!out) return BH_ERR_INVALID_ARG;
+    std::memset(out, 0, sizeof(*out));
+    out->rs = 1.0f;
+    out->delta_time_mult = 0.5f;
+    out->bg_brightness = 0.5f;
+    out->blackout_eh = 1u;
+    out->max_dist = 250.0f;
+    out->distortion_power = 1.0f;
+    return BH_OK;
+}
+
+// src/scene.rs:68-76
+int bh_camera_default(uint32_t width, uint32_t height, bh_camera* out) {
+    if (!out || width == 0 || height == 0) return BH_ERR_INVALID_ARG;
+    const float PI = 3.14159265358979323846f;  // std::f32::consts::PI
+    *out = bh_camera{{0.0f, 0.0f, -20.0f}, {0.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 0.0f},
+                     (float)width / (float)height, PI * 0.5f, 0.1f, 100.0f};
+    return BH_OK;
+}
+
+int bh_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                      bh_camera* out) {
+    if (!pos || !target) return BH_ERR_INVALID_ARG;
+    int st = bh_camera_default(width, height, out);
+    if (st != BH_OK) return st;
+    V3 p{pos[0], pos[1], pos[2]}, t{target[0], target[1], target[2]};
+    V3 d = v_normalize(v_sub(t, p));
+    std::memcpy(out->pos, pos, 3 * sizeof(float));
+    out->dir[0] = d.x; out->dir[1] = d.y; out->dir[2] = d.z;
+    return BH_OK;
+}
+
+// CameraUniform::new (src/uniforms.rs:108-122) + ::update (:123-133) ->
+// Camera::pos_to_world_space_screen_triangle (src/camera.rs:89-112):
+//   corner_i = rot_matrix * ( -(tx * cx_i), -(-ty) * cy_i ... ) — concretely
+//   dir_camera = -vec3(tx*cx, -ty*cy, 1)  (camera.rs:70-74),
+//   rot_matrix = look_at_rh(pos, pos + dir, up).inverse()  (camera.rs:56-58),
+//   world = rot_matrix.transform_vector3(dir_camera)  (camera.rs:76).
+// The view matrix is a rigid transform, so its inverse's rotation block is the transpose
+// (columns s, u, -f).  glam's general f32 Mat4::inverse may differ from the transpose in the last
+// ulp; the corners are kernel INPUTS, so this host step is outside kernel parity.
+int bh_camera_uniform_update(const bh_camera* cam, bh_camera_uniform* out) {
+    if (!cam || !out) return BH_ERR_INVALID_ARG;
+    std::memset(out, 0, sizeof(*out));
+    static const float st[3][2] = {{3.0f, 1.0f}, {-1.0f, 1.0f}, {-1.0f, -3.0f}};
+    for (int i = 0; i < 3; ++i) { out->screen_tri[i][0] = st[i][0]; out->screen_tri[i][1] = st[i][1]; }
+    V3 pos{cam->pos[0], cam->pos[1], cam->pos[2]};
+    V3 dir{cam->dir[0], cam->dir[1], cam->dir[2]};
+    V3 up{cam->up[0], cam->up[1], cam->up[2]};
+    // look_at_rh(eye, center, up) = look_to_rh(eye, center - eye, up)
+    V3 f = v_normalize(v_sub(v_add(pos, dir), pos));
+    V3 s = v_normalize(v_cross(f, up));
+    V3 u = v_cross(s, f);
+    V3 col0 = s, col1 = u, col2 = v_neg(f);
+    // tan_fov_half (camera.rs:60-63)
+    float tfy = std::tan(cam->fovy / 2.0f);
+    float tfx = tfy * cam->aspect;
+    for (int i = 0; i < 3; ++i) {
+        float cx = st[i][0], cy = st[i][1];
+        V3 dc = v_neg(V3{tfx * cx, -tfy * cy, 1.0f});
+        // transform_vector3: res = x_axis*x; res = y_axis*y + res; res = z_axis*z + res
+        V3 res = v_mul(col0, dc.x);
+        res = v_add(v_mul(col1, dc.y), res);
+        res = v_add(v_mul(col2, dc.z), res);
+        out->world_tri[i][0] = res.x; out->world_tri[i][1] = res.y; out->world_tri[i][2] = res.z;
+        out->world_tri[i][3] = 0.0f;
+    }
+    out->pos[0] = pos.x; out->pos[1] = pos.y; out->pos[2] = pos.z;
+    return BH_OK;
+}
+
+static void sky_rows(uint8_t* out, uint32_t w, uint32_t h, uint64_t seed, uint32_t y0, uint32_t y1) {
+    const int base = 6;  // nebula lattice cells around the equator at octave 0
+    for (uint32_t y = y0; y < y1; ++y) {
+        for (uint32_t x = 0; x < w; ++x) {
+            float u = ((float)x + 0.5f) / (float)w, v = ((float)y + 0.5f) / (float)h;
+            float n1 = 0.0f, n2 = 0.0f, amp = 0.5f;
+            for (int o = 0; o < 5; ++o) {
+                int per = base << o;
+                n1 += amp * value_noise(seed, o, u * per, v * (per / 2), per);
+                n2 += amp * value_noise(seed ^ 0xA5A5A5A5ull, o, u * per, v * (per / 2), per);
+                amp *= 0.5f;
+            }
+            float neb = std::fmax(0.0f, n1 - 0.45f) * 1.6f;
+            float r = 0.012f + 0.55f * neb * neb + 0.10f * n2 * neb;
+            float g = 0.010f + 0.22f * neb * n2;
+            float b = 0.030f + 0.65f * neb * (1.0f - 0.5f * n2);
+            uint64_t hs = hash3(seed ^ 0x5354415253ull, 99, x, y);  // "STARS"
+            if ((hs & 0xFFFu) < 6u) {                                // ~0.15 % of texels
+                float mag = unit(hs);
+                float temp = unit(hs * 0x2545F4914F6CDD1Dull);
+                float L = 0.25f + 0.75f * mag * mag;
+                r += L * (0.8f + 0.2f * temp);
+                g += L * 0.85f;
+                b += L * (1.0f - 0.3f * temp);
+            }
+            uint8_t* p = out + ((size_t)y * w + x) * 4u;
+            p[0] = encode8(r); p[1] = encode8(g); p[2] = encode8(b); p[3] = 255;
+        }
+    }
+}
+
+// Rows are independent, so the result does not depend on the thread count.
+int bh_synthetic_sky(uint8_t* out, uint32_t w, uint32_t h, uint64_t seed) {
+    if (!out || w == 0 || h == 0) return BH_ERR_INVALID_ARG;
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt == 0 ? 1 : (nt > 16 ? 16 : nt);
+    if (nt > h) nt = h;
+    std::vector<std::thread> pool;
+    for (unsigned t = 0; t < nt; ++t) {
+        uint32_t y0 = (uint32_t)((uint64_t)h * t / nt), y1 = (uint32_t)((uint64_t)h * (t + 1) / nt);
+        pool.emplace_back(sky_rows, out, w, h, seed, y0, y1);
+    }
+    for (auto& th : pool) th.join();
+    return BH_OK;
+}
+
+int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh_ctx** out) {
+    if (!sky || !out || sky_w == 0 || sky_h == 0 || sky_w > 32768u || sky_h > 32768u) return BH_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) { g_last_error = "no HIP device"; return BH_ERR_NO_DEVICE; }
+    if (device < 0 || device >= ndev) { g_last_error = "device index out of range"; return BH_ERR_NO_DEVICE; }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if ((e = hipSetDevice(device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    bh_ctx* c = new (std::nothrow) bh_ctx();
+    if (!c) return BH_ERR_OUT_OF_MEMORY;
+    c->device = device;
+    c->sky_w = sky_w;
+    c->sky_h = sky_h;
+    const size_t bytes = (size_t)sky_w * sky_h * 4u;
+    float lut[256];
+    srgb_lut(lut);
+    int st = BH_OK;
+    if ((e = hipMalloc(&c->sky, bytes)) != hipSuccess) st = (e == hipErrorOutOfMemory) ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "hipMalloc(sky)");
+    else if ((e = hipMalloc(&c->lut, sizeof(lut))) != hipSuccess) st = hip_fail(e, "hipMalloc(lut)");
+    else if ((e = hipMemcpy(c->sky, sky, bytes, hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(sky)");
+    else if ((e = hipMemcpy(c->lut, lut, sizeof(lut), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(lut)");
+    (void)hipSetDevice(prev);
+    if (st != BH_OK) { bh_destroy(c); return st; }
+    *out = c;
+    return BH_OK;
+}
+
+int bh_destroy(bh_ctx* c) {
+    if (!c) return BH_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(c->device);
+    if (c->sky) (void)hipFree(c->sky);
+    if (c->lut) (void)hipFree(c->lut);
+    (void)hipSetDevice(prev);
+    delete c;
+    return BH_OK;
+}
+
+int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count) {
+    if (width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count) return BH_ERR_INVALID_ARG;
+    return (int64_t)bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, shard_index, shard_count);
+}
+
+int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, const bh_render_desc* d,
+              void* stream) {
+    if (!c || !cam || !U || !d || !d->out_col) return BH_ERR_INVALID_ARG;
+    if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
+    if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
+    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES) return BH_ERR_INVALID_ARG;
+    if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
+    if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
+    if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
+    if (d->format == BH_OUT_BGRA8_SRGB) { g_last_error = "BGRA8 sRGB output not implemented yet"; return BH_ERR_UNSUPPORTED; }
+    if (!screen_tri_default(cam)) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
+
+    bh::MarchArgs a;
+    std::memset(&a, 0, sizeof(a));
+    for (int k = 0; k < 3; ++k) {
+        a.pos[k] = cam->pos[k];
+        a.c0[k] = cam->world_tri[0][k];
+        a.c1[k] = cam->world_tri[1][k];
+        a.c2[k] = cam->world_tri[2][k];
+    }
+    a.rs = U->rs; a.dtm = U->delta_time_mult; a.max_dist = U->max_dist; a.dp = U->distortion_power;
+    a.blackout_eh = U->blackout_eh;
+    a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
+    a.format = d->format; a.layout = d->layout;
+    a.shard_index = d->shard_index; a.shard_count = d->shard_count;
+    a.tiles_x = (d->width + 7u) / 8u; a.tiles_y = (d->height + 7u) / 8u;
+    const uint64_t nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
+    if (nt > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
+    a.n_tiles = (uint32_t)nt;
+    a.sky = c->sky; a.srgb_lut = c->lut; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
+    a.out_col = d->out_col; a.out_blackout = d->out_blackout;
+    a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate;
+    if (a.n_tiles == 0) return BH_OK;
+
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (prev != c->device) (void)hipSetDevice(c->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, s) : bh_launch_march_fast(a, s);
+    if (prev != c->device) (void)hipSetDevice(prev);
+    if (e != 0) return hip_fail((hipError_t)e, "march kernel launch");
+    return BH_OK;
+}
+
+int bh_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
+                    uint64_t shard_stride_tiles, uint32_t bpp, void* stream) {
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
+    if (bpp != 4 && bpp != 8 && bpp != 16) return BH_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < shard_count; ++k)
+        if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
+            return BH_ERR_INVALID_ARG;
+    int e = bh_launch_tiles_unpack(packed, out, width, height, shard_count, shard_stride_tiles, bpp,
+                                   reinterpret_cast<hipStream_t>(stream));
+    if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
+    return BH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+"""Host-side mirror of the reference's render-to-texture interface, over the C ABI.
+
+Reference (jonathandw743/black_hole_ray_marching):
+  Camera            src/camera.rs:11-20, 56-112
+  CameraUniform     src/uniforms.rs:98-133
+  OtherUniforms     src/otheruniforms.rs:105-118, defaults src/scene.rs:89-137
+  Scene             src/scene.rs:28-522  (new :53, resize :370, update :444, render :470)
+
+`Scene.render(output, blackout_output=None)` mirrors `Scene::render(encoder, output_view,
+blackout_output_view)`: the caller owns the output images (device tensors here, texture views
+there); `None` for the blackout target mirrors `Option::None`.  Errors raise `BhError` (the
+reference panics on wgpu validation errors).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _abi
+from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
+                   BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
+
+MAX_ITERATIONS = 1000  # src/black_hole_maybe.wgsl:85
+
+
+@dataclass
+class Camera:
+    """src/camera.rs:11-20."""
+    pos: tuple = (0.0, 0.0, -20.0)
+    dir: tuple = (0.0, 0.0, 1.0)
+    up: tuple = (0.0, 1.0, 0.0)
+    aspect: float = 1.0
+    fovy: float = float(np.float32(np.pi) * np.float32(0.5))
+    znear: float = 0.1
+    zfar: float = 100.0
+
+    @classmethod
+    def default(cls, width: int, height: int) -> "Camera":
+        """The camera of Scene::new (src/scene.rs:68-76)."""
+        c = _abi.bh_camera()
+        check(load().bh_camera_default(width, height, C.byref(c)), "bh_camera_default")
+        return cls._from_c(c)
+
+    @classmethod
+    def look_at(cls, pos, target, width: int, height: int) -> "Camera":
+        c = _abi.bh_camera()
+        check(load().bh_camera_look_at((C.c_float * 3)(*pos), (C.c_float * 3)(*target), width, height,
+                                       C.byref(c)), "bh_camera_look_at")
+        return cls._from_c(c)
+
+    @classmethod
+    def _from_c(cls, c) -> "Camera":
+        return cls(tuple(c.pos), tuple(c.dir), tuple(c.up), c.aspect, c.fovy, c.znear, c.zfar)
+
+    def to_c(self) -> _abi.bh_camera:
+        return _abi.bh_camera((C.c_float * 3)(*self.pos), (C.c_float * 3)(*self.dir),
+                              (C.c_float * 3)(*self.up), self.aspect, self.fovy, self.znear, self.zfar)
+
+
+class CameraUniform:
+    """src/uniforms.rs:98-133 — the 112-byte WGSL `Camera` uniform."""
+
+    def __init__(self) -> None:
+        self.c = _abi.bh_camera_uniform()
+        for i, (x, y) in enumerate(((3.0, 1.0), (-1.0, 1.0), (-1.0, -3.0))):  # ::new
+            self.c.screen_tri[i][0], self.c.screen_tri[i][1] = x, y
+
+    def update(self, camera: Camera) -> None:
+        check(load().bh_camera_uniform_update(C.byref(camera.to_c()), C.byref(self.c)),
+              "bh_camera_uniform_update")
+
+    @property
+    def pos(self) -> np.ndarray:
+        return np.array(self.c.pos, dtype=np.float32)
+
+    @property
+    def world_tri(self) -> np.ndarray:
+        return np.array([[self.c.world_tri[i][k] for k in range(3)] for i in range(3)], dtype=np.float32)
+
+    def to_bytes(self) -> bytes:
+        return bytes(self.c)
+
+
+@dataclass
+class Uniforms:
+    """The 32-byte WGSL `Uniforms` block (src/black_hole_maybe.wgsl:58-69) with Scene::new defaults."""
+    rs: float = 1.0
+    delta_time_mult: float = 0.5
+    bg_brightness: float = 0.5
+    blackout_eh: int = 1   # PodBool::r#false() stores inner = 1 (src/podbool.rs:24-26) => on
+    max_dist: float = 250.0
+    distortion_power: float = 1.0
+
+    @classmethod
+    def default(cls) -> "Uniforms":
+        u = _abi.bh_uniforms()
+        check(load().bh_uniforms_default(C.byref(u)), "bh_uniforms_default")
+        return cls(u.rs, u.delta_time_mult, u.bg_brightness, u.blackout_eh, u.max_dist, u.distortion_power)
+
+    def to_c(self) -> _abi.bh_uniforms:
+        return _abi.bh_uniforms(self.rs, self.delta_time_mult, self.bg_brightness, int(self.blackout_eh),
+                                self.max_dist, self.distortion_power)
+
+    def as_dict(self) -> dict:
+        return dict(rs=self.rs, delta_time_mult=self.delta_time_mult, blackout_eh=self.blackout_eh,
+                    max_dist=self.max_dist, distortion_power=self.distortion_power)
+
+
+def synthetic_sky(width: int = 4096, height: int = 2048, seed: int = 0x5EED_B1AC_401E) -> np.ndarray:
+    """Deterministic RGBA8 sRGB equirectangular sky, (height, width, 4) uint8."""
+    out = np.empty((height, width, 4), dtype=np.uint8)
+    check(load().bh_synthetic_sky(out.ctypes.data, width, height, seed), "bh_synthetic_sky")
+    return out
+
+
+def shard_tile_count(width: int, height: int, shard_index: int, shard_count: int) -> int:
+    n = load().bh_shard_tile_count(width, height, shard_index, shard_count)
+    if n < 0:
+        raise BhError(int(n), "bh_shard_tile_count")
+    return int(n)
+
+
+def _ptr(t) -> int | None:
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+class Scene:
+    """src/scene.rs `Scene`: owns the sky texture (on `device`), camera, uniforms; renders frames."""
+
+    def __init__(self, width: int, height: int, sky: np.ndarray | None = None, device: int = 0,
+                 render_blackout: bool = True, max_iters: int = MAX_ITERATIONS,
+                 scene_flags: int = BH_SCENE_DEFAULT, math: int = BH_MATH_FAST) -> None:
+        self.lib = load()
+        self.width, self.height = width, height
+        self.render_blackout = render_blackout
+        self.max_iters, self.scene_flags, self.math = max_iters, scene_flags, math
+        self.camera = Camera.default(width, height)
+        self.camera_uniform = CameraUniform()
+        self.camera_uniform.update(self.camera)
+        self.uniforms = Uniforms.default()
+        if sky is None:
+            sky = synthetic_sky()
+        sky = np.ascontiguousarray(sky, dtype=np.uint8)
+        if sky.ndim != 3 or sky.shape[2] != 4:
+            raise ValueError("sky must be (H, W, 4) uint8 RGBA (Rgba8UnormSrgb texels)")
+        self.sky = sky
+        ctx = C.c_void_p()
+        check(self.lib.bh_create(sky.ctypes.data, sky.shape[1], sky.shape[0], device, C.byref(ctx)), "bh_create")
+        self._ctx = ctx
+        self.device = device
+
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self.lib.bh_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def resize(self, width: int, height: int) -> None:
+        """src/scene.rs:370-382: only the aspect changes; corners are re-derived by update()."""
+        self.width, self.height = width, height
+        self.camera.aspect = float(np.float32(width) / np.float32(height))
+
+    def update(self, camera: Camera | None = None) -> None:
+        """src/scene.rs:444-466 (minus the interactive controller): re-derive the camera uniform."""
+        if camera is not None:
+            self.camera = camera
+        self.camera_uniform.update(self.camera)
+
+    def render(self, output, blackout_output=None, *, fmt: int = BH_OUT_RGBA32F, stream=None,
+               dbg_n_rk=None, dbg_fate=None, math: int | None = None, layout: int = BH_LAYOUT_ROWMAJOR,
+               shard_index: int = 0, shard_count: int = 1, width: int | None = None,
+               height: int | None = None) -> None:
+        """Scene::render (src/scene.rs:470-522): one pass writing `col` and optionally `blackout_col`.
+
+        `output`/`blackout_output`: caller-owned device buffers (torch tensors or raw pointers).
+        Asynchronous on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None = current).
+        """
+        if output is None:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, "render: output is required")
+        if not self.render_blackout and blackout_output is not None:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, "render: scene built without a blackout target")
+        d = _abi.bh_render_desc()
+        d.width, d.height = width or self.width, height or self.height
+        d.max_iters, d.scene_flags = self.max_iters, self.scene_flags
+        d.format = fmt
+        d.math = self.math if math is None else math
+        d.layout, d.shard_index, d.shard_count = layout, shard_index, shard_count
+        d.out_col, d.out_blackout = _ptr(output), _ptr(blackout_output)
+        d.dbg_n_rk, d.dbg_fate = _ptr(dbg_n_rk), _ptr(dbg_fate)
+        check(self.lib.bh_render(self._ctx, C.byref(self.camera_uniform.c), C.byref(self.uniforms.to_c()),
+                                 C.byref(d), _stream_handle(stream)), "bh_render")
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                return torch.cuda.current_stream().cuda_stream
+        except ImportError:
+            pass
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_stride_tiles: int,
+                 bytes_per_pixel: int, stream=None) -> None:
+    check(load().bh_tiles_unpack(_ptr(packed), _ptr(out), width, height, shard_count, shard_stride_tiles,
+                                 bytes_per_pixel, _stream_handle(stream)), "bh_tiles_unpack")
+
+
+__all__ = ["Camera", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+           "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
+           "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -1,0 +1,185 @@
+/*
+ * bh_render.h — C ABI of the MI355X-native geodesic ray-marcher.
+ *
+ * This is the drop-in boundary for ONE hot path of jonathandw743/black_hole_ray_marching:
+ * the per-pixel Schwarzschild photon integrator `fs_main -> get_col`
+ * (src/black_hole_maybe.wgsl:259-370), which the reference drives through
+ * `Scene::render(encoder, output_view, blackout_output_view)` (src/scene.rs:470-522).
+ *
+ * Mapping of reference interfaces onto entry points (all paths relative to the reference repo):
+ *
+ *   bh_camera_uniform          == WGSL `Camera` (src/black_hole_maybe.wgsl:9-17), packed by
+ *                                 `CameraUniform` (src/uniforms.rs:98-106) with encase: 112 B.
+ *   bh_uniforms                == WGSL `Uniforms` (src/black_hole_maybe.wgsl:58-69), packed by
+ *                                 `OtherUniforms::uniform_buffer_content` (src/otheruniforms.rs:105-118): 32 B.
+ *   bh_camera                  == `Camera` (src/camera.rs:11-20).
+ *   bh_uniforms_default        == the six `OtherUniform` defaults of `Scene::new` (src/scene.rs:89-137),
+ *                                 including the inverted PodBool (src/podbool.rs:21-26) => blackout_eh = 1.
+ *   bh_camera_default          == the camera literal of `Scene::new` (src/scene.rs:68-76).
+ *   bh_camera_uniform_update   == `CameraUniform::update` (src/uniforms.rs:123-133) ->
+ *                                 `Camera::pos_to_world_space_screen_triangle` (src/camera.rs:89-112).
+ *   bh_create                  == the sky-texture half of `Scene::new`: `Texture::from_bytes` /
+ *                                 `from_image` (src/texture.rs:11-77, Rgba8UnormSrgb, clamp, mag Linear)
+ *                                 as bound at src/scene.rs:186-232.
+ *   bh_render                  == `Scene::render` (src/scene.rs:470-522): one full-screen pass writing
+ *                                 `col` (target 0) and optionally `blackout_col` (target 1; NULL == None).
+ *   bh_destroy                 == dropping the `Scene`'s GPU resources.
+ *
+ * Conventions: every function returns BH_OK (0) or a negative bh_status; nothing aborts or throws
+ * across the ABI.  Output pointers are caller-owned DEVICE pointers (the reference's consumer, Bloom,
+ * owns its textures and lends views: src/bloom.rs:31-37).  bh_render is asynchronous on the given
+ * HIP stream (NULL = the legacy default stream) and performs no allocation or synchronisation, so a
+ * caller may capture it into a hipGraph.  One bh_ctx per device; a ctx is not thread-safe, distinct
+ * ctx objects may be used from distinct threads (one per rank).
+ */
+#ifndef BH_RENDER_H
+#define BH_RENDER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BH_ABI_VERSION 1
+
+typedef enum {
+    BH_OK = 0,
+    BH_ERR_INVALID_ARG = -1,   /* NULL/zero/out-of-range argument */
+    BH_ERR_UNSUPPORTED = -2,   /* valid for the reference but not implemented (e.g. non-default screen triangle) */
+    BH_ERR_HIP = -3,           /* a HIP runtime call failed; see bh_last_error() */
+    BH_ERR_NO_DEVICE = -4,     /* no HIP device / device index out of range */
+    BH_ERR_OUT_OF_MEMORY = -5
+} bh_status;
+
+/* WGSL `Camera` (src/black_hole_maybe.wgsl:9-17), std140/encase layout, 112 bytes:
+ *   pos @0 (vec3, padded to 16), screen_space_screen_triangle @16 (3 x vec4),
+ *   pos_to_world_space_screen_triangle @64 (3 x vec4). */
+typedef struct {
+    float pos[3];
+    float _pad0;
+    float screen_tri[3][4];
+    float world_tri[3][4];
+} bh_camera_uniform;
+
+/* WGSL `Uniforms` (src/black_hole_maybe.wgsl:58-69), 32 bytes.
+ * bg_brightness is carried for layout fidelity but unused by the shader (as in the reference). */
+typedef struct {
+    float rs;               /* RS: Schwarzschild radius (default 1.0) */
+    float delta_time_mult;  /* DELTA_TIME_MULT (default 0.5) */
+    float bg_brightness;    /* BG_BRIGHTNESS (default 0.5, unused) */
+    uint32_t blackout_eh;   /* BLACKOUT_EH: != 0 enables event-horizon blackout (default 1) */
+    float max_dist;         /* MAX_DIST (default 250.0) */
+    float distortion_power; /* DISTORTION_POWER (default 1.0) */
+    uint32_t _pad[2];
+} bh_uniforms;
+
+/* `Camera` (src/camera.rs:11-20). */
+typedef struct {
+    float pos[3];
+    float dir[3];
+    float up[3];
+    float aspect;
+    float fovy;
+    float znear;
+    float zfar;
+} bh_camera;
+
+/* Output texel formats.  The reference stores into Bgra8UnormSrgb surfaces (src/copy.rs:132,
+ * src/remix.rs:160); RGBA32F is the parity format, RGBA16F the production format. */
+typedef enum {
+    BH_OUT_RGBA32F = 0,     /* 16 B / pixel, linear */
+    BH_OUT_RGBA16F = 1,     /*  8 B / pixel, linear, round-to-nearest-even from the fp32 result */
+    BH_OUT_BGRA8_SRGB = 2   /*  4 B / pixel, sRGB-encoded, clamped, byte order B,G,R,A */
+} bh_out_format;
+
+/* Arithmetic mode of the integrator (see DESIGN.md "Math modes"). */
+typedef enum {
+    BH_MATH_EXACT = 0,      /* IEEE div/sqrt, no contraction, same op order as the oracle: bit-exact parity */
+    BH_MATH_FAST = 1        /* rsq/rcp/FMA reformulation: production speed, tolerance parity */
+} bh_math_mode;
+
+/* Scene contents (bit mask).  The reference always has both (src/black_hole_maybe.wgsl:119-123);
+ * 0 removes every surface (sdf == +inf), BASELINE config 1. */
+#define BH_SCENE_DISC    1u
+#define BH_SCENE_MARKERS 2u
+#define BH_SCENE_DEFAULT (BH_SCENE_DISC | BH_SCENE_MARKERS)
+
+/* Output layout. */
+typedef enum {
+    BH_LAYOUT_ROWMAJOR = 0, /* out[y * width + x]; requires shard_count == 1 */
+    BH_LAYOUT_TILES = 1     /* the shard's 8x8 tiles packed in shard order, 64 pixels per tile,
+                               pixel (x & 7) + 8 * (y & 7) inside a tile; pixels outside the frame
+                               are left untouched */
+} bh_layout;
+
+/* Per-pixel fate codes written to dbg_fate. */
+#define BH_FATE_CAP      0u  /* loop ran out (max_iters); still shades sky with its current rd */
+#define BH_FATE_ESCAPE   1u  /* distance_travelled > MAX_DIST (src/black_hole_maybe.wgsl:325-327) */
+#define BH_FATE_SURFACE  2u  /* sdf < MIN_DIST (:286-288) -> colour 1 */
+#define BH_FATE_BLACKOUT 3u  /* event-horizon blackout (:272-283) -> colour 0 */
+
+#define BH_TILE 8u           /* tile edge in pixels (multi-GPU sharding and BH_LAYOUT_TILES) */
+
+typedef struct {
+    uint32_t width, height;   /* frame size in pixels */
+    uint32_t max_iters;       /* MAX_ITERATIONS (WGSL const 1000, src/black_hole_maybe.wgsl:85), 1..65535 */
+    uint32_t scene_flags;     /* BH_SCENE_* */
+    uint32_t format;          /* bh_out_format */
+    uint32_t math;            /* bh_math_mode */
+    uint32_t layout;          /* bh_layout */
+    uint32_t shard_index;     /* this rank's tile share: tile (tx,ty) belongs to shard (tx + 3*ty) % shard_count */
+    uint32_t shard_count;     /* 1 = whole frame */
+    uint32_t _reserved;
+    void* out_col;            /* target 0 (`col`), device pointer, never NULL */
+    void* out_blackout;       /* target 1 (`blackout_col`), device pointer or NULL (== Option::None) */
+    uint16_t* dbg_n_rk;       /* optional: completed RK4 steps per pixel (same layout as outputs, 1 elem/px) */
+    uint8_t* dbg_fate;        /* optional: BH_FATE_* per pixel */
+} bh_render_desc;
+
+typedef struct bh_ctx bh_ctx;
+
+int bh_abi_version(void);
+const char* bh_status_string(int status);
+/* Thread-local text of the last HIP error seen by this library ("" if none). */
+const char* bh_last_error(void);
+
+/* Defaults of Scene::new (src/scene.rs:68-137). */
+int bh_uniforms_default(bh_uniforms* out);
+int bh_camera_default(uint32_t width, uint32_t height, bh_camera* out);
+/* CameraUniform::new (src/uniforms.rs:108-122) + ::update (:123-133). */
+int bh_camera_uniform_update(const bh_camera* camera, bh_camera_uniform* out);
+/* Camera aimed at `target` from `pos` (up +Y, fovy pi/2): SURVEY §8d cameras B and C. */
+int bh_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
+                      bh_camera* out);
+
+/* Deterministic synthetic equirectangular sky (RGBA8, sRGB-encoded, alpha 255):
+ * splitmix64-seeded value-noise nebula + sparse stars.  Stand-in for src/space_4096x2048.jpg. */
+int bh_synthetic_sky(uint8_t* out_rgba8, uint32_t width, uint32_t height, uint64_t seed);
+
+/* Upload the sky (width*height*4 bytes, Rgba8UnormSrgb semantics) to `device` and build the
+ * sRGB->linear table.  The context owns the device copy. */
+int bh_create(const uint8_t* sky_rgba8_srgb, uint32_t sky_width, uint32_t sky_height, int device,
+              bh_ctx** out);
+int bh_destroy(bh_ctx* ctx);
+
+/* Scene::render.  Asynchronous on `hip_stream` (a hipStream_t, NULL = default stream). */
+int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* uniforms,
+              const bh_render_desc* desc, void* hip_stream);
+
+/* Number of 8x8 tiles owned by `shard_index` of `shard_count` in a width x height frame. */
+int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);
+
+/* Scatter the gathered tile-packed shards back into a row-major frame (rank 0 after the gather).
+ * `packed` holds shard 0's tiles, then shard 1's, ... (the concatenation a gather produces, each
+ * shard's block padded to `shard_stride_tiles` tiles); `bytes_per_pixel` is 4, 8 or 16. */
+int bh_tiles_unpack(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
+                    uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t bytes_per_pixel,
+                    void* hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BH_RENDER_H */

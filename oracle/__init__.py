@@ -1,0 +1,78 @@
+"""ctypes wrapper of the CPU oracle (oracle/libbh_oracle.so).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package, and
+only as the checker / the timed CPU baseline.  PARITY UNPINNED: see oracle/bh_oracle.c header.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libbh_oracle.so"
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} missing: run `python -m black_hole_ray_marching_amd.build`")
+        lib = C.CDLL(str(LIB_PATH))
+        lib.bho_render_rows.restype = C.c_int
+        lib.bho_render_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        lib.bho_trace_ray.restype = C.c_int
+        lib.bho_trace_ray.argtypes = [C.c_float * 3, C.c_float * 3, C.c_void_p, C.c_void_p, C.c_uint32,
+                                      C.c_uint32, C.c_uint32, C.c_uint32, C.c_float * 3,
+                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        lib.bho_srgb_lut.restype = None
+        lib.bho_srgb_lut.argtypes = [C.c_void_p]
+        lib.bho_srgb_encode.restype = C.c_uint8
+        lib.bho_srgb_encode.argtypes = [C.c_float]
+        _lib = lib
+    return _lib
+
+
+def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: int, height: int,
+                max_iters: int, scene_flags: int, row0: int = 0, row1: int | None = None,
+                threads: int = 0, blackout: bool = True):
+    """Oracle render of rows [row0, row1).  camera_uniform/uniforms: the 112-/32-byte ABI structs.
+
+    Returns (col (R,W,4) f32, blackout (R,W,4) f32 or None, n_rk (R,W) u16, fate (R,W) u8).
+    """
+    lib = load()
+    row1 = height if row1 is None else row1
+    rows = row1 - row0
+    sky = np.ascontiguousarray(sky, dtype=np.uint8)
+    col = np.empty((rows, width, 4), np.float32)
+    bo = np.empty((rows, width, 4), np.float32) if blackout else None
+    n_rk = np.empty((rows, width), np.uint16)
+    fate = np.empty((rows, width), np.uint8)
+    cam = C.create_string_buffer(bytes(camera_uniform), 112)
+    uni = C.create_string_buffer(bytes(uniforms), 32)
+    st = lib.bho_render_rows(cam, uni, sky.ctypes.data, sky.shape[1], sky.shape[0], width, height, max_iters,
+                             scene_flags, row0, row1, col.ctypes.data, bo.ctypes.data if bo is not None else None,
+                             n_rk.ctypes.data, fate.ctypes.data, threads)
+    if st != 0:
+        raise ValueError(f"bho_render_rows failed: {st}")
+    return col, bo, n_rk, fate
+
+
+def trace_ray(ro0, rd0, uniforms: bytes, sky: np.ndarray, max_iters: int, scene_flags: int):
+    lib = load()
+    sky = np.ascontiguousarray(sky, dtype=np.uint8)
+    out = (C.c_float * 3)()
+    n, f = C.c_uint32(), C.c_uint32()
+    uni = C.create_string_buffer(bytes(uniforms), 32)
+    lib.bho_trace_ray((C.c_float * 3)(*ro0), (C.c_float * 3)(*rd0), uni, sky.ctypes.data, sky.shape[1],
+                      sky.shape[0], max_iters, scene_flags, out, C.byref(n), C.byref(f))
+    return np.array(out, np.float32), int(n.value), int(f.value)
+
+
+def srgb_lut() -> np.ndarray:
+    out = np.empty(256, np.float32)
+    load().bho_srgb_lut(out.ctypes.data)
+    return out
