@@ -45,8 +45,9 @@ __device__ __forceinline__ v3 normalize(v3 a) { return muls(a, rsq(dot(a, a))); 
 __device__ __forceinline__ float len(v3 a) { return __builtin_sqrtf(dot(a, a)); }  // correctly rounded
 __device__ __forceinline__ v3 divs(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
 __device__ __forceinline__ v3 normalize(v3 a) { return divs(a, len(a)); }
-__device__ __forceinline__ float pow25(float q) { double d = (double)q; return (float)(d * d * __builtin_sqrt(d)); }
-__device__ __forceinline__ float pow15(float c) { double d = (double)c; return (float)(d * __builtin_sqrt(d)); }
+// normative pow forms (oracle/bh_oracle.c header): three correctly rounded f32 ops each
+__device__ __forceinline__ float pow25(float q) { return (q * q) * __builtin_sqrtf(q); }
+__device__ __forceinline__ float pow15(float c) { return c * __builtin_sqrtf(c); }
 #endif
 
 constexpr float MIN_DIST = 0.001f;        // :80
@@ -69,12 +70,16 @@ __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
         float q = fminf(p.x * p.x + ay * ay, ax * ax + p.y * p.y) + dz * dz;
         float m = __builtin_sqrtf(q) - 0.5f;
 #else
-        // sdf_sphere = length(centre - p) - r, evaluated exactly as written
-        float s1 = len(sub(mk(0.0f, 10.0f, -10.0f), p)) - 0.5f;
-        float s2 = len(sub(mk(0.0f, -10.0f, -10.0f), p)) - 0.5f;
-        float s3 = len(sub(mk(10.0f, 0.0f, -10.0f), p)) - 0.5f;
-        float s4 = len(sub(mk(-10.0f, 0.0f, -10.0f), p)) - 0.5f;
-        float m = fminf(s1, fminf(s2, fminf(s3, s4)));
+        // sdf_sphere = length(centre - p) - r for the four spheres, each squared length evaluated
+        // exactly as written ((dx*dx + dy*dy) + dz*dz with dx = cx - px, ...).  Shared terms are
+        // computed once (identical roundings) and min(sqrt(qi) - 0.5) == sqrt(min(qi)) - 0.5
+        // exactly, because correctly rounded sqrt and x - 0.5 are monotone: one sqrt, bit-exact.
+        const float xx = p.x * p.x, yy = p.y * p.y;          // (0 - p)^2 == p^2
+        const float dz = -10.0f - p.z, zz = dz * dz;
+        const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
+        const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
+        const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
+        float m = __builtin_sqrtf(fminf(q1, fminf(q2, fminf(q3, q4)))) - 0.5f;
 #endif
         d = (flags & BH_SCENE_DISC) ? fminf(d, m) : m;
     }

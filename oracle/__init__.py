@@ -23,7 +23,8 @@ def load() -> C.CDLL:
         lib.bho_render_rows.restype = C.c_int
         lib.bho_render_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
-                                        C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+                                        C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_int]
         lib.bho_trace_ray.restype = C.c_int
         lib.bho_trace_ray.argtypes = [C.c_float * 3, C.c_float * 3, C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_float * 3,
@@ -38,14 +39,15 @@ def load() -> C.CDLL:
 
 def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: int, height: int,
                 max_iters: int, scene_flags: int, row0: int = 0, row1: int | None = None,
-                threads: int = 0, blackout: bool = True):
-    """Oracle render of rows [row0, row1).  camera_uniform/uniforms: the 112-/32-byte ABI structs.
+                threads: int = 0, blackout: bool = True, row_step: int = 1):
+    """Oracle render of rows row0, row0+row_step, ... < row1.  camera_uniform/uniforms: the
+    112-/32-byte ABI structs.
 
     Returns (col (R,W,4) f32, blackout (R,W,4) f32 or None, n_rk (R,W) u16, fate (R,W) u8).
     """
     lib = load()
     row1 = height if row1 is None else row1
-    rows = row1 - row0
+    rows = (row1 - row0 + row_step - 1) // row_step
     sky = np.ascontiguousarray(sky, dtype=np.uint8)
     col = np.empty((rows, width, 4), np.float32)
     bo = np.empty((rows, width, 4), np.float32) if blackout else None
@@ -54,7 +56,7 @@ def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: 
     cam = C.create_string_buffer(bytes(camera_uniform), 112)
     uni = C.create_string_buffer(bytes(uniforms), 32)
     st = lib.bho_render_rows(cam, uni, sky.ctypes.data, sky.shape[1], sky.shape[0], width, height, max_iters,
-                             scene_flags, row0, row1, col.ctypes.data, bo.ctypes.data if bo is not None else None,
+                             scene_flags, row0, row1, row_step, col.ctypes.data, bo.ctypes.data if bo is not None else None,
                              n_rk.ctypes.data, fate.ctypes.data, threads)
     if st != 0:
         raise ValueError(f"bho_render_rows failed: {st}")

@@ -15,8 +15,8 @@
  *   - f32 + - * / sqrt are IEEE-754 correctly rounded, evaluated in WGSL source order, no FMA
  *     contraction (build with -ffp-contract=off, no -ffast-math);
  *   - length(v) = sqrt(dot(v,v)), dot = (x*x + y*y) + z*z, normalize(v) = v / length(v);
- *   - pow(q, 2.5) = (float)((double)q * (double)q * sqrt((double)q))  (q^2 exact in double);
- *   - pow(c, 1.5) = (float)((double)c * sqrt((double)c));
+ *   - pow(q, 2.5) = (q * q) * sqrt(q)   (f32, three correctly rounded ops; <= 1.5 ulp of q^2.5);
+ *   - pow(c, 1.5) = c * sqrt(c)         (f32);
  *   - atan2(y, x) = (float)atan2((double)y, (double)x);
  *   - textureSampleLevel on Rgba8UnormSrgb with a mag=Linear, clamp-to-edge sampler = decode each
  *     texel through the 256-entry sRGB->linear table, then bilinear with fp32 weights
@@ -47,14 +47,8 @@ static inline v3 normalize(v3 a) { return divs(a, len(a)); }
 static inline v3 cross(v3 a, v3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-static inline float pow25(float q) {
-    double d = (double)q;
-    return (float)(d * d * sqrt(d));
-}
-static inline float pow15(float c) {
-    double d = (double)c;
-    return (float)(d * sqrt(d));
-}
+static inline float pow25(float q) { return (q * q) * sqrtf(q); }
+static inline float pow15(float c) { return c * sqrtf(c); }
 
 /* constants, src/black_hole_maybe.wgsl:80-85 (abstract floats rounded to f32 at use) */
 #define MIN_DIST 0.001f
@@ -236,15 +230,17 @@ int bho_screen_tri_is_default(const bh_camera_uniform* cam) {
 }
 
 /*
- * Render rows [row0, row1) of a width x height frame.  Outputs are row-major over the band:
- * out_col / out_blackout: (row1-row0)*width*4 floats (RGBA, alpha = 1; blackout may be NULL);
+ * Render rows row0, row0 + row_step, ... (< row1) of a width x height frame (row_step 0 == 1).
+ * Outputs are row-major over the rendered rows, nrows = ceil((row1-row0)/row_step):
+ * out_col / out_blackout: nrows*width*4 floats (RGBA, alpha = 1; blackout may be NULL);
  * n_rk (u16) / fate (u8): one per pixel, may be NULL.  threads <= 0: OpenMP default.
  * Returns 0, or -1 on invalid arguments.
  */
 int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
                     uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
                     uint32_t max_iters, uint32_t scene_flags, uint32_t row0, uint32_t row1,
-                    float* out_col, float* out_blackout, uint16_t* n_rk, uint8_t* fate, int threads) {
+                    uint32_t row_step, float* out_col, float* out_blackout, uint16_t* n_rk, uint8_t* fate,
+                    int threads) {
     if (!cam || !U || !sky || !out_col || sky_w == 0 || sky_h == 0 || width == 0 || height == 0 ||
         row0 > row1 || row1 > height || max_iters == 0 || max_iters > 65535u)
         return -1;
@@ -256,7 +252,8 @@ int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     S.tex = sky; S.w = sky_w; S.h = sky_h;
     bho_srgb_lut(S.lut);
     v3 ro0 = mk(cam->pos[0], cam->pos[1], cam->pos[2]);
-    long nrows = (long)row1 - (long)row0;
+    if (row_step == 0) row_step = 1;
+    long nrows = ((long)row1 - (long)row0 + (long)row_step - 1) / (long)row_step;
 #ifdef _OPENMP
     if (threads > 0) omp_set_num_threads(threads);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -264,7 +261,7 @@ int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     (void)threads;
 #endif
     for (long rr = 0; rr < nrows; rr++) {
-        uint32_t py = row0 + (uint32_t)rr;
+        uint32_t py = row0 + (uint32_t)rr * row_step;
         for (uint32_t px = 0; px < width; px++) {
             size_t o = (size_t)rr * width + px;
             v3 rd0 = normalize(pixel_dir(cam, width, height, px, py)); /* :362 */

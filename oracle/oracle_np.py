@@ -30,14 +30,12 @@ def _len(x, y, z):
     return np.sqrt(_dot(x, y, z, x, y, z))
 
 
-def _pow25(q):
-    d = q.astype(np.float64)
-    return (d * d * np.sqrt(d)).astype(f32)
+def _pow25(q):  # pow(q, 2.5) := (q*q)*sqrt(q) in f32 (normative)
+    return (q * q) * np.sqrt(q)
 
 
-def _pow15(c):
-    d = c.astype(np.float64)
-    return (d * np.sqrt(d)).astype(f32)
+def _pow15(c):  # pow(c, 1.5) := c*sqrt(c) in f32
+    return c * np.sqrt(c)
 
 
 def srgb_lut():
