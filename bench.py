@@ -44,6 +44,7 @@ def parse():
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--max-iters", type=int, default=512)
     p.add_argument("--camera", choices=["A", "B", "C"], default="A")
+    p.add_argument("--schedule", choices=["persistent", "tile"], default="persistent")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores in this process's affinity")
     return p.parse_args()
@@ -89,6 +90,12 @@ def main() -> None:
         scene.update(bh.Camera.look_at(spec[0], spec[1], W, H))
     dev = torch.device("cuda", local)
     stream = torch.cuda.current_stream(dev)
+    sched = bh.BH_SCHED_PERSISTENT if args.schedule == "persistent" else bh.BH_SCHED_TILE
+    _render = scene.render
+
+    def render(*a, **kw):
+        return _render(*a, schedule=sched, **kw)
+    scene.render = render
 
     if n == 1:
         col = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
@@ -152,7 +159,7 @@ def main() -> None:
     kern_avg_s = float(np.mean(kern_ms)) / 1e3
 
     # algorithmic work of one launch: sum of completed RK steps over this rank's pixels (deterministic)
-    nrk_buf = torch.empty(col.shape[:-1], dtype=torch.int16, device=dev)
+    nrk_buf = torch.zeros(col.shape[:-1], dtype=torch.int16, device=dev)
     if n == 1:
         scene.render(col, bo, fmt=fmt, stream=stream, dbg_n_rk=nrk_buf)
     else:

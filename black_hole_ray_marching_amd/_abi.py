@@ -19,6 +19,7 @@ BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
 BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES = 0, 1
+BH_SCHED_PERSISTENT, BH_SCHED_TILE = 0, 1
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 
@@ -45,7 +46,7 @@ class bh_render_desc(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("max_iters", C.c_uint32),
                 ("scene_flags", C.c_uint32), ("format", C.c_uint32), ("math", C.c_uint32),
                 ("layout", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
-                ("_reserved", C.c_uint32), ("out_col", C.c_void_p), ("out_blackout", C.c_void_p),
+                ("schedule", C.c_uint32), ("out_col", C.c_void_p), ("out_blackout", C.c_void_p),
                 ("dbg_n_rk", C.c_void_p), ("dbg_fate", C.c_void_p)]
 
 

@@ -75,8 +75,14 @@ __host__ __device__ inline void shard_tile_coords(uint32_t t, uint32_t tiles_x, 
 }  // namespace bh
 
 // Launchers (defined in the .hip translation units).
-extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, hipStream_t s);
-extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_fast(const bh::MarchArgs& a, hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
+                                                                         uint32_t* counters, uint32_t grid,
+                                                                         hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_fast(const bh::MarchArgs& a, uint32_t schedule,
+                                                                        uint32_t* counters, uint32_t grid,
+                                                                        hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exact(void);
+extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_fast(void);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
                                       uint32_t shard_count, uint64_t shard_stride_tiles,
                                       uint32_t bytes_per_pixel, hipStream_t s);

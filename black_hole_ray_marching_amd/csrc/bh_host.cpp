@@ -15,9 +15,11 @@
 
 struct bh_ctx {
     int device = 0;
-    uint32_t* sky = nullptr;   // device RGBA8 texels
-    float* lut = nullptr;      // device sRGB->linear table (256 floats)
+    uint32_t* sky = nullptr;       // device RGBA8 texels
+    float* lut = nullptr;          // device sRGB->linear table (256 floats)
+    uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
+    uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
 };
 
 namespace {
@@ -252,6 +254,16 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     else if ((e = hipMalloc(&c->lut, sizeof(lut))) != hipSuccess) st = hip_fail(e, "hipMalloc(lut)");
     else if ((e = hipMemcpy(c->sky, sky, bytes, hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(sky)");
     else if ((e = hipMemcpy(c->lut, lut, sizeof(lut), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(lut)");
+    else if ((e = hipMalloc(&c->counters, 1024)) != hipSuccess) st = hip_fail(e, "hipMalloc(counters)");
+    if (st == BH_OK) {
+        int cus = 0;
+        if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess || cus <= 0) {
+            st = hip_fail(e, "hipDeviceGetAttribute(CU count)");
+        } else {
+            c->grid_exact = (uint32_t)(cus * bh_march_blocks_per_cu_exact());
+            c->grid_fast = (uint32_t)(cus * bh_march_blocks_per_cu_fast());
+        }
+    }
     (void)hipSetDevice(prev);
     if (st != BH_OK) { bh_destroy(c); return st; }
     *out = c;
@@ -265,6 +277,7 @@ int bh_destroy(bh_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->sky) (void)hipFree(c->sky);
     if (c->lut) (void)hipFree(c->lut);
+    if (c->counters) (void)hipFree(c->counters);
     (void)hipSetDevice(prev);
     delete c;
     return BH_OK;
@@ -281,6 +294,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
     if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES) return BH_ERR_INVALID_ARG;
+    if (d->schedule > BH_SCHED_TILE) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
@@ -313,7 +327,8 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     (void)hipGetDevice(&prev);
     if (prev != c->device) (void)hipSetDevice(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, s) : bh_launch_march_fast(a, s);
+    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, d->schedule, c->counters, c->grid_exact, s)
+                                     : bh_launch_march_fast(a, d->schedule, c->counters, c->grid_fast, s);
     if (prev != c->device) (void)hipSetDevice(prev);
     if (e != 0) return hip_fail((hipError_t)e, "march kernel launch");
     return BH_OK;

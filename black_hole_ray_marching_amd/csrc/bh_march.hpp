@@ -136,57 +136,94 @@ __device__ __forceinline__ v3 sample_sky(const MarchArgs& a, const float* lut, f
     return add(muls(top, ib), muls(bot, fb));
 }
 
-// get_col (:259-345)
-__device__ __forceinline__ Ray get_col(const MarchArgs& a, const float* lut, v3 ro0, v3 rd0) {
-    v3 ro = ro0, rd = rd0;
-    v3 c = cross(ro, rd);                                   // :262
-    const float h2 = dot(c, c);                             // :263
-    const float s = ((a.dp * a.rs) * -1.5f) * h2;           // :126 scalar chain, loop-invariant
-    const v3 nro0 = normalize(ro0);
-    const v3 cps = muls(muls(mk(-nro0.x, -nro0.y, -nro0.z), 1.5f), a.rs);  // :294
-    float travelled = 0.0f;                                 // :264
-    bool outside = false;                                   // :265
-    Ray out;
-    out.fate = BH_FATE_CAP;
-    uint32_t i = 0;
-    for (; i < a.max_iters; ++i) {                          // :266
-        const float r = len(ro);                            // :271
-        if (a.blackout_eh != 0u) {                          // :272-283
-            if (r < 1.0f && dot(rd, ro) < 0.0f) { out.fate = BH_FATE_BLACKOUT; break; }
-            if (r > 1.0f) outside = true;
-            else if (outside) { out.fate = BH_FATE_BLACKOUT; break; }
-        }
-        const float ds = sdf(ro, a.rs, a.scene_flags);      // :285
-        if (ds < MIN_DIST) { out.fate = BH_FATE_SURFACE; break; }  // :286-288
-        const float dps = len(sub(cps, ro)) - 0.075f;       // :294
-        const float dist = fminf(ds, dps);                  // :299
-        const float dd = fminf(dist * 0.9f, a.dtm * r);     // :307-310
-        // get_delta_photon_rk4 (:134-151)
-        const float dt = dd;
-        v3 ro_k1 = smul(dt, rd);
-        v3 rd_k1 = smul(dt, accel(ro, s));
-        v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
-        v3 rd_k2 = smul(dt, accel(add(ro, smul(0.5f, ro_k1)), s));
-        v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
-        v3 rd_k3 = smul(dt, accel(add(ro, smul(0.5f, ro_k2)), s));
-        v3 ro_k4 = smul(dt, add(rd, rd_k3));
-        v3 rd_k4 = smul(dt, accel(add(ro, ro_k3), s));
-#if BH_FAST
-        constexpr float SIXTH = 1.0f / 6.0f;
-        v3 dro = muls(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), SIXTH);
-        v3 drd = muls(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), SIXTH);
-#else
-        v3 dro = divs(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), 6.0f);
-        v3 drd = divs(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), 6.0f);
-#endif
-        ro = add(ro, dro);                                  // :315
-        rd = add(rd, drd);                                  // :322
-        travelled += dd;                                    // :324
-        if (travelled > a.max_dist) { ++i; out.fate = BH_FATE_ESCAPE; break; }  // :325-327
+// ---- per-ray pieces of get_col (:259-345) -------------------------------------------------------
+
+// Per-frame invariants (identical for every pixel: ro0 == camera.pos, :363).
+struct Frame {
+    v3 ro0;
+    v3 cps;      // photon-sphere centre -normalize(ro0) * 1.5 * RS  (:294)
+    float k;     // (DP * RS) * -1.5: the scalar prefix of rd_derivative (:126)
+};
+__device__ __forceinline__ Frame make_frame(const MarchArgs& a) {
+    Frame f;
+    f.ro0 = mk(a.pos[0], a.pos[1], a.pos[2]);
+    const v3 n = normalize(f.ro0);
+    f.cps = muls(muls(mk(-n.x, -n.y, -n.z), 1.5f), a.rs);
+    f.k = (a.dp * a.rs) * -1.5f;
+    return f;
+}
+
+// vs_main + rasteriser interpolation + fs_main :362 for pixel (px, py): the world-space corner rays of
+// the screen triangle (3,1),(-1,1),(-1,-3) interpolated at the pixel centre, normalised.
+__device__ __forceinline__ v3 pixel_ray(const MarchArgs& a, uint32_t px, uint32_t py) {
+    const float l0 = ((float)px + 0.5f) / (2.0f * (float)a.width);
+    const float l2 = ((float)py + 0.5f) / (2.0f * (float)a.height);
+    const float l1 = (1.0f - l0) - l2;
+    const v3 d = add(add(smul(l0, mk(a.c0[0], a.c0[1], a.c0[2])), smul(l1, mk(a.c1[0], a.c1[1], a.c1[2]))),
+                     smul(l2, mk(a.c2[0], a.c2[1], a.c2[2])));
+    return normalize(d);
+}
+
+// s = ((DP*RS)*-1.5) * h2 with h2 = |ro0 x rd0|^2 (:262-263), hoisted out of rd_derivative.
+__device__ __forceinline__ float ray_s(const Frame& f, v3 rd0) {
+    const v3 c = cross(f.ro0, rd0);
+    return f.k * dot(c, c);
+}
+
+struct RayState {
+    v3 ro, rd;
+    float travelled;
+    float s;
+    uint32_t n_rk;
+    bool outside;
+};
+
+// One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
+// iteration (n_rk counts completed RK updates), or 0xFF if it continues.
+__device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
+    v3 ro = st.ro, rd = st.rd;
+    const float r = len(ro);                            // :271
+    if (a.blackout_eh != 0u) {                          // :272-283
+        if (r < 1.0f && dot(rd, ro) < 0.0f) return BH_FATE_BLACKOUT;
+        if (r > 1.0f) st.outside = true;
+        else if (st.outside) return BH_FATE_BLACKOUT;
     }
-    out.n_rk = i;
-    if (out.fate == BH_FATE_BLACKOUT) { out.col = mk(0.0f, 0.0f, 0.0f); return out; }
-    if (out.fate == BH_FATE_SURFACE) { out.col = mk(1.0f, 1.0f, 1.0f); return out; }
+    const float ds = sdf(ro, a.rs, a.scene_flags);      // :285
+    if (ds < MIN_DIST) return BH_FATE_SURFACE;          // :286-288
+    const float dps = len(sub(f.cps, ro)) - 0.075f;     // :294
+    const float dist = fminf(ds, dps);                  // :299
+    const float dt = fminf(dist * 0.9f, a.dtm * r);     // :307-310
+    const float s = st.s;
+    // get_delta_photon_rk4 (:134-151)
+    v3 ro_k1 = smul(dt, rd);
+    v3 rd_k1 = smul(dt, accel(ro, s));
+    v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
+    v3 rd_k2 = smul(dt, accel(add(ro, smul(0.5f, ro_k1)), s));
+    v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
+    v3 rd_k3 = smul(dt, accel(add(ro, smul(0.5f, ro_k2)), s));
+    v3 ro_k4 = smul(dt, add(rd, rd_k3));
+    v3 rd_k4 = smul(dt, accel(add(ro, ro_k3), s));
+#if BH_FAST
+    constexpr float SIXTH = 1.0f / 6.0f;
+    v3 dro = muls(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), SIXTH);
+    v3 drd = muls(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), SIXTH);
+#else
+    v3 dro = divs(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), 6.0f);
+    v3 drd = divs(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), 6.0f);
+#endif
+    st.ro = add(ro, dro);                               // :315
+    st.rd = add(rd, drd);                               // :322
+    st.travelled += dt;                                 // :324
+    st.n_rk += 1u;
+    if (st.travelled > a.max_dist) return BH_FATE_ESCAPE;  // :325-327
+    if (st.n_rk >= a.max_iters) return BH_FATE_CAP;        // loop exhausted (:266)
+    return 0xFFu;
+}
+
+// Colour of a finished ray (:329-345 for sky rays; :275/:281 blackout -> 0; :287 surface -> 1).
+__device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32_t fate, v3 rd) {
+    if (fate == BH_FATE_BLACKOUT) return mk(0.0f, 0.0f, 0.0f);
+    if (fate == BH_FATE_SURFACE) return mk(1.0f, 1.0f, 1.0f);
     const v3 n = normalize(rd);                             // :330
 #if BH_FAST
     const float az = atan2f(n.z, n.x);                      // :332
@@ -203,8 +240,7 @@ __device__ __forceinline__ Ray get_col(const MarchArgs& a, const float* lut, v3 
     col.y = pow15(col.y);
     col.z = pow15(col.z);
 #endif
-    out.col = col;
-    return out;
+    return col;
 }
 
 __device__ __forceinline__ void store_px(void* base, uint32_t fmt, size_t idx, v3 c) {
@@ -220,8 +256,23 @@ __device__ __forceinline__ void store_px(void* base, uint32_t fmt, size_t idx, v
     }
 }
 
-// One wave64 = one 8x8 tile; 4 waves (4 tiles) per 256-thread workgroup.
-__global__ void __launch_bounds__(256) march_kernel(MarchArgs a) {
+// fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
+__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate) {
+    store_px(a.out_col, a.format, idx, col);
+    if (a.out_blackout) {
+        const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
+        store_px(a.out_blackout, a.format, idx, bo);
+    }
+    if (a.dbg_n_rk) a.dbg_n_rk[idx] = (uint16_t)n_rk;
+    if (a.dbg_fate) a.dbg_fate[idx] = (uint8_t)fate;
+}
+
+__device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
+    return (a.layout == BH_LAYOUT_TILES) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
+}
+
+// ---- schedule 1: one wave64 = one 8x8 tile (simple reference schedule) ---------------------------
+__global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     __shared__ float lut[256];
     lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
     __syncthreads();
@@ -232,24 +283,145 @@ __global__ void __launch_bounds__(256) march_kernel(MarchArgs a) {
     shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
     const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
     if (px >= a.width || py >= a.height) return;
+    const Frame f = make_frame(a);
+    RayState st;
+    st.ro = f.ro0;
+    st.rd = pixel_ray(a, px, py);
+    st.s = ray_s(f, st.rd);
+    st.travelled = 0.0f;
+    st.n_rk = 0;
+    st.outside = false;
+    uint32_t fate = 0xFFu;
+    while ((fate = march_step(a, f, st)) == 0xFFu) {}
+    write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate);
+}
 
-    // vs_main + rasteriser interpolation + fs_main :362 (screen triangle (3,1),(-1,1),(-1,-3))
-    const float l0 = ((float)px + 0.5f) / (2.0f * (float)a.width);
-    const float l2 = ((float)py + 0.5f) / (2.0f * (float)a.height);
-    const float l1 = (1.0f - l0) - l2;
-    const v3 d = add(add(smul(l0, mk(a.c0[0], a.c0[1], a.c0[2])), smul(l1, mk(a.c1[0], a.c1[1], a.c1[2]))),
-                     smul(l2, mk(a.c2[0], a.c2[1], a.c2[2])));
-    const v3 ro0 = mk(a.pos[0], a.pos[1], a.pos[2]);
-    const Ray ray = get_col(a, lut, ro0, normalize(d));
+// ---- schedule 0: persistent waves with per-lane refill (default) --------------------------------
+//
+// Each wave keeps all 64 lanes marching.  Rays are prepared (pixel_ray + s, :362-363, :262-263) in
+// full-width batches of one 8x8 tile into an LDS "ready" queue, and a lane whose ray terminates pops
+// the next ready ray at once, so no lane idles while a slow (photon-sphere "Zeno", capped) ray runs
+// on.  Finished rays are pushed into an LDS "done" queue and shaded (sky lookup, :329-345) in
+// full-width batches of 64.  Tiles are dequeued from NQ work counters (one 128-B line each; the
+// shard-local tile range is split into NQ contiguous parts; a wave starts on part blockIdx % NQ and
+// moves on when it is exhausted), so the result never depends on dispatch order or placement.
+constexpr uint32_t NQ = 8;
+constexpr uint32_t CTR_STRIDE = 32;  // u32 words between counters (128 B)
+constexpr uint32_t READY_CAP = 128;
+constexpr uint32_t DONE_CAP = 128;
 
-    const size_t idx = (a.layout == BH_LAYOUT_TILES) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
-    store_px(a.out_col, a.format, idx, ray.col);
-    if (a.out_blackout) {                                   // :365-368
-        const v3 bo = dot(ray.col, ray.col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : ray.col;
-        store_px(a.out_blackout, a.format, idx, bo);
+struct WaveQueues {
+    float r_x[READY_CAP], r_y[READY_CAP], r_z[READY_CAP], r_s[READY_CAP];
+    uint32_t r_idx[READY_CAP];
+    float d_x[DONE_CAP], d_y[DONE_CAP], d_z[DONE_CAP];
+    uint32_t d_idx[DONE_CAP], d_meta[DONE_CAP];  // meta = fate << 16 | n_rk
+};
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set lanes below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint32_t* __restrict__ counters) {
+    __shared__ float lut[256];
+    __shared__ WaveQueues queues[4];
+    lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    __syncthreads();  // the only workgroup barrier: waves run independently afterwards
+
+    const uint32_t lane = threadIdx.x & 63u;
+    WaveQueues& Q = queues[threadIdx.x >> 6];
+    const Frame f = make_frame(a);
+    const uint32_t T = a.n_tiles;
+
+    uint32_t part = blockIdx.x % NQ, parts_left = NQ;  // work-queue cursor (wave-uniform)
+    uint32_t n_ready = 0, n_done = 0;                  // queue fill levels (wave-uniform)
+
+    RayState st;
+    st.ro = f.ro0; st.rd = f.ro0; st.s = 0.0f; st.travelled = 0.0f; st.n_rk = 0; st.outside = false;
+    uint32_t idx = 0;
+    bool alive = false;
+
+    for (;;) {
+        // -- refill dead lanes from the ready queue; top the queue up with one tile if short --
+        const uint64_t dead = __ballot(!alive);
+        const uint32_t n_dead = __popcll(dead);
+        if (n_dead != 0u) {
+            while (n_ready < n_dead && parts_left != 0u) {
+                // dequeue one tile
+                uint32_t t = 0xFFFFFFFFu;
+                if (lane == 0) {
+                    const uint32_t lo = (uint32_t)((uint64_t)T * part / NQ);
+                    const uint32_t hi = (uint32_t)((uint64_t)T * (part + 1u) / NQ);
+                    const uint32_t i = atomicAdd(&counters[part * CTR_STRIDE], 1u);
+                    t = (lo + i < hi) ? lo + i : 0xFFFFFFFFu;
+                }
+                t = __builtin_amdgcn_readfirstlane(t);
+                if (t == 0xFFFFFFFFu) { part = (part + 1u) % NQ; --parts_left; continue; }
+                uint32_t tx, ty;
+                shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
+                const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
+                const bool valid = px < a.width && py < a.height;
+                const uint64_t vm = __ballot(valid);
+                if (valid) {
+                    const v3 rd0 = pixel_ray(a, px, py);
+                    const uint32_t e = n_ready + lane_rank(vm);
+                    Q.r_x[e] = rd0.x; Q.r_y[e] = rd0.y; Q.r_z[e] = rd0.z;
+                    Q.r_s[e] = ray_s(f, rd0);
+                    Q.r_idx[e] = (uint32_t)out_index(a, t, lane, px, py);
+                }
+                n_ready += (uint32_t)__popcll(vm);
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (n_ready != 0u) {
+                if (!alive) {
+                    const uint32_t k = lane_rank(dead);
+                    if (k < n_ready) {
+                        const uint32_t e = n_ready - 1u - k;
+                        st.ro = f.ro0;
+                        st.rd = mk(Q.r_x[e], Q.r_y[e], Q.r_z[e]);
+                        st.s = Q.r_s[e];
+                        idx = Q.r_idx[e];
+                        st.travelled = 0.0f; st.n_rk = 0; st.outside = false;
+                        alive = true;
+                    }
+                }
+                n_ready -= (n_dead < n_ready) ? n_dead : n_ready;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        if (__ballot(alive) == 0ull) break;  // no rays left anywhere for this wave
+
+        // -- one RK iteration for every live lane --
+        uint32_t fate = 0xFFu;
+        if (alive) fate = march_step(a, f, st);
+        const bool fin = fate != 0xFFu;
+        const uint64_t fm = __ballot(fin);
+        if (fm != 0ull) {
+            if (fin) {
+                const uint32_t e = n_done + lane_rank(fm);
+                Q.d_x[e] = st.rd.x; Q.d_y[e] = st.rd.y; Q.d_z[e] = st.rd.z;
+                Q.d_idx[e] = idx;
+                Q.d_meta[e] = (fate << 16) | st.n_rk;
+                alive = false;
+            }
+            n_done += (uint32_t)__popcll(fm);
+            __builtin_amdgcn_wave_barrier();
+            // -- shade a full batch of 64 finished rays --
+            if (n_done >= 64u) {
+                const uint32_t e = n_done - 64u + lane;
+                const uint32_t meta = Q.d_meta[e];
+                const v3 col = shade(a, lut, meta >> 16, mk(Q.d_x[e], Q.d_y[e], Q.d_z[e]));
+                write_pixel(a, Q.d_idx[e], col, meta & 0xFFFFu, meta >> 16);
+                n_done -= 64u;
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
     }
-    if (a.dbg_n_rk) a.dbg_n_rk[idx] = (uint16_t)ray.n_rk;
-    if (a.dbg_fate) a.dbg_fate[idx] = (uint8_t)ray.fate;
+    // -- shade what is left --
+    if (lane < n_done) {
+        const uint32_t meta = Q.d_meta[lane];
+        const v3 col = shade(a, lut, meta >> 16, mk(Q.d_x[lane], Q.d_y[lane], Q.d_z[lane]));
+        write_pixel(a, Q.d_idx[lane], col, meta & 0xFFFFu, meta >> 16);
+    }
 }
 
 }  // namespace BH_NS

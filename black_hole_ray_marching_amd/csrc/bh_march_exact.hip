@@ -4,8 +4,23 @@
 #define BH_NS exact
 #include "bh_march.hpp"
 
-extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, hipStream_t s) {
-    const uint32_t blocks = (a.n_tiles + 3u) / 4u;
-    hipLaunchKernelGGL(bh::exact::march_kernel, dim3(blocks), dim3(256), 0, s, a);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
+                                                                             uint32_t* counters, uint32_t grid,
+                                                                             hipStream_t s) {
+    if (schedule == BH_SCHED_TILE) {
+        const uint32_t blocks = (a.n_tiles + 3u) / 4u;
+        hipLaunchKernelGGL(bh::exact::march_tile_kernel, dim3(blocks), dim3(256), 0, s, a);
+    } else {
+        hipError_t e = hipMemsetAsync(counters, 0, bh::exact::NQ * bh::exact::CTR_STRIDE * sizeof(uint32_t), s);
+        if (e != hipSuccess) return (int)e;
+        hipLaunchKernelGGL(bh::exact::march_persistent_kernel, dim3(grid), dim3(256), 0, s, a, counters);
+    }
     return (int)hipGetLastError();
+}
+
+// Resident 256-thread blocks per CU of the persistent kernel (sizes its grid: every block resident).
+extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exact(void) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::exact::march_persistent_kernel, 256, 0) != hipSuccess) return 1;
+    return n > 0 ? n : 1;
 }

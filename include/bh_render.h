@@ -114,6 +114,12 @@ typedef enum {
                                are left untouched */
 } bh_layout;
 
+/* Work schedule of the march kernel (same results, different speed). */
+typedef enum {
+    BH_SCHED_PERSISTENT = 0, /* resident waves, per-lane refill from an LDS ray queue (default) */
+    BH_SCHED_TILE = 1        /* one wave64 per 8x8 tile, exits when its slowest ray finishes */
+} bh_schedule;
+
 /* Per-pixel fate codes written to dbg_fate. */
 #define BH_FATE_CAP      0u  /* loop ran out (max_iters); still shades sky with its current rd */
 #define BH_FATE_ESCAPE   1u  /* distance_travelled > MAX_DIST (src/black_hole_maybe.wgsl:325-327) */
@@ -131,7 +137,7 @@ typedef struct {
     uint32_t layout;          /* bh_layout */
     uint32_t shard_index;     /* this rank's tile share: tile (tx,ty) belongs to shard (tx + 3*ty) % shard_count */
     uint32_t shard_count;     /* 1 = whole frame */
-    uint32_t _reserved;
+    uint32_t schedule;        /* bh_schedule */
     void* out_col;            /* target 0 (`col`), device pointer, never NULL */
     void* out_blackout;       /* target 1 (`blackout_col`), device pointer or NULL (== Option::None) */
     uint16_t* dbg_n_rk;       /* optional: completed RK4 steps per pixel (same layout as outputs, 1 elem/px) */
