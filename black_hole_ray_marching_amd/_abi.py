@@ -70,6 +70,7 @@ SIGNATURES = {
     "bh_shard_tile_count": (C.c_int64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
+    "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
 }
 
 _lib = None

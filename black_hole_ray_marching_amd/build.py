@@ -30,6 +30,7 @@ TU_FLAGS = {
     "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
     "bh_tiles.hip": [],
+    "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
 }
 

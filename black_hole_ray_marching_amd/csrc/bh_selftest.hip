@@ -1,0 +1,102 @@
+// bh_selftest.hip — on-device verification of the correctly rounded cores of bh_crmath.hpp against
+// hipcc's IEEE division / sqrt (this TU: -ffp-contract=off, correctly rounded f32 div/sqrt).
+// Exposed as bh_selftest_crmath (diagnostics API of include/bh_render.h).
+#include "bh_common.hpp"
+#include "bh_crmath.hpp"
+
+namespace bh {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+// float with a uniformly random exponent in [elo, ehi] (unbiased exponents) and random mantissa/sign
+__device__ __forceinline__ float rnd_float(uint64_t h, int elo, int ehi) {
+    const uint32_t span = (uint32_t)(ehi - elo + 1);
+    const uint32_t e = (uint32_t)(elo + 127) + (uint32_t)((h >> 32) % span);
+    const uint32_t bits = ((uint32_t)(h >> 8) & 0x807FFFFFu) | (e << 23);
+    return __uint_as_float(bits);
+}
+
+__device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, uint32_t a, uint32_t b, uint32_t got,
+                                       uint32_t want) {
+    const unsigned long long k = atomicAdd(cnt, 1ull);
+    if (k < 2) { ex[4 * k + 0] = a; ex[4 * k + 1] = b; ex[4 * k + 2] = got; ex[4 * k + 3] = want; }
+}
+
+// op 0: sqrt_core over EVERY float with bits in [base, base + count) (guard-passing inputs only)
+// op 1: div6 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
+// op 2: div_core on `count` random (n, d) pairs from the guarded domain, seeded by base
+// op 3: div_core with n = d * m for random small integers m (exact quotients) and n = d*q +- ulps
+__global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, uint64_t count,
+                                                      unsigned long long* cnt, uint32_t* ex) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        if (op == 0) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            if (crm::sqrt_bad(x) && x != 0.0f) continue;
+            const float got = crm::sqrt_core(x), want = __builtin_sqrtf(x);
+            if (__float_as_uint(got) != __float_as_uint(want) && !(got != got && want != want))
+                record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 1) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            if (crm::key(x) < crm::KEY_MIN) continue;
+            if (x != x || __builtin_isinf(x)) continue;
+            const float got = crm::div6(x), want = x / 6.0f;
+            if (__float_as_uint(got) != __float_as_uint(want))
+                record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 2 || op == 3) {
+            const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
+            float d = fabsf(rnd_float(h1, -40, 59));
+            float n;
+            if (op == 2) {
+                n = rnd_float(h2, -60, 64);
+                if ((h2 & 0xFF) == 7) n = ((h2 >> 9) & 1) ? -0.0f : 0.0f;
+            } else {
+                const float m = (float)((int32_t)((h2 >> 40) & 0xFFFF) - 32768);
+                n = d * m;  // often exact
+                const int32_t ulps = (int32_t)((h2 >> 8) & 7) - 3;
+                n = __uint_as_float(__float_as_uint(n) + (uint32_t)ulps);
+            }
+            if (crm::div_d_bad(d) || crm::key(n) < crm::KEY_MIN || n != n || __builtin_isinf(n) || fabsf(n) > 0x1p64f) continue;
+            const float got = crm::div_core(n, crm::rcp_refined(d)), want = n / d;
+            if (__float_as_uint(got) != __float_as_uint(want))
+                record(cnt, ex, __float_as_uint(n), __float_as_uint(d), __float_as_uint(got), __float_as_uint(want));
+        }
+    }
+}
+
+}  // namespace bh
+
+extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
+                                  uint32_t* out_examples, int device) {
+    if (op < 0 || op > 3 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;
+    unsigned long long* cnt = nullptr;
+    uint32_t* ex = nullptr;
+    int st = BH_OK;
+    if (hipMalloc(&cnt, sizeof(*cnt)) != hipSuccess || hipMalloc(&ex, 8 * sizeof(uint32_t)) != hipSuccess) {
+        st = BH_ERR_OUT_OF_MEMORY;
+    } else {
+        (void)hipMemset(cnt, 0, sizeof(*cnt));
+        (void)hipMemset(ex, 0, 8 * sizeof(uint32_t));
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex);
+        if (hipDeviceSynchronize() != hipSuccess) st = BH_ERR_HIP;
+        unsigned long long h = 0;
+        (void)hipMemcpy(&h, cnt, sizeof(h), hipMemcpyDeviceToHost);
+        *out_mismatches = h;
+        if (out_examples) (void)hipMemcpy(out_examples, ex, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    }
+    if (cnt) (void)hipFree(cnt);
+    if (ex) (void)hipFree(ex);
+    (void)hipSetDevice(prev);
+    return st;
+}

@@ -184,6 +184,14 @@ int bh_tiles_unpack(const void* packed, void* out_rowmajor, uint32_t width, uint
                     uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t bytes_per_pixel,
                     void* hip_stream);
 
+/* Diagnostics: check the correctly rounded division/sqrt cores the exact kernel uses against IEEE
+ * results on `device` (op 0: sqrt over float bit patterns [base, base+count); op 1: x/6 over bit
+ * patterns [base, base+count); op 2: n/d on `count` random pairs seeded by base; op 3: n/d near exact
+ * quotients).  *out_mismatches = number of differing results; out_examples (8 u32, optional) = up
+ * to two (a, b, got, want) bit patterns.  Synchronous. */
+int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
+                       uint32_t* out_examples, int device);
+
 #ifdef __cplusplus
 }
 #endif
