@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bh_common.hpp"
+#include "bh_crmath.hpp"
 
 #ifndef BH_FAST
 #error "define BH_FAST to 0 or 1"
@@ -178,6 +179,7 @@ struct RayState {
     bool outside;
 };
 
+#if BH_FAST
 // One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
 // iteration (n_rk counts completed RK updates), or 0xFF if it continues.
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
@@ -203,14 +205,9 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
     v3 rd_k3 = smul(dt, accel(add(ro, smul(0.5f, ro_k2)), s));
     v3 ro_k4 = smul(dt, add(rd, rd_k3));
     v3 rd_k4 = smul(dt, accel(add(ro, ro_k3), s));
-#if BH_FAST
     constexpr float SIXTH = 1.0f / 6.0f;
     v3 dro = muls(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), SIXTH);
     v3 drd = muls(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), SIXTH);
-#else
-    v3 dro = divs(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), 6.0f);
-    v3 drd = divs(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), 6.0f);
-#endif
     st.ro = add(ro, dro);                               // :315
     st.rd = add(rd, drd);                               // :322
     st.travelled += dt;                                 // :324
@@ -219,6 +216,124 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
     if (st.n_rk >= a.max_iters) return BH_FATE_CAP;        // loop exhausted (:266)
     return 0xFFu;
 }
+#else
+// Exact mode.  The arithmetic is the normative op sequence of oracle/bh_oracle.c: every rounding
+// the same as IEEE f32 evaluated in WGSL source order.  CR = true evaluates the divisions and
+// square roots with the cheap correctly rounded cores of bh_crmath.hpp and raises `bad` for any
+// operand outside their proven domain; CR = false is plain IEEE ops (hipcc's expansions).  Both
+// produce identical bits wherever `bad` stays false.
+template <bool CR>
+struct XOps {
+    bool bad = false;
+    uint32_t kmin = 0xFFFFFFFFu;  // running min of crm::key() over division numerators
+    __device__ __forceinline__ float sqrt(float x) {
+        if constexpr (CR) { bad |= crm::sqrt_bad(x); return crm::sqrt_core(x); }
+        else return __builtin_sqrtf(x);
+    }
+    __device__ __forceinline__ float div6(float x) {
+        if constexpr (CR) { kmin = min(kmin, crm::key(x)); return crm::div6(x); }
+        else return x / 6.0f;
+    }
+    // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
+    // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq) {
+        const float Q = (q * q) * sq;
+        const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
+        if constexpr (CR) {
+            bad |= crm::div_d_bad(Q);
+            kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
+            const crm::Rcp R = crm::rcp_refined(Q);
+            return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
+        } else {
+            return mk(nx / Q, ny / Q, nz / Q);
+        }
+    }
+    __device__ __forceinline__ v3 accel(v3 p, float s) {
+        const float q = dot(p, p);
+        return accel_qs(p, s, q, sqrt(q));
+    }
+    __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
+    // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
+    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
+        float d = __builtin_inff();
+        if (flags & BH_SCENE_DISC) {
+            const float rho = sqrt(p.x * p.x + p.z * p.z);
+            d = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
+        }
+        if (flags & BH_SCENE_MARKERS) {
+            const float xx = p.x * p.x, yy = p.y * p.y;
+            const float dz = -10.0f - p.z, zz = dz * dz;
+            const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
+            const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
+            const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
+            const float m = sqrt(fminf(q1, fminf(q2, fminf(q3, q4)))) - 0.5f;
+            d = (flags & BH_SCENE_DISC) ? fminf(d, m) : m;
+        }
+        return d;
+    }
+};
+
+template <bool CR>
+__device__ __forceinline__ uint32_t march_step_x(const MarchArgs& a, const Frame& f, RayState& st, XOps<CR>& X) {
+    const v3 ro = st.ro, rd = st.rd;
+    const float r2 = dot(ro, ro);
+    const float r = X.sqrt(r2);                         // :271
+    if (a.blackout_eh != 0u) {                          // :272-283
+        if (r < 1.0f && dot(rd, ro) < 0.0f) return BH_FATE_BLACKOUT;
+        if (r > 1.0f) st.outside = true;
+        else if (st.outside) return BH_FATE_BLACKOUT;
+    }
+    const float ds = X.sdf(ro, a.rs, a.scene_flags);    // :285
+    if (ds < MIN_DIST) return BH_FATE_SURFACE;          // :286-288
+    const float dps = X.length(sub(f.cps, ro)) - 0.075f;  // :294
+    const float dist = fminf(ds, dps);                  // :299
+    const float dt = fminf(dist * 0.9f, a.dtm * r);     // :307-310
+    const float s = st.s;
+    // get_delta_photon_rk4 (:134-151)
+    v3 ro_k1 = smul(dt, rd);
+    v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r));
+    v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
+    v3 rd_k2 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k1)), s));
+    v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
+    v3 rd_k3 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k2)), s));
+    v3 ro_k4 = smul(dt, add(rd, rd_k3));
+    v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
+    const v3 nro = add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4);
+    const v3 nrd = add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4);
+    const v3 dro = mk(X.div6(nro.x), X.div6(nro.y), X.div6(nro.z));
+    const v3 drd = mk(X.div6(nrd.x), X.div6(nrd.y), X.div6(nrd.z));
+    st.ro = add(ro, dro);                               // :315
+    st.rd = add(rd, drd);                               // :322
+    st.travelled += dt;                                 // :324
+    if constexpr (CR) {
+        // numerator magnitudes, |s| bound (|n| <= 2^30 * |p|), finite state (overflow anywhere)
+        X.bad |= X.kmin < crm::KEY_MIN;
+        X.bad |= !(fabsf(s) <= 0x1p30f);
+        X.bad |= !__builtin_isfinite(((st.ro.x + st.ro.y) + (st.ro.z + st.rd.x)) + ((st.rd.y + st.rd.z) + dt));
+    }
+    st.n_rk += 1u;
+    if (st.travelled > a.max_dist) return BH_FATE_ESCAPE;  // :325-327
+    if (st.n_rk >= a.max_iters) return BH_FATE_CAP;        // loop exhausted (:266)
+    return 0xFFu;
+}
+
+// One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
+// iteration (n_rk counts completed RK updates), or 0xFF if it continues.
+__device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
+    RayState t = st;
+    XOps<true> X;
+    uint32_t fate = march_step_x<true>(a, f, t, X);
+    if (__builtin_expect(__ballot(X.bad) != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
+        if (X.bad) {
+            t = st;
+            XOps<false> Y;
+            fate = march_step_x<false>(a, f, t, Y);
+        }
+    }
+    st = t;
+    return fate;
+}
+#endif
 
 // Colour of a finished ray (:329-345 for sky rays; :275/:281 blackout -> 0; :287 surface -> 1).
 __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32_t fate, v3 rd) {
