@@ -42,9 +42,10 @@ __device__ __forceinline__ bool sqrt_bad(float x) { return x < SQRT_MIN; }
 // Correctly rounded when d and n/d are normal and far from the exponent limits and |n| is not tiny
 // (the residual n - d*y must not underflow).  The caller guarantees:
 //   DIV_D_MIN <= d <= DIV_D_MAX  (checked per denominator, div_d_bad)
-//   n == 0 or |n| >= DIV_N_MIN    (checked per numerator through key(), see below)
-// and |n| <= 2^64 (follows from the march state bounds, caught by the per-step finiteness check).
-// The zero sign comes from copysign with y = n*r, which has the sign of n/d.
+//   n == 0 or DIV_N_MIN <= |n| <= 2^64
+// The residuals are formed negated, e' = d*y - n = -(n - d*y) (exact in an FMA, RN is symmetric),
+// and added back as fma(-e', r, y): identical for n != 0, and for n = +-0 every sum then keeps the
+// IEEE sign of the zero quotient (-0 + -0 = -0) without a copysign.
 constexpr float DIV_D_MIN = 0x1p-40f;
 constexpr float DIV_D_MAX = 0x1p+60f;
 constexpr float DIV_N_MIN = 0x1p-60f;
@@ -59,34 +60,31 @@ __device__ __forceinline__ Rcp rcp_refined(float d) {
 }
 __device__ __forceinline__ float div_core(float n, const Rcp& R) {
     const float y = n * R.r;
-    const float e1 = __builtin_fmaf(-R.d, y, n);
-    const float y1 = __builtin_fmaf(e1, R.r, y);
-    const float e2 = __builtin_fmaf(-R.d, y1, n);
-    const float q = __builtin_fmaf(e2, R.r, y1);
-    return __builtin_copysignf(q, y);
+    const float e1 = __builtin_fmaf(R.d, y, -n);
+    const float y1 = __builtin_fmaf(-e1, R.r, y);
+    const float e2 = __builtin_fmaf(R.d, y1, -n);
+    return __builtin_fmaf(-e2, R.r, y1);
 }
 __device__ __forceinline__ bool div_d_bad(float d) { return !(d >= DIV_D_MIN && d <= DIV_D_MAX); }
 
 // ---- division by 6 ----------------------------------------------------------------------------
 // y = x * RN(1/6); q = y + RN(1/6) * (x - 6y): equals RN(x / 6) for every x whose quotient is not
-// subnormal (exhaustively checked over all 2^32 inputs on the CPU with hardware FMA; the sign of a
-// zero quotient comes from copysign with x).  Callers guarantee x == 0 or |x| >= DIV_N_MIN.
+// subnormal (exhaustively checked over all 2^32 inputs; the residual is formed negated as in
+// div_core so that x = +-0 gives the IEEE zero).  Callers guarantee x == 0 or |x| >= DIV_N_MIN.
 __device__ __forceinline__ float div6(float x) {
     constexpr float R6 = 1.0f / 6.0f;
     const float y = x * R6;
-    const float e = __builtin_fmaf(-y, 6.0f, x);
-    return __builtin_copysignf(__builtin_fmaf(e, R6, y), x);
+    const float e = __builtin_fmaf(y, 6.0f, -x);
+    return __builtin_fmaf(-e, R6, y);
 }
 
 // ---- numerator magnitude guard ----------------------------------------------------------------
-// key(n) = 2*bits(|n|) - 1 (mod 2^32): +-0 -> 0xFFFFFFFF, tiny -> small.  A running unsigned min of
-// keys flags any nonzero |n| < DIV_N_MIN with one compare at the end (NaN/inf map high; they are
-// caught by the finiteness check instead).
+// key(n) = 2*bits(|n|) - 1 (mod 2^32): +-0 -> 0xFFFFFFFF, tiny -> small, so key(n) < KEY_MIN iff
+// 0 < |n| < DIV_N_MIN.  (Used by the self-test; the march loop uses the cheaper min-of-|n| form.)
 constexpr uint32_t KEY_MIN = (0x21800000u << 1) - 1u;  // key(2^-60)
 __device__ __forceinline__ uint32_t key(float n) { return (__float_as_uint(n) << 1) - 1u; }
-__device__ __forceinline__ uint32_t kmin3(uint32_t a, uint32_t b, uint32_t c) {
-    return min(min(a, b), c);  // v_min3_u32
-}
+// min(|a|, |b|, |c|) in one v_min3_f32 with |.| source modifiers
+__device__ __forceinline__ float amin3(float a, float b, float c) { return fminf(fminf(fabsf(a), fabsf(b)), fabsf(c)); }
 
 }  // namespace crm
 }  // namespace bh

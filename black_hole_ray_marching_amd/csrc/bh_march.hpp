@@ -225,14 +225,18 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
 template <bool CR>
 struct XOps {
     bool bad = false;
-    uint32_t kmin = 0xFFFFFFFFu;  // running min of crm::key() over division numerators
+    float nmin = __builtin_inff();  // running min of |numerator| over the accel divisions
     __device__ __forceinline__ float sqrt(float x) {
         if constexpr (CR) { bad |= crm::sqrt_bad(x); return crm::sqrt_core(x); }
         else return __builtin_sqrtf(x);
     }
-    __device__ __forceinline__ float div6(float x) {
-        if constexpr (CR) { kmin = min(kmin, crm::key(x)); return crm::div6(x); }
-        else return x / 6.0f;
+    __device__ __forceinline__ v3 div6(v3 x) {
+        if constexpr (CR) {
+            bad |= crm::amin3(x.x, x.y, x.z) < crm::DIV_N_MIN;  // zeros too: rare, IEEE path
+            return mk(crm::div6(x.x), crm::div6(x.y), crm::div6(x.z));
+        } else {
+            return mk(x.x / 6.0f, x.y / 6.0f, x.z / 6.0f);
+        }
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
     // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
@@ -241,7 +245,7 @@ struct XOps {
         const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
         if constexpr (CR) {
             bad |= crm::div_d_bad(Q);
-            kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
+            nmin = fminf(nmin, crm::amin3(nx, ny, nz));
             const crm::Rcp R = crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
         } else {
@@ -300,16 +304,18 @@ __device__ __forceinline__ uint32_t march_step_x(const MarchArgs& a, const Frame
     v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
     const v3 nro = add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4);
     const v3 nrd = add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4);
-    const v3 dro = mk(X.div6(nro.x), X.div6(nro.y), X.div6(nro.z));
-    const v3 drd = mk(X.div6(nrd.x), X.div6(nrd.y), X.div6(nrd.z));
+    const v3 dro = X.div6(nro);
+    const v3 drd = X.div6(nrd);
     st.ro = add(ro, dro);                               // :315
     st.rd = add(rd, drd);                               // :322
     st.travelled += dt;                                 // :324
     if constexpr (CR) {
-        // numerator magnitudes, |s| bound (|n| <= 2^30 * |p|), finite state (overflow anywhere)
-        X.bad |= X.kmin < crm::KEY_MIN;
+        // Domain of the division cores: every accel numerator s*p_i is 0 or >= 2^-60 in magnitude
+        // (exact zeros only occur when s == 0, i.e. DISTORTION_POWER == 0 or a radial ray, and the
+        // cores are exact for them), and |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds
+        // |s*p_i| <= 2^42.
+        X.bad |= (X.nmin < crm::DIV_N_MIN) && (s != 0.0f);
         X.bad |= !(fabsf(s) <= 0x1p30f);
-        X.bad |= !__builtin_isfinite(((st.ro.x + st.ro.y) + (st.ro.z + st.rd.x)) + ((st.rd.y + st.rd.z) + dt));
     }
     st.n_rk += 1u;
     if (st.travelled > a.max_dist) return BH_FATE_ESCAPE;  // :325-327
