@@ -5,7 +5,7 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "libbh_render.so"
+LIB_PATH = Path(os.environ.get("BH_LIB", Path(__file__).resolve().parent / "libbh_render.so"))
 
 BH_OK = 0
 BH_ERR_INVALID_ARG = -1

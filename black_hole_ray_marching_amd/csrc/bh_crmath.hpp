@@ -80,11 +80,12 @@ __device__ __forceinline__ float div6(float x) {
 
 // ---- numerator magnitude guard ----------------------------------------------------------------
 // key(n) = 2*bits(|n|) - 1 (mod 2^32): +-0 -> 0xFFFFFFFF, tiny -> small, so key(n) < KEY_MIN iff
-// 0 < |n| < DIV_N_MIN.  (Used by the self-test; the march loop uses the cheaper min-of-|n| form.)
+// 0 < |n| < DIV_N_MIN; a running v_min3_u32 over keys needs one compare per step.  (A float
+// min of |n| would be one op cheaper but cannot tell 0 from tiny: measured 2x slower overall,
+// because every camera-A ray starts on two coordinate planes and its first step then re-runs.)
 constexpr uint32_t KEY_MIN = (0x21800000u << 1) - 1u;  // key(2^-60)
 __device__ __forceinline__ uint32_t key(float n) { return (__float_as_uint(n) << 1) - 1u; }
-// min(|a|, |b|, |c|) in one v_min3_f32 with |.| source modifiers
-__device__ __forceinline__ float amin3(float a, float b, float c) { return fminf(fminf(fabsf(a), fabsf(b)), fabsf(c)); }
+__device__ __forceinline__ uint32_t kmin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
 
 }  // namespace crm
 }  // namespace bh

@@ -225,14 +225,16 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
 template <bool CR>
 struct XOps {
     bool bad = false;
-    float nmin = __builtin_inff();  // running min of |numerator| over the accel divisions
+    // running unsigned min of crm::key() over every division numerator: zeros map high (the cores
+    // are exact for them; camera-A rays start on two coordinate planes), tiny values low
+    uint32_t kmin = 0xFFFFFFFFu;
     __device__ __forceinline__ float sqrt(float x) {
         if constexpr (CR) { bad |= crm::sqrt_bad(x); return crm::sqrt_core(x); }
         else return __builtin_sqrtf(x);
     }
     __device__ __forceinline__ v3 div6(v3 x) {
         if constexpr (CR) {
-            bad |= crm::amin3(x.x, x.y, x.z) < crm::DIV_N_MIN;  // zeros too: rare, IEEE path
+            kmin = min(kmin, crm::kmin3(crm::key(x.x), crm::key(x.y), crm::key(x.z)));
             return mk(crm::div6(x.x), crm::div6(x.y), crm::div6(x.z));
         } else {
             return mk(x.x / 6.0f, x.y / 6.0f, x.z / 6.0f);
@@ -245,7 +247,7 @@ struct XOps {
         const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
         if constexpr (CR) {
             bad |= crm::div_d_bad(Q);
-            nmin = fminf(nmin, crm::amin3(nx, ny, nz));
+            kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
             const crm::Rcp R = crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
         } else {
@@ -310,11 +312,9 @@ __device__ __forceinline__ uint32_t march_step_x(const MarchArgs& a, const Frame
     st.rd = add(rd, drd);                               // :322
     st.travelled += dt;                                 // :324
     if constexpr (CR) {
-        // Domain of the division cores: every accel numerator s*p_i is 0 or >= 2^-60 in magnitude
-        // (exact zeros only occur when s == 0, i.e. DISTORTION_POWER == 0 or a radial ray, and the
-        // cores are exact for them), and |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds
-        // |s*p_i| <= 2^42.
-        X.bad |= (X.nmin < crm::DIV_N_MIN) && (s != 0.0f);
+        // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
+        // |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds every |s*p_i| <= 2^42.
+        X.bad |= X.kmin < crm::KEY_MIN;
         X.bad |= !(fabsf(s) <= 0x1p30f);
     }
     st.n_rk += 1u;
@@ -325,11 +325,21 @@ __device__ __forceinline__ uint32_t march_step_x(const MarchArgs& a, const Frame
 
 // One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
 // iteration (n_rk counts completed RK updates), or 0xFF if it continues.
+#ifdef BH_DIAG_SLOW
+__device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
+#endif
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
     RayState t = st;
     XOps<true> X;
     uint32_t fate = march_step_x<true>(a, f, t, X);
-    if (__builtin_expect(__ballot(X.bad) != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
+    const uint64_t badm = __ballot(X.bad);
+    if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
+#ifdef BH_DIAG_SLOW
+        if ((threadIdx.x & 63u) == 0u) {
+            atomicAdd(&g_diag_slow_wave_steps, 1u);
+            atomicAdd(&g_diag_slow_lane_steps, (uint32_t)__popcll(badm));
+        }
+#endif
         if (X.bad) {
             t = st;
             XOps<false> Y;

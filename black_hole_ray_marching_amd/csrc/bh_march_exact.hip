@@ -24,3 +24,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exac
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::exact::march_persistent_kernel, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
+
+#ifdef BH_DIAG_SLOW
+// diagnostics build only: read and reset the fallback counters
+extern "C" int bh_diag_slow_counts(uint32_t* lane_steps, uint32_t* wave_steps) {
+    uint32_t z = 0;
+    if (hipMemcpyFromSymbol(lane_steps, HIP_SYMBOL(bh::exact::g_diag_slow_lane_steps), 4) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(wave_steps, HIP_SYMBOL(bh::exact::g_diag_slow_wave_steps), 4) != hipSuccess) return -1;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::exact::g_diag_slow_lane_steps), &z, 4);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::exact::g_diag_slow_wave_steps), &z, 4);
+    return 0;
+}
+#endif

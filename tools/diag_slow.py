@@ -1,0 +1,25 @@
+"""Count guarded-fallback (IEEE) steps of the exact kernel: BH_LIB=tools/variants/diag.so python tools/diag_slow.py"""
+import ctypes as C
+import sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch
+import black_hole_ray_marching_amd as bh
+
+lib = bh.load()
+lib.bh_diag_slow_counts.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+sky = bh.synthetic_sky()
+for cam in ("A", "B"):
+    sc = bh.Scene(4096, 2048, sky=sky, max_iters=512, math=bh.BH_MATH_EXACT)
+    if cam == "B":
+        sc.update(bh.Camera.look_at((0.0, 3.0, -20.0), (0.0, 0.0, 0.0), 4096, 2048))
+    col = torch.empty((2048, 4096, 4), dtype=torch.float16, device="cuda")
+    nrk = torch.empty((2048, 4096), dtype=torch.int16, device="cuda")
+    a, b = C.c_uint32(), C.c_uint32()
+    lib.bh_diag_slow_counts(C.byref(a), C.byref(b))
+    sc.render(col, None, fmt=bh.BH_OUT_RGBA16F, dbg_n_rk=nrk, schedule=bh.BH_SCHED_TILE)
+    torch.cuda.synchronize()
+    lib.bh_diag_slow_counts(C.byref(a), C.byref(b))
+    steps = int(nrk.cpu().numpy().view("uint16").astype("int64").sum())
+    print(f"camera {cam}: lane-steps total {steps}, slow lane-steps {a.value}, slow wave-steps {b.value}, "
+          f"waves {4096*2048//64}")
