@@ -1,0 +1,84 @@
+"""Tile-sharded frames over several GPUs (one process per GPU, torch.distributed over RCCL).
+
+The frame is cut into 8x8 tiles; tile (tx, ty) belongs to rank (tx + 3*ty) % world (SURVEY.md
+§8e: the diagonal interleave spreads the expensive photon-sphere region over all ranks; contiguous
+bands would leave the centre band's owner with ~1.3x the average work).  Each rank renders its
+tiles with BH_LAYOUT_TILES into one contiguous buffer, the buffers are gathered to rank 0 in a
+single collective (no reduction exists in this path), and rank 0 scatters them to a row-major frame
+with the bh_tiles_unpack kernel.
+
+The reference renders one frame on one GPU (src/state.rs:255-307); this module is the multi-GPU
+extension named by north_star.  The pure-Python tile math mirrors bh_common.hpp so that host logic
+can be tested without a GPU.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TILE = 8
+
+
+def shard_period(S: int) -> int:
+    return S // 3 if S % 3 == 0 else S
+
+
+def shard_row_start(ty: int, k: int, S: int) -> int:
+    return (k - 3 * ty) % S
+
+
+def shard_row_count(tiles_x: int, ty: int, k: int, S: int) -> int:
+    st = shard_row_start(ty, k, S)
+    return (tiles_x - st + S - 1) // S if st < tiles_x else 0
+
+
+def shard_tile_count(width: int, height: int, k: int, S: int) -> int:
+    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+    return sum(shard_row_count(tx, r, k, S) for r in range(ty))
+
+
+def shard_tiles(width: int, height: int, k: int, S: int) -> np.ndarray:
+    """(n, 2) array of (tx, ty) for shard k, in its packed order (row-major over owned tiles)."""
+    tiles_x, tiles_y = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+    out = [(tx, ty) for ty in range(tiles_y) for tx in range(shard_row_start(ty, k, S), tiles_x, S)]
+    return np.array(out, dtype=np.int64).reshape(-1, 2)
+
+
+def packed_stride(width: int, height: int, S: int) -> int:
+    """Tiles per rank in the gather buffer (the largest shard; smaller shards are padded)."""
+    return max(shard_tile_count(width, height, k, S) for k in range(S))
+
+
+def unpack_tiles_numpy(packed: np.ndarray, width: int, height: int, S: int, stride: int) -> np.ndarray:
+    """Reference (CPU) version of bh_tiles_unpack: packed (S*stride*64, C) -> (height, width, C)."""
+    C = packed.shape[-1]
+    out = np.zeros((height, width, C), dtype=packed.dtype)
+    lane = np.arange(64)
+    for k in range(S):
+        for t, (tx, ty) in enumerate(shard_tiles(width, height, k, S)):
+            px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
+            ok = (px < width) & (py < height)
+            out[py[ok], px[ok]] = packed[(k * stride + t) * 64 + lane[ok]]
+    return out
+
+
+def gather_packed(packed, rank: int, world: int, gathered=None, group=None):
+    """Gather every rank's packed tile buffer (same shape on all ranks) to rank 0.
+
+    One torch.distributed.gather: RCCL on GPUs (rank 0 receives the 7 peers over 7 xGMI links at
+    once), gloo in CPU tests.  Returns the list of buffers on rank 0, None elsewhere."""
+    import torch.distributed as dist
+    if world == 1:
+        return [packed]
+    if rank == 0 and gathered is None:
+        import torch
+        gathered = [torch.empty_like(packed) for _ in range(world)]
+    dist.gather(packed, gathered if rank == 0 else None, dst=0, group=group)
+    return gathered if rank == 0 else None
+
+
+def weak_scaling_frame(world: int, base_w: int = 4096, base_h: int = 2048) -> tuple[int, int]:
+    """Frame for `world` GPUs with about base_w*base_h pixels per GPU at the base aspect (weak scaling)."""
+    if world == 1:
+        return base_w, base_h
+    w = int(round(base_w * np.sqrt(world) / TILE)) * TILE
+    return w, int(round(w * base_h / base_w / TILE)) * TILE

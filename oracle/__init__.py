@@ -28,7 +28,7 @@ def load() -> C.CDLL:
         lib.bho_trace_ray.restype = C.c_int
         lib.bho_trace_ray.argtypes = [C.c_float * 3, C.c_float * 3, C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_float * 3,
-                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+                                      C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_float * 6]
         lib.bho_srgb_lut.restype = None
         lib.bho_srgb_lut.argtypes = [C.c_void_p]
         lib.bho_srgb_encode.restype = C.c_uint8
@@ -64,14 +64,17 @@ def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: 
 
 
 def trace_ray(ro0, rd0, uniforms: bytes, sky: np.ndarray, max_iters: int, scene_flags: int):
+    """One explicit ray through get_col.  Returns (rgb, n_rk, fate, final ro, final rd)."""
     lib = load()
     sky = np.ascontiguousarray(sky, dtype=np.uint8)
     out = (C.c_float * 3)()
+    st = (C.c_float * 6)()
     n, f = C.c_uint32(), C.c_uint32()
     uni = C.create_string_buffer(bytes(uniforms), 32)
     lib.bho_trace_ray((C.c_float * 3)(*ro0), (C.c_float * 3)(*rd0), uni, sky.ctypes.data, sky.shape[1],
-                      sky.shape[0], max_iters, scene_flags, out, C.byref(n), C.byref(f))
-    return np.array(out, np.float32), int(n.value), int(f.value)
+                      sky.shape[0], max_iters, scene_flags, out, C.byref(n), C.byref(f), st)
+    s = np.array(st, np.float32)
+    return np.array(out, np.float32), int(n.value), int(f.value), s[:3], s[3:]
 
 
 def srgb_lut() -> np.ndarray:

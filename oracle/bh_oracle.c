@@ -147,8 +147,10 @@ static v3 sample_bilinear(const sky_t* S, float u, float v) {
     return add(muls(top, ib), muls(bot, b));
 }
 
-/* get_col, :259-345.  Returns rgb; *n_rk = completed RK updates; *fate = BH_FATE_*. */
-static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_rk, uint32_t* fate) {
+/* get_col, :259-345.  Returns rgb; *n_rk = completed RK updates; *fate = BH_FATE_*;
+ * final_state (optional): ro, rd at exit. */
+static v3 get_col_state(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_rk, uint32_t* fate,
+                        float* final_state) {
     v3 ro = ro0, rd = rd0;
     v3 c = cross(ro, rd);                       /* :262 */
     float h2 = dot(c, c);                       /* :263 */
@@ -158,17 +160,19 @@ static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_r
     v3 cps = muls(muls(mk(-nro0.x, -nro0.y, -nro0.z), 1.5f), P->RS); /* :294, (-n * 1.5) * RS */
     uint32_t i;
     *fate = BH_FATE_CAP;
+#define FINAL() do { if (final_state) { final_state[0] = ro.x; final_state[1] = ro.y; final_state[2] = ro.z; \
+                     final_state[3] = rd.x; final_state[4] = rd.y; final_state[5] = rd.z; } } while (0)
     for (i = 0; i < P->max_iters; i++) {        /* :266 */
         float r = len(ro);                      /* :271 */
         if (P->BLACKOUT_EH != 0u) {             /* :272-283 */
             if (r < 1.0f) {
-                if (dot(rd, ro) < 0.0f) { *n_rk = i; *fate = BH_FATE_BLACKOUT; return mk(0, 0, 0); }
+                if (dot(rd, ro) < 0.0f) { *n_rk = i; *fate = BH_FATE_BLACKOUT; FINAL(); return mk(0, 0, 0); }
             }
             if (r > 1.0f) outside = 1;
-            else if (outside) { *n_rk = i; *fate = BH_FATE_BLACKOUT; return mk(0, 0, 0); }
+            else if (outside) { *n_rk = i; *fate = BH_FATE_BLACKOUT; FINAL(); return mk(0, 0, 0); }
         }
         float ds = sdf(P, ro);                  /* :285 */
-        if (ds < MIN_DIST) { *n_rk = i; *fate = BH_FATE_SURFACE; return mk(1, 1, 1); } /* :286-288 */
+        if (ds < MIN_DIST) { *n_rk = i; *fate = BH_FATE_SURFACE; FINAL(); return mk(1, 1, 1); } /* :286-288 */
         float dps = sdf_sphere(ro, cps, 0.075f);/* :294 */
         float dist = fminf(ds, dps);            /* :299 */
         float dd = P->DTM * r;                  /* :307 */
@@ -181,6 +185,8 @@ static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_r
         if (distance_travelled > P->MAX_DIST) { i++; *fate = BH_FATE_ESCAPE; break; } /* :325-327 */
     }
     *n_rk = i;
+    FINAL();
+#undef FINAL
     v3 n = normalize(rd);                                       /* :330 */
     float az = (float)atan2((double)n.z, (double)n.x);          /* :332 */
     float x = (az + ONE_PI) / TWO_PI;                           /* :334 */
@@ -189,6 +195,9 @@ static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_r
     col.y = pow15(col.y);                                       /* :342 */
     col.z = pow15(col.z);                                       /* :343 */
     return col;
+}
+static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_rk, uint32_t* fate) {
+    return get_col_state(P, S, ro0, rd0, n_rk, fate, 0);
 }
 
 /* sRGB -> linear decode of an 8-bit unorm (Rgba8UnormSrgb), computed in double. */
@@ -302,18 +311,19 @@ int bho_trace_pixel(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     return 0;
 }
 
-/* Integrate one explicit ray (ro0, rd0 not necessarily from a camera) — physics KATs. */
+/* Integrate one explicit ray (ro0, rd0 not necessarily from a camera) — physics KATs.
+ * out_state (optional, 6 floats): final ro, rd. */
 int bho_trace_ray(const float ro0_in[3], const float rd0_in[3], const bh_uniforms* U,
                   const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, uint32_t max_iters,
-                  uint32_t scene_flags, float out_rgb[3], uint32_t* n_rk, uint32_t* fate) {
+                  uint32_t scene_flags, float out_rgb[3], uint32_t* n_rk, uint32_t* fate, float* out_state) {
     params P;
     P.RS = U->rs; P.DTM = U->delta_time_mult; P.MAX_DIST = U->max_dist; P.DP = U->distortion_power;
     P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters;
     sky_t S;
     S.tex = sky; S.w = sky_w; S.h = sky_h;
     bho_srgb_lut(S.lut);
-    v3 col = get_col(&P, &S, mk(ro0_in[0], ro0_in[1], ro0_in[2]), mk(rd0_in[0], rd0_in[1], rd0_in[2]),
-                     n_rk, fate);
+    v3 col = get_col_state(&P, &S, mk(ro0_in[0], ro0_in[1], ro0_in[2]), mk(rd0_in[0], rd0_in[1], rd0_in[2]),
+                           n_rk, fate, out_state);
     out_rgb[0] = col.x; out_rgb[1] = col.y; out_rgb[2] = col.z;
     return 0;
 }

@@ -8,12 +8,15 @@ CAMERAS = {
     "B": ((0.0, 3.0, -20.0), (0.0, 0.0, 0.0)),
     "C": ((0.0, 6.0, -12.0), (0.0, 0.0, 0.0)),
     "D": ((7.0, 1.5, -9.0), (0.0, 0.0, 0.0)),    # off-axis, close: many disc/photon-sphere rays
+    "E": ((0.0, 0.0, -20.0), (2.6, 0.0, 0.0), 0.1),  # zoom on the shadow edge: capped "Zeno" rays
 }
 
 
 def camera_uniform(name: str, width: int, height: int) -> bh.CameraUniform:
     spec = CAMERAS[name]
     cam = bh.Camera.default(width, height) if spec is None else bh.Camera.look_at(spec[0], spec[1], width, height)
+    if spec is not None and len(spec) > 2:
+        cam.fovy = spec[2]
     cu = bh.CameraUniform()
     cu.update(cam)
     return cu

@@ -93,6 +93,8 @@ CASES = [
     ("C", 80, 48, 512, 3, {"rs": 1.4, "delta_time_mult": 0.3, "max_dist": 60.0}),
     ("A", 64, 40, 512, 1, {}),                    # disc only
     ("A", 64, 40, 512, 2, {}),                    # markers only
+    ("E", 48, 32, 512, 3, {}),                    # shadow-edge zoom: capped "Zeno" rays
+    ("E", 64, 40, 1000, 3, {"blackout_eh": 0}),   # ... without blackout (rays reach r ~ 0)
 ]
 
 
@@ -208,3 +210,31 @@ def test_invalid_arguments_fail_loudly(torch_cuda, scene_small):
     with pytest.raises(bh.BhError):
         scene_small.render(out, None, width=8, height=8)
     scene_small.camera_uniform = old
+
+
+GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("*.npz"))
+
+
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
+def test_exact_matches_golden_fixtures(torch_cuda, path, schedule):
+    torch = torch_cuda
+    z = np.load(path)
+    W, H, cap, flags = (int(v) for v in z["meta"])
+    scene = bh.Scene(W, H, sky=z["sky"], max_iters=cap, scene_flags=flags, math=bh.BH_MATH_EXACT)
+    cu = bh.CameraUniform()
+    C = __import__("ctypes")
+    C.memmove(C.addressof(cu.c), z["camera_uniform"].tobytes(), 112)
+    scene.camera_uniform = cu
+    u = bh._abi.bh_uniforms.from_buffer_copy(z["uniforms"].tobytes())
+    scene.uniforms = bh.Uniforms(u.rs, u.delta_time_mult, u.bg_brightness, u.blackout_eh, u.max_dist,
+                                 u.distortion_power)
+    col = torch.full((H, W, 4), float("nan"), device="cuda")
+    nrk = torch.zeros((H, W), dtype=torch.int16, device="cuda")
+    fate = torch.full((H, W), 0xFF, dtype=torch.uint8, device="cuda")
+    scene.render(col, None, dbg_n_rk=nrk, dbg_fate=fate, schedule=schedule)
+    torch.cuda.synchronize()
+    assert np.array_equal(fate.cpu().numpy(), z["fate"])
+    assert np.array_equal(nrk.cpu().numpy().view(np.uint16), z["n_rk"])
+    assert np.array_equal(col.cpu().numpy().view(np.uint32), z["col"].view(np.uint32))
+    scene.close()
