@@ -294,7 +294,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
     if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES) return BH_ERR_INVALID_ARG;
-    if (d->schedule > BH_SCHED_TILE) return BH_ERR_INVALID_ARG;
+    if (d->schedule > BH_SCHED_PERSISTENT) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;

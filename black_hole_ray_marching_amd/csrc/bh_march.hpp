@@ -179,43 +179,37 @@ struct RayState {
     bool outside;
 };
 
+// ---- one RK iteration, branch-free ---------------------------------------------------------------
+//
+// Ops supplies sqrt / length / sdf / rd_derivative / x/6 for the math mode:
+//   exact: XOps<true>  correctly rounded cores + domain guard (bh_crmath.hpp);
+//          XOps<false> plain IEEE ops (the guard's fallback);  both = the oracle's arithmetic;
+//   fast:  FOps        hardware rsq / sqrt, FMA contraction.
+// The early exits of the loop body (:272-288) are predicates and the state update is a select, so a
+// whole iteration is one basic block: the pair schedule interleaves two rays' iterations and the
+// scheduler fills each ray's dependency stalls with the other's instructions.
+
 #if BH_FAST
-// One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
-// iteration (n_rk counts completed RK updates), or 0xFF if it continues.
-__device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
-    v3 ro = st.ro, rd = st.rd;
-    const float r = len(ro);                            // :271
-    if (a.blackout_eh != 0u) {                          // :272-283
-        if (r < 1.0f && dot(rd, ro) < 0.0f) return BH_FATE_BLACKOUT;
-        if (r > 1.0f) st.outside = true;
-        else if (st.outside) return BH_FATE_BLACKOUT;
+struct FOps {
+    bool bad = false;  // no guard in fast mode
+    __device__ __forceinline__ float sqrt(float x) { return __builtin_sqrtf(x); }  // v_sqrt_f32 here
+    __device__ __forceinline__ float length(v3 p) { return __builtin_sqrtf(dot(p, p)); }
+    __device__ __forceinline__ v3 div6(v3 x) { return muls(x, 1.0f / 6.0f); }
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
+        const float iq = rsq(q), iq2 = iq * iq;
+        return muls(p, s * (iq2 * iq2 * iq));
     }
-    const float ds = sdf(ro, a.rs, a.scene_flags);      // :285
-    if (ds < MIN_DIST) return BH_FATE_SURFACE;          // :286-288
-    const float dps = len(sub(f.cps, ro)) - 0.075f;     // :294
-    const float dist = fminf(ds, dps);                  // :299
-    const float dt = fminf(dist * 0.9f, a.dtm * r);     // :307-310
-    const float s = st.s;
-    // get_delta_photon_rk4 (:134-151)
-    v3 ro_k1 = smul(dt, rd);
-    v3 rd_k1 = smul(dt, accel(ro, s));
-    v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
-    v3 rd_k2 = smul(dt, accel(add(ro, smul(0.5f, ro_k1)), s));
-    v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
-    v3 rd_k3 = smul(dt, accel(add(ro, smul(0.5f, ro_k2)), s));
-    v3 ro_k4 = smul(dt, add(rd, rd_k3));
-    v3 rd_k4 = smul(dt, accel(add(ro, ro_k3), s));
-    constexpr float SIXTH = 1.0f / 6.0f;
-    v3 dro = muls(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4), SIXTH);
-    v3 drd = muls(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4), SIXTH);
-    st.ro = add(ro, dro);                               // :315
-    st.rd = add(rd, drd);                               // :322
-    st.travelled += dt;                                 // :324
-    st.n_rk += 1u;
-    if (st.travelled > a.max_dist) return BH_FATE_ESCAPE;  // :325-327
-    if (st.n_rk >= a.max_iters) return BH_FATE_CAP;        // loop exhausted (:266)
-    return 0xFFu;
-}
+    __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs(p, s, dot(p, p), 0.0f); }
+    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
+        const float rho = __builtin_sqrtf(p.x * p.x + p.z * p.z);
+        const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y) - 0.02f);
+        // min of the four sphere SDFs == sqrt(min of squared distances) - 0.5 (sqrt is monotone)
+        const float ay = fabsf(p.y) - 10.0f, ax = fabsf(p.x) - 10.0f, dz = p.z + 10.0f;
+        const float m = __builtin_sqrtf(fminf(p.x * p.x + ay * ay, ax * ax + p.y * p.y) + dz * dz) - 0.5f;
+        return (flags == BH_SCENE_DEFAULT) ? fminf(disc, m)
+             : (flags == BH_SCENE_DISC) ? disc : (flags == BH_SCENE_MARKERS) ? m : __builtin_inff();
+    }
+};
 #else
 // Exact mode.  The arithmetic is the normative op sequence of oracle/bh_oracle.c: every rounding
 // the same as IEEE f32 evaluated in WGSL source order.  CR = true evaluates the divisions and
@@ -224,12 +218,13 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
 // produce identical bits wherever `bad` stays false.
 template <bool CR>
 struct XOps {
+    static constexpr bool kCR = CR;
     bool bad = false;
     // running unsigned min of crm::key() over every division numerator: zeros map high (the cores
     // are exact for them; camera-A rays start on two coordinate planes), tiny values low
     uint32_t kmin = 0xFFFFFFFFu;
-    __device__ __forceinline__ float sqrt(float x) {
-        if constexpr (CR) { bad |= crm::sqrt_bad(x); return crm::sqrt_core(x); }
+    __device__ __forceinline__ float sqrt(float x, bool used = true) {
+        if constexpr (CR) { bad |= used && crm::sqrt_bad(x); return crm::sqrt_core(x); }
         else return __builtin_sqrtf(x);
     }
     __device__ __forceinline__ v3 div6(v3 x) {
@@ -261,77 +256,82 @@ struct XOps {
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
     __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
-        float d = __builtin_inff();
-        if (flags & BH_SCENE_DISC) {
-            const float rho = sqrt(p.x * p.x + p.z * p.z);
-            d = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
-        }
-        if (flags & BH_SCENE_MARKERS) {
-            const float xx = p.x * p.x, yy = p.y * p.y;
-            const float dz = -10.0f - p.z, zz = dz * dz;
-            const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
-            const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
-            const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
-            const float m = sqrt(fminf(q1, fminf(q2, fminf(q3, q4)))) - 0.5f;
-            d = (flags & BH_SCENE_DISC) ? fminf(d, m) : m;
-        }
-        return d;
+        const float rho = sqrt(p.x * p.x + p.z * p.z, (flags & BH_SCENE_DISC) != 0u);
+        const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
+        const float xx = p.x * p.x, yy = p.y * p.y;
+        const float dz = -10.0f - p.z, zz = dz * dz;
+        const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
+        const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
+        const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
+        const float m = sqrt(fminf(q1, fminf(q2, fminf(q3, q4))), (flags & BH_SCENE_MARKERS) != 0u) - 0.5f;
+        return (flags == BH_SCENE_DEFAULT) ? fminf(disc, m)
+             : (flags == BH_SCENE_DISC) ? disc : (flags == BH_SCENE_MARKERS) ? m : __builtin_inff();
     }
 };
+#endif
 
-template <bool CR>
-__device__ __forceinline__ uint32_t march_step_x(const MarchArgs& a, const Frame& f, RayState& st, XOps<CR>& X) {
+// One iteration of the loop body (:266-328) on `st`.  Returns BH_FATE_* if the ray terminates in
+// this iteration (state then unchanged except `outside`; n_rk counts completed RK updates), or
+// 0xFF if it continues.
+template <class Ops>
+__device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, RayState& st, Ops& X) {
     const v3 ro = st.ro, rd = st.rd;
     const float r2 = dot(ro, ro);
-    const float r = X.sqrt(r2);                         // :271
-    if (a.blackout_eh != 0u) {                          // :272-283
-        if (r < 1.0f && dot(rd, ro) < 0.0f) return BH_FATE_BLACKOUT;
-        if (r > 1.0f) st.outside = true;
-        else if (st.outside) return BH_FATE_BLACKOUT;
-    }
-    const float ds = X.sdf(ro, a.rs, a.scene_flags);    // :285
-    if (ds < MIN_DIST) return BH_FATE_SURFACE;          // :286-288
-    const float dps = X.length(sub(f.cps, ro)) - 0.075f;  // :294
-    const float dist = fminf(ds, dps);                  // :299
-    const float dt = fminf(dist * 0.9f, a.dtm * r);     // :307-310
+    const float r = X.sqrt(r2);                                        // :271
+    // :272-283
+    const bool bo_on = a.blackout_eh != 0u;
+    const bool out_now = r > 1.0f;
+    const bool blackout = bo_on && ((r < 1.0f && dot(rd, ro) < 0.0f) || (!out_now && st.outside));
+    st.outside = st.outside || out_now;                                // only read when bo_on
+    const float ds = X.sdf(ro, a.rs, a.scene_flags);                   // :285
+    const uint32_t pre = blackout ? BH_FATE_BLACKOUT : (ds < MIN_DIST ? BH_FATE_SURFACE : 0xFFu);  // :286-288
+    const float dps = X.length(sub(f.cps, ro)) - 0.075f;               // :294
+    const float dist = fminf(ds, dps);                                 // :299
+    const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
     const float s = st.s;
     // get_delta_photon_rk4 (:134-151)
-    v3 ro_k1 = smul(dt, rd);
-    v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r));
-    v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
-    v3 rd_k2 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k1)), s));
-    v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
-    v3 rd_k3 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k2)), s));
-    v3 ro_k4 = smul(dt, add(rd, rd_k3));
-    v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
-    const v3 nro = add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4);
-    const v3 nrd = add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4);
-    const v3 dro = X.div6(nro);
-    const v3 drd = X.div6(nrd);
-    st.ro = add(ro, dro);                               // :315
-    st.rd = add(rd, drd);                               // :322
-    st.travelled += dt;                                 // :324
-    if constexpr (CR) {
+    const v3 ro_k1 = smul(dt, rd);
+    const v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r));
+    const v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
+    const v3 rd_k2 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k1)), s));
+    const v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
+    const v3 rd_k3 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k2)), s));
+    const v3 ro_k4 = smul(dt, add(rd, rd_k3));
+    const v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
+    const v3 dro = X.div6(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4));
+    const v3 drd = X.div6(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4));
+#if !BH_FAST
+    if constexpr (Ops::kCR) {
         // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
         // |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds every |s*p_i| <= 2^42.
         X.bad |= X.kmin < crm::KEY_MIN;
         X.bad |= !(fabsf(s) <= 0x1p30f);
     }
-    st.n_rk += 1u;
-    if (st.travelled > a.max_dist) return BH_FATE_ESCAPE;  // :325-327
-    if (st.n_rk >= a.max_iters) return BH_FATE_CAP;        // loop exhausted (:266)
-    return 0xFFu;
+#endif
+    const bool go = pre == 0xFFu;
+    const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
+    const float ntr = st.travelled + dt;                               // :324
+    st.ro = go ? nro : ro;
+    st.rd = go ? nrd : rd;
+    st.travelled = go ? ntr : st.travelled;
+    st.n_rk += go ? 1u : 0u;
+    return !go ? pre : (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE     // :325-327
+                     : (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
 }
 
-// One iteration of the loop body (:266-328).  Returns BH_FATE_* if the ray terminated in this
-// iteration (n_rk counts completed RK updates), or 0xFF if it continues.
 #ifdef BH_DIAG_SLOW
 __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 #endif
+
+// One iteration for one ray (tile / persistent schedules).
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
+#if BH_FAST
+    FOps X;
+    return step_bf(a, f, st, X);
+#else
     RayState t = st;
     XOps<true> X;
-    uint32_t fate = march_step_x<true>(a, f, t, X);
+    uint32_t fate = step_bf(a, f, t, X);
     const uint64_t badm = __ballot(X.bad);
     if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
 #ifdef BH_DIAG_SLOW
@@ -343,13 +343,36 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
         if (X.bad) {
             t = st;
             XOps<false> Y;
-            fate = march_step_x<false>(a, f, t, Y);
+            fate = step_bf(a, f, t, Y);
         }
     }
     st = t;
     return fate;
-}
 #endif
+}
+
+// One iteration for two independent rays of the same lane (pair schedule).  Dead rays (alive_k
+// false) are computed on their frozen state and discarded, so the two iterations stay one block.
+__device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, RayState& s0, RayState& s1,
+                                            bool& alive0, bool& alive1, uint32_t& fate0, uint32_t& fate1) {
+    RayState t0 = s0, t1 = s1;
+#if BH_FAST
+    FOps X0, X1;
+    uint32_t f0 = step_bf(a, f, t0, X0);
+    uint32_t f1 = step_bf(a, f, t1, X1);
+#else
+    XOps<true> X0, X1;
+    uint32_t f0 = step_bf(a, f, t0, X0);
+    uint32_t f1 = step_bf(a, f, t1, X1);
+    const bool bad0 = X0.bad && alive0, bad1 = X1.bad && alive1;
+    if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
+        if (bad0) { t0 = s0; XOps<false> Y; f0 = step_bf(a, f, t0, Y); }
+        if (bad1) { t1 = s1; XOps<false> Y; f1 = step_bf(a, f, t1, Y); }
+    }
+#endif
+    if (alive0) { s0 = t0; if (f0 != 0xFFu) { fate0 = f0; alive0 = false; } }
+    if (alive1) { s1 = t1; if (f1 != 0xFFu) { fate1 = f1; alive1 = false; } }
+}
 
 // Colour of a finished ray (:329-345 for sky rays; :275/:281 blackout -> 0; :287 surface -> 1).
 __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32_t fate, v3 rd) {
@@ -553,6 +576,47 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
         const v3 col = shade(a, lut, meta >> 16, mk(Q.d_x[lane], Q.d_y[lane], Q.d_z[lane]));
         write_pixel(a, Q.d_idx[lane], col, meta & 0xFFFFu, meta >> 16);
     }
+}
+
+// ---- schedule 2: two rays per lane (default) ----------------------------------------------------
+// One wave64 = two consecutive shard-local 8x8 tiles; each lane marches the pixel at the same (x&7,
+// y&7) position in both (8 px apart for an unsharded frame: coherent step counts) and the loop body
+// interleaves the two rays' iterations: on gfx950 one dependent chain per wave issues only every
+// ~4-5 cycles however many waves share the SIMD, two chains reach the ~2.3-cycle peak
+// (tools/ubench/latency.hip).
+__global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
+    __shared__ float lut[256];
+    lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t pair = blockIdx.x * 4u + (threadIdx.x >> 6);
+    const uint32_t t0 = 2u * pair, t1 = t0 + 1u;
+    if (t0 >= a.n_tiles) return;
+    const Frame f = make_frame(a);
+    uint32_t px0 = 0, py0 = 0, px1 = 0, py1 = 0;
+    {
+        uint32_t tx, ty;
+        shard_tile_coords(t0, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
+        px0 = tx * 8u + (lane & 7u); py0 = ty * 8u + (lane >> 3);
+        if (t1 < a.n_tiles) {
+            shard_tile_coords(t1, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
+            px1 = tx * 8u + (lane & 7u); py1 = ty * 8u + (lane >> 3);
+        }
+    }
+    bool alive0 = px0 < a.width && py0 < a.height;
+    bool alive1 = t1 < a.n_tiles && px1 < a.width && py1 < a.height;
+    const bool valid0 = alive0, valid1 = alive1;
+    RayState s0, s1;
+    s0.ro = f.ro0; s0.travelled = 0.0f; s0.n_rk = 0; s0.outside = false;
+    s1 = s0;
+    s0.rd = valid0 ? pixel_ray(a, px0, py0) : f.ro0;
+    s1.rd = valid1 ? pixel_ray(a, px1, py1) : f.ro0;
+    s0.s = ray_s(f, s0.rd);
+    s1.s = ray_s(f, s1.rd);
+    uint32_t fate0 = BH_FATE_CAP, fate1 = BH_FATE_CAP;
+    while (alive0 || alive1) march_step2(a, f, s0, s1, alive0, alive1, fate0, fate1);
+    if (valid0) write_pixel(a, out_index(a, t0, lane, px0, py0), shade(a, lut, fate0, s0.rd), s0.n_rk, fate0);
+    if (valid1) write_pixel(a, out_index(a, t1, lane, px1, py1), shade(a, lut, fate1, s1.rd), s1.n_rk, fate1);
 }
 
 }  // namespace BH_NS

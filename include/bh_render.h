@@ -116,8 +116,9 @@ typedef enum {
 
 /* Work schedule of the march kernel (same results, different speed). */
 typedef enum {
-    BH_SCHED_PERSISTENT = 0, /* resident waves, per-lane refill from an LDS ray queue (default) */
-    BH_SCHED_TILE = 1        /* one wave64 per 8x8 tile, exits when its slowest ray finishes */
+    BH_SCHED_PAIR = 0,       /* one wave64 per two 8x8 tiles, two interleaved rays per lane (default) */
+    BH_SCHED_TILE = 1,       /* one wave64 per 8x8 tile, exits when its slowest ray finishes */
+    BH_SCHED_PERSISTENT = 2  /* resident waves, per-lane refill from an LDS ray queue */
 } bh_schedule;
 
 /* Per-pixel fate codes written to dbg_fate. */

@@ -101,7 +101,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PERSISTENT, bh.BH_SCHED_TILE])
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
 @pytest.mark.parametrize("cam,W,H,cap,flags,over", CASES)
 def test_exact_bitexact(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over, schedule):
     cu, U = camera_uniform(cam, W, H), uniforms(**over)
@@ -145,7 +145,7 @@ def test_blackout_target_none(torch_cuda, scene_small, sky_small):
     assert np.array_equal(g[0].view(np.uint32), o[0].view(np.uint32))
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PERSISTENT, bh.BH_SCHED_TILE])
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
 @pytest.mark.parametrize("S", [1, 2, 3, 5, 8])
 def test_tiles_shards_unpack(torch_cuda, scene_small, S, schedule):
     torch = torch_cuda
@@ -221,7 +221,7 @@ def test_invalid_arguments_fail_loudly(torch_cuda, scene_small):
 GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("*.npz"))
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
 @pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
 def test_exact_matches_golden_fixtures(torch_cuda, path, schedule):
     torch = torch_cuda
