@@ -33,6 +33,8 @@ __device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, 
 __device__ __forceinline__ v3 smul(float s, v3 a) { return mk(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ v3 muls(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ float dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+// per-component select (an aggregate `c ? a : b` keeps the struct in scratch memory)
+__device__ __forceinline__ v3 sel(bool c, v3 a, v3 b) { return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
 __device__ __forceinline__ v3 cross(v3 a, v3 b) {
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -192,8 +194,8 @@ struct RayState {
 #if BH_FAST
 struct FOps {
     bool bad = false;  // no guard in fast mode
-    __device__ __forceinline__ float sqrt(float x) { return __builtin_sqrtf(x); }  // v_sqrt_f32 here
-    __device__ __forceinline__ float length(v3 p) { return __builtin_sqrtf(dot(p, p)); }
+    __device__ __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }  // raw v_sqrt_f32
+    __device__ __forceinline__ float length(v3 p) { return __builtin_amdgcn_sqrtf(dot(p, p)); }
     __device__ __forceinline__ v3 div6(v3 x) { return muls(x, 1.0f / 6.0f); }
     __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
         const float iq = rsq(q), iq2 = iq * iq;
@@ -201,13 +203,13 @@ struct FOps {
     }
     __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs(p, s, dot(p, p), 0.0f); }
     __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
-        const float rho = __builtin_sqrtf(p.x * p.x + p.z * p.z);
+        const float rho = __builtin_amdgcn_sqrtf(p.x * p.x + p.z * p.z);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y) - 0.02f);
         // min of the four sphere SDFs == sqrt(min of squared distances) - 0.5 (sqrt is monotone)
         const float ay = fabsf(p.y) - 10.0f, ax = fabsf(p.x) - 10.0f, dz = p.z + 10.0f;
-        const float m = __builtin_sqrtf(fminf(p.x * p.x + ay * ay, ax * ax + p.y * p.y) + dz * dz) - 0.5f;
-        return (flags == BH_SCENE_DEFAULT) ? fminf(disc, m)
-             : (flags == BH_SCENE_DISC) ? disc : (flags == BH_SCENE_MARKERS) ? m : __builtin_inff();
+        const float m = __builtin_amdgcn_sqrtf(fminf(p.x * p.x + ay * ay, ax * ax + p.y * p.y) + dz * dz) - 0.5f;
+        return fminf((flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
+                     (flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
     }
 };
 #else
@@ -224,7 +226,7 @@ struct XOps {
     // are exact for them; camera-A rays start on two coordinate planes), tiny values low
     uint32_t kmin = 0xFFFFFFFFu;
     __device__ __forceinline__ float sqrt(float x, bool used = true) {
-        if constexpr (CR) { bad |= used && crm::sqrt_bad(x); return crm::sqrt_core(x); }
+        if constexpr (CR) { bad |= used & crm::sqrt_bad(x); return crm::sqrt_core(x); }
         else return __builtin_sqrtf(x);
     }
     __device__ __forceinline__ v3 div6(v3 x) {
@@ -264,8 +266,9 @@ struct XOps {
         const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
         const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
         const float m = sqrt(fminf(q1, fminf(q2, fminf(q3, q4))), (flags & BH_SCENE_MARKERS) != 0u) - 0.5f;
-        return (flags == BH_SCENE_DEFAULT) ? fminf(disc, m)
-             : (flags == BH_SCENE_DISC) ? disc : (flags == BH_SCENE_MARKERS) ? m : __builtin_inff();
+        // fminf(disc, inf) == disc and fminf(inf, m) == m bit for bit: same result as selecting
+        return fminf((flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
+                     (flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
     }
 };
 #endif
@@ -279,12 +282,14 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const float r2 = dot(ro, ro);
     const float r = X.sqrt(r2);                                        // :271
     // :272-283
+    // bitwise (not short-circuit) logic keeps the iteration one basic block
     const bool bo_on = a.blackout_eh != 0u;
     const bool out_now = r > 1.0f;
-    const bool blackout = bo_on && ((r < 1.0f && dot(rd, ro) < 0.0f) || (!out_now && st.outside));
-    st.outside = st.outside || out_now;                                // only read when bo_on
+    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | ((!out_now) & st.outside));
+    st.outside = st.outside | out_now;                                 // only read when bo_on
     const float ds = X.sdf(ro, a.rs, a.scene_flags);                   // :285
-    const uint32_t pre = blackout ? BH_FATE_BLACKOUT : (ds < MIN_DIST ? BH_FATE_SURFACE : 0xFFu);  // :286-288
+    uint32_t pre = (ds < MIN_DIST) ? (uint32_t)BH_FATE_SURFACE : 0xFFu;   // :286-288
+    pre = blackout ? (uint32_t)BH_FATE_BLACKOUT : pre;
     const float dps = X.length(sub(f.cps, ro)) - 0.075f;               // :294
     const float dist = fminf(ds, dps);                                 // :299
     const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
@@ -311,12 +316,14 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const bool go = pre == 0xFFu;
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
     const float ntr = st.travelled + dt;                               // :324
-    st.ro = go ? nro : ro;
-    st.rd = go ? nrd : rd;
+    st.ro = sel(go, nro, ro);
+    st.rd = sel(go, nrd, rd);
     st.travelled = go ? ntr : st.travelled;
     st.n_rk += go ? 1u : 0u;
-    return !go ? pre : (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE     // :325-327
-                     : (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
+    // flat selects (a nested ?: becomes exec-mask branches)
+    uint32_t fate = (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
+    fate = (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;              // :325-327
+    return go ? fate : pre;
 }
 
 #ifdef BH_DIAG_SLOW
@@ -364,14 +371,24 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
     XOps<true> X0, X1;
     uint32_t f0 = step_bf(a, f, t0, X0);
     uint32_t f1 = step_bf(a, f, t1, X1);
-    const bool bad0 = X0.bad && alive0, bad1 = X1.bad && alive1;
+    const bool bad0 = X0.bad & alive0, bad1 = X1.bad & alive1;
     if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
         if (bad0) { t0 = s0; XOps<false> Y; f0 = step_bf(a, f, t0, Y); }
         if (bad1) { t1 = s1; XOps<false> Y; f1 = step_bf(a, f, t1, Y); }
     }
 #endif
-    if (alive0) { s0 = t0; if (f0 != 0xFFu) { fate0 = f0; alive0 = false; } }
-    if (alive1) { s1 = t1; if (f1 != 0xFFu) { fate1 = f1; alive1 = false; } }
+    // selects, not branches
+    s0.ro = sel(alive0, t0.ro, s0.ro); s0.rd = sel(alive0, t0.rd, s0.rd);
+    s0.travelled = alive0 ? t0.travelled : s0.travelled; s0.n_rk = alive0 ? t0.n_rk : s0.n_rk;
+    s0.outside = alive0 ? t0.outside : s0.outside;
+    s1.ro = sel(alive1, t1.ro, s1.ro); s1.rd = sel(alive1, t1.rd, s1.rd);
+    s1.travelled = alive1 ? t1.travelled : s1.travelled; s1.n_rk = alive1 ? t1.n_rk : s1.n_rk;
+    s1.outside = alive1 ? t1.outside : s1.outside;
+    const bool e0 = alive0 & (f0 != 0xFFu), e1 = alive1 & (f1 != 0xFFu);
+    fate0 = e0 ? f0 : fate0;
+    fate1 = e1 ? f1 : fate1;
+    alive0 = alive0 & !e0;
+    alive1 = alive1 & !e1;
 }
 
 // Colour of a finished ray (:329-345 for sky rays; :275/:281 blackout -> 0; :287 surface -> 1).
@@ -609,8 +626,8 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
     RayState s0, s1;
     s0.ro = f.ro0; s0.travelled = 0.0f; s0.n_rk = 0; s0.outside = false;
     s1 = s0;
-    s0.rd = valid0 ? pixel_ray(a, px0, py0) : f.ro0;
-    s1.rd = valid1 ? pixel_ray(a, px1, py1) : f.ro0;
+    s0.rd = sel(valid0, pixel_ray(a, px0, py0), f.ro0);
+    s1.rd = sel(valid1, pixel_ray(a, px1, py1), f.ro0);
     s0.s = ray_s(f, s0.rd);
     s1.s = ray_s(f, s1.rd);
     uint32_t fate0 = BH_FATE_CAP, fate1 = BH_FATE_CAP;
