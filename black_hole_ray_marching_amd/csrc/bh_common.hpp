@@ -21,6 +21,8 @@ struct MarchArgs {
     uint32_t shard_index, shard_count;
     uint32_t tiles_x, tiles_y;
     uint32_t n_tiles;          // tiles owned by this shard (= grid work items)
+    uint32_t order_block;      // centre-out dispatch: shard-local tiles permuted in blocks of this
+    uint32_t order_centre;     //   many tiles (~ one tile row), starting at block order_centre
     // sky (Rgba8UnormSrgb texels as packed u32, little endian: r | g<<8 | b<<16 | a<<24)
     const uint32_t* sky;
     const float* srgb_lut;     // 256 entries, sRGB byte -> linear
@@ -70,6 +72,26 @@ __host__ __device__ inline void shard_tile_coords(uint32_t t, uint32_t tiles_x, 
     }
     *ty = row;
     *tx = shard_row_start(row, k, S) + rem * S;
+}
+
+// Centre-out dispatch order (a bijection of [0, n)): the shard-local tile range is cut into blocks
+// of L tiles (~ one tile row); block slot k of the dispatch takes block c, c+1, c-1, c+2, c-2, ...
+// (clipped to the range) and the partial tail block stays last.  c is the block holding the black
+// hole's projected screen row, so the photon-ring tiles -- where the capped "Zeno" rays that run
+// the full 512-step chain live -- start first and their serial chains overlap the rest of the frame.
+// Only the order changes, never a result.
+__host__ __device__ inline uint32_t centre_out(uint32_t b, uint32_t n, uint32_t L, uint32_t c) {
+    if (L == 0u) return b;
+    const uint32_t nb = n / L;
+    const uint32_t j = b / L, i = b - j * L;
+    if (j >= nb) return b;
+    if (c >= nb) c = nb - 1u;
+    const uint32_t m = c < nb - 1u - c ? c : nb - 1u - c;  // full pairs on both sides
+    uint32_t J;
+    if (j == 0u) J = c;
+    else if (j <= 2u * m) J = (j & 1u) ? c + (j + 1u) / 2u : c - j / 2u;
+    else J = (c - m == 0u) ? c + m + (j - 2u * m) : c - m - (j - 2u * m);
+    return J * L + i;
 }
 
 }  // namespace bh

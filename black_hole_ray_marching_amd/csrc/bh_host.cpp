@@ -49,6 +49,30 @@ void srgb_lut(float lut[256]) {
     }
 }
 
+// Screen row (in tiles) of the black hole's projection: solve C1 + l0 (C0 - C1) + l2 (C2 - C1) = -t ro0
+// (t > 0) for the barycentrics of the pixel looking at the origin; py = 2 H l2 - 0.5.  Falls back to
+// the middle row when the origin is behind the camera or the system is degenerate.
+uint32_t bh_tile_row(const bh_camera_uniform* c, uint32_t height) {
+    const double C0[3] = {c->world_tri[0][0], c->world_tri[0][1], c->world_tri[0][2]};
+    const double C1[3] = {c->world_tri[1][0], c->world_tri[1][1], c->world_tri[1][2]};
+    const double C2[3] = {c->world_tri[2][0], c->world_tri[2][1], c->world_tri[2][2]};
+    const double A[3] = {C0[0] - C1[0], C0[1] - C1[1], C0[2] - C1[2]};
+    const double B[3] = {C2[0] - C1[0], C2[1] - C1[1], C2[2] - C1[2]};
+    const double P[3] = {c->pos[0], c->pos[1], c->pos[2]};  // l0 A + l2 B + t P = -C1
+    auto det3 = [](const double* x, const double* y, const double* z) {
+        return x[0] * (y[1] * z[2] - y[2] * z[1]) - y[0] * (x[1] * z[2] - x[2] * z[1]) + z[0] * (x[1] * y[2] - x[2] * y[1]);
+    };
+    const double R[3] = {-C1[0], -C1[1], -C1[2]};
+    const double D = det3(A, B, P);
+    const uint32_t tiles_y = (height + 7u) / 8u;
+    if (std::fabs(D) < 1e-12) return tiles_y / 2u;
+    const double l2 = det3(A, R, P) / D, t = det3(A, B, R) / D;
+    if (!(t > 0.0)) return tiles_y / 2u;
+    double py = 2.0 * height * l2 - 0.5;
+    py = py < 0.0 ? 0.0 : (py > height - 1.0 ? height - 1.0 : py);
+    return (uint32_t)(py / 8.0);
+}
+
 bool screen_tri_default(const bh_camera_uniform* c) {
     static const float st[3][2] = {{3.0f, 1.0f}, {-1.0f, 1.0f}, {-1.0f, -3.0f}};
     for (int i = 0; i < 3; ++i)
@@ -318,6 +342,9 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     const uint64_t nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
     if (nt > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
     a.n_tiles = (uint32_t)nt;
+    // centre-out dispatch blocks of ~one tile row of this shard, centred on the black hole's row
+    a.order_block = (uint32_t)((nt + a.tiles_y - 1u) / a.tiles_y);
+    a.order_centre = bh_tile_row(cam, d->height);
     a.sky = c->sky; a.srgb_lut = c->lut; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
     a.out_col = d->out_col; a.out_blackout = d->out_blackout;
     a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate;

@@ -442,14 +442,20 @@ __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint
     return (a.layout == BH_LAYOUT_TILES) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
 }
 
+// A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a photon-sphere
+// ray that may run to the cap: raise its issue priority so its serial chain is not stretched by the
+// SIMD's other waves (the tail of the frame, measured +34 % of kernel time at cap 512 vs cap 64).
+constexpr uint32_t PRIO_ITERS = 48;
+
 // ---- schedule 1: one wave64 = one 8x8 tile (simple reference schedule) ---------------------------
 __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     __shared__ float lut[256];
     lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t t = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (t >= a.n_tiles) return;
+    const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
+    if (slot >= a.n_tiles) return;
+    const uint32_t t = centre_out(slot, a.n_tiles, a.order_block, a.order_centre);
     uint32_t tx, ty;
     shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
     const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
@@ -463,7 +469,10 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     st.n_rk = 0;
     st.outside = false;
     uint32_t fate = 0xFFu;
-    while ((fate = march_step(a, f, st)) == 0xFFu) {}
+    for (uint32_t it = 0;; ++it) {
+        if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);  // it is wave-uniform
+        if ((fate = march_step(a, f, st)) != 0xFFu) break;
+    }
     write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate);
 }
 
@@ -607,8 +616,11 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t pair = blockIdx.x * 4u + (threadIdx.x >> 6);
-    const uint32_t t0 = 2u * pair, t1 = t0 + 1u;
-    if (t0 >= a.n_tiles) return;
+    const uint32_t npairs = (a.n_tiles + 1u) / 2u;
+    if (pair >= npairs) return;
+    // centre-out over pairs (block = half a tile row of pairs); tiles 2p, 2p+1 stay adjacent
+    const uint32_t pp = centre_out(pair, a.n_tiles / 2u, a.order_block / 2u, a.order_centre);
+    const uint32_t t0 = 2u * pp, t1 = t0 + 1u;
     const Frame f = make_frame(a);
     uint32_t px0 = 0, py0 = 0, px1 = 0, py1 = 0;
     {
@@ -631,7 +643,10 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
     s0.s = ray_s(f, s0.rd);
     s1.s = ray_s(f, s1.rd);
     uint32_t fate0 = BH_FATE_CAP, fate1 = BH_FATE_CAP;
-    while (alive0 || alive1) march_step2(a, f, s0, s1, alive0, alive1, fate0, fate1);
+    for (uint32_t it = 0; alive0 || alive1; ++it) {
+        if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);
+        march_step2(a, f, s0, s1, alive0, alive1, fate0, fate1);
+    }
     if (valid0) write_pixel(a, out_index(a, t0, lane, px0, py0), shade(a, lut, fate0, s0.rd), s0.n_rk, fate0);
     if (valid1) write_pixel(a, out_index(a, t1, lane, px1, py1), shade(a, lut, fate1, s1.rd), s1.n_rk, fate1);
 }
