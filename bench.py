@@ -41,7 +41,7 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
-    p.add_argument("--schedule", choices=["pair", "tile", "persistent"], default="pair")
+    p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
     p.add_argument("--fmt", choices=["rgba16f", "rgba32f"], default="rgba16f")
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--height", type=int, default=0)
@@ -81,7 +81,8 @@ def main() -> None:
     ch_dtype = torch.float16 if fmt == bh.BH_OUT_RGBA16F else torch.float32
     bpp = bh.BYTES_PER_PIXEL[fmt]
     math_mode = bh.BH_MATH_EXACT if args.math == "exact" else bh.BH_MATH_FAST
-    sched = {"pair": bh.BH_SCHED_PAIR, "tile": bh.BH_SCHED_TILE, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
+    sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
+             "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
 
     sky = bh.synthetic_sky(4096, 2048)
     scene = bh.Scene(W, H, sky=sky, device=local, max_iters=cap, math=math_mode)

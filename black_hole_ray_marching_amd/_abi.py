@@ -19,7 +19,8 @@ BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
 BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES = 0, 1
-BH_SCHED_PAIR, BH_SCHED_TILE, BH_SCHED_PERSISTENT = 0, 1, 2
+BH_SCHED_TILE, BH_SCHED_PAIR, BH_SCHED_PERSISTENT = 0, 1, 2
+BH_SCHED_FLAG_STATIC_ORDER = 0x100
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 

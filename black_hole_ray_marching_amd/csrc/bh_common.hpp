@@ -23,6 +23,12 @@ struct MarchArgs {
     uint32_t n_tiles;          // tiles owned by this shard (= grid work items)
     uint32_t order_block;      // centre-out dispatch: shard-local tiles permuted in blocks of this
     uint32_t order_centre;     //   many tiles (~ one tile row), starting at block order_centre
+    const uint32_t* order;     // optional dispatch order (slot -> shard-local tile), else centre-out
+    uint8_t* tile_cost;        // optional output: per shard-local tile, min(255, max n_rk / 2)
+    // per-frame invariants, computed on the host with the same correctly rounded f32 ops as the
+    // oracle: photon-sphere centre -normalize(ro0) * 1.5 * RS (:294) and (DP * RS) * -1.5 (:126)
+    float cps[3];
+    float kfac;
     // sky (Rgba8UnormSrgb texels as packed u32, little endian: r | g<<8 | b<<16 | a<<24)
     const uint32_t* sky;
     const float* srgb_lut;     // 256 entries, sRGB byte -> linear
@@ -96,6 +102,14 @@ __host__ __device__ inline uint32_t centre_out(uint32_t b, uint32_t n, uint32_t 
 
 }  // namespace bh
 
+namespace bh {
+// Dispatch-order buckets by the previous frame's per-tile cost (max n_rk / 2): expensive first.
+constexpr uint32_t ORDER_BUCKETS = 6;
+__host__ __device__ inline uint32_t cost_bucket(uint32_t c) {
+    return c >= 128u ? 0u : c >= 64u ? 1u : c >= 32u ? 2u : c >= 20u ? 3u : c >= 12u ? 4u : 5u;
+}
+}  // namespace bh
+
 // Launchers (defined in the .hip translation units).
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
                                                                          uint32_t* counters, uint32_t grid,
@@ -105,6 +119,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_fast(const 
                                                                         hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exact(void);
 extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_fast(void);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const uint8_t* cost, uint32_t n_tiles,
+                                                                         uint32_t block, uint32_t centre,
+                                                                         uint32_t* counters, uint32_t* order,
+                                                                         hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
                                       uint32_t shard_count, uint64_t shard_stride_tiles,
                                       uint32_t bytes_per_pixel, hipStream_t s);

@@ -20,6 +20,12 @@ struct bh_ctx {
     uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
+    // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order
+    uint8_t* tile_cost = nullptr;
+    uint32_t* order = nullptr;
+    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS words
+    uint64_t order_cap = 0;              // tiles the two buffers hold
+    uint64_t order_key = ~0ull;          // (width, height, shard) the costs belong to
 };
 
 namespace {
@@ -302,6 +308,9 @@ int bh_destroy(bh_ctx* c) {
     if (c->sky) (void)hipFree(c->sky);
     if (c->lut) (void)hipFree(c->lut);
     if (c->counters) (void)hipFree(c->counters);
+    if (c->tile_cost) (void)hipFree(c->tile_cost);
+    if (c->order) (void)hipFree(c->order);
+    if (c->order_counters) (void)hipFree(c->order_counters);
     (void)hipSetDevice(prev);
     delete c;
     return BH_OK;
@@ -318,7 +327,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
     if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES) return BH_ERR_INVALID_ARG;
-    if (d->schedule > BH_SCHED_PERSISTENT) return BH_ERR_INVALID_ARG;
+    if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER))) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
@@ -346,6 +355,15 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     a.order_block = (uint32_t)((nt + a.tiles_y - 1u) / a.tiles_y);
     a.order_centre = bh_tile_row(cam, d->height);
     a.sky = c->sky; a.srgb_lut = c->lut; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
+    // per-frame invariants with the oracle's op sequence (correctly rounded f32, no contraction):
+    // c_ps = ((-normalize(ro0)) * 1.5) * RS (src/black_hole_maybe.wgsl:294), k = (DP * RS) * -1.5 (:126)
+    {
+        const float x = a.pos[0], y = a.pos[1], z = a.pos[2];
+        const float len = std::sqrt((x * x + y * y) + z * z);
+        const float n[3] = {x / len, y / len, z / len};
+        for (int k = 0; k < 3; ++k) a.cps[k] = (-n[k] * 1.5f) * a.rs;
+        a.kfac = (a.dp * a.rs) * -1.5f;
+    }
     a.out_col = d->out_col; a.out_blackout = d->out_blackout;
     a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate;
     if (a.n_tiles == 0) return BH_OK;
@@ -354,8 +372,36 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     (void)hipGetDevice(&prev);
     if (prev != c->device) (void)hipSetDevice(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, d->schedule, c->counters, c->grid_exact, s)
-                                     : bh_launch_march_fast(a, d->schedule, c->counters, c->grid_fast, s);
+    const uint32_t sched = d->schedule & 0xFFu;
+    if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
+        // temporal order: (re)allocate on a new geometry (the only allocation bh_render ever makes:
+        // capture into a graph after one call per frame size), reset costs, build this frame's order
+        const uint64_t key = ((uint64_t)d->width << 40) ^ ((uint64_t)d->height << 20) ^
+                             ((uint64_t)d->shard_index << 8) ^ d->shard_count;
+        hipError_t he = hipSuccess;
+        if (key != c->order_key) {
+            if (nt > c->order_cap) {
+                if (c->tile_cost) (void)hipFree(c->tile_cost);
+                if (c->order) (void)hipFree(c->order);
+                c->tile_cost = nullptr; c->order = nullptr; c->order_cap = 0;
+                if ((he = hipMalloc(&c->tile_cost, nt)) == hipSuccess &&
+                    (he = hipMalloc(&c->order, nt * sizeof(uint32_t))) == hipSuccess)
+                    c->order_cap = nt;
+            }
+            if (he == hipSuccess && !c->order_counters)
+                he = hipMalloc(&c->order_counters, 2 * bh::ORDER_BUCKETS * sizeof(uint32_t));
+            if (he == hipSuccess) he = hipMemsetAsync(c->tile_cost, 0, nt, s);
+            if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order buffers"); }
+            c->order_key = key;
+        }
+        int oe = bh_launch_build_order(c->tile_cost, a.n_tiles, a.order_block, a.order_centre, c->order_counters,
+                                       c->order, s);
+        if (oe != 0) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail((hipError_t)oe, "order kernels"); }
+        a.order = c->order;
+        a.tile_cost = c->tile_cost;
+    }
+    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
+                                     : bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s);
     if (prev != c->device) (void)hipSetDevice(prev);
     if (e != 0) return hip_fail((hipError_t)e, "march kernel launch");
     return BH_OK;

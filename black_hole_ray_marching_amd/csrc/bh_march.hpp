@@ -148,11 +148,10 @@ struct Frame {
     float k;     // (DP * RS) * -1.5: the scalar prefix of rd_derivative (:126)
 };
 __device__ __forceinline__ Frame make_frame(const MarchArgs& a) {
-    Frame f;
+    Frame f;  // invariants precomputed on the host (bh_host.cpp, frame_constants)
     f.ro0 = mk(a.pos[0], a.pos[1], a.pos[2]);
-    const v3 n = normalize(f.ro0);
-    f.cps = muls(muls(mk(-n.x, -n.y, -n.z), 1.5f), a.rs);
-    f.k = (a.dp * a.rs) * -1.5f;
+    f.cps = mk(a.cps[0], a.cps[1], a.cps[2]);
+    f.k = a.kfac;
     return f;
 }
 
@@ -447,33 +446,46 @@ __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint
 // SIMD's other waves (the tail of the frame, measured +34 % of kernel time at cap 512 vs cap 64).
 constexpr uint32_t PRIO_ITERS = 48;
 
-// ---- schedule 1: one wave64 = one 8x8 tile (simple reference schedule) ---------------------------
+// ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
+// Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
+// the centre-out permutation; each wave records its tile's max n_rk for the next frame's order.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
 __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     __shared__ float lut[256];
     lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (slot >= a.n_tiles) return;
-    const uint32_t t = centre_out(slot, a.n_tiles, a.order_block, a.order_centre);
+    if (slot >= a.n_tiles) return;  // wave-uniform
+    const uint32_t t = a.order ? a.order[slot] : centre_out(slot, a.n_tiles, a.order_block, a.order_centre);
     uint32_t tx, ty;
     shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
     const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
-    if (px >= a.width || py >= a.height) return;
+    const bool valid = px < a.width && py < a.height;
     const Frame f = make_frame(a);
     RayState st;
     st.ro = f.ro0;
-    st.rd = pixel_ray(a, px, py);
+    st.rd = pixel_ray(a, valid ? px : 0u, valid ? py : 0u);
     st.s = ray_s(f, st.rd);
     st.travelled = 0.0f;
     st.n_rk = 0;
     st.outside = false;
     uint32_t fate = 0xFFu;
-    for (uint32_t it = 0;; ++it) {
-        if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);  // it is wave-uniform
-        if ((fate = march_step(a, f, st)) != 0xFFu) break;
+    if (valid) {
+        for (uint32_t it = 0;; ++it) {
+            if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);  // it is wave-uniform
+            if ((fate = march_step(a, f, st)) != 0xFFu) break;
+        }
+        write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate);
     }
-    write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate);
+    if (a.tile_cost) {
+        const uint32_t m = wave_max_u32(st.n_rk);
+        if (lane == 0u) a.tile_cost[t] = (uint8_t)min(m >> 1, 255u);
+    }
 }
 
 // ---- schedule 0: persistent waves with per-lane refill (default) --------------------------------

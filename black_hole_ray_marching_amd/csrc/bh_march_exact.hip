@@ -7,12 +7,12 @@
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
                                                                              uint32_t* counters, uint32_t grid,
                                                                              hipStream_t s) {
-    if (schedule == BH_SCHED_PAIR) {
-        const uint32_t pairs = (a.n_tiles + 1u) / 2u;
-        hipLaunchKernelGGL(bh::exact::march_pair_kernel, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
-    } else if (schedule == BH_SCHED_TILE) {
+    if (schedule == BH_SCHED_TILE) {
         const uint32_t blocks = (a.n_tiles + 3u) / 4u;
         hipLaunchKernelGGL(bh::exact::march_tile_kernel, dim3(blocks), dim3(256), 0, s, a);
+    } else if (schedule == BH_SCHED_PAIR) {
+        const uint32_t pairs = (a.n_tiles + 1u) / 2u;
+        hipLaunchKernelGGL(bh::exact::march_pair_kernel, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
     } else {
         hipError_t e = hipMemsetAsync(counters, 0, bh::exact::NQ * bh::exact::CTR_STRIDE * sizeof(uint32_t), s);
         if (e != hipSuccess) return (int)e;

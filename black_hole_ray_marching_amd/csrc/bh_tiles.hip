@@ -24,7 +24,57 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const T* __restrict__
     out[(size_t)py * width + px] = packed[g * 64u + lane];
 }
 
+// Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), stable
+// enough: slots are visited in centre-out order and each block reserves its bucket ranges with one
+// atomic per bucket, so ties keep (roughly) the centre-out order.  counters: [0..B) counts,
+// [B..2B) cursors, zeroed before the count pass.
+__global__ void __launch_bounds__(256) order_count_kernel(const uint8_t* __restrict__ cost, uint32_t n,
+                                                        uint32_t L, uint32_t c, uint32_t* counters) {
+    __shared__ uint32_t hist[ORDER_BUCKETS];
+    if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&hist[cost_bucket(cost[centre_out(i, n, L, c)])], 1u);
+    __syncthreads();
+    if (threadIdx.x < ORDER_BUCKETS && hist[threadIdx.x]) atomicAdd(&counters[threadIdx.x], hist[threadIdx.x]);
+}
+__global__ void __launch_bounds__(256) order_scatter_kernel(const uint8_t* __restrict__ cost, uint32_t n,
+                                                          uint32_t L, uint32_t c, uint32_t* counters,
+                                                          uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[ORDER_BUCKETS], base[ORDER_BUCKETS];
+    if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t t = 0, b = 0, k = 0;
+    if (i < n) {
+        t = centre_out(i, n, L, c);
+        b = cost_bucket(cost[t]);
+        k = atomicAdd(&hist[b], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < ORDER_BUCKETS && hist[threadIdx.x]) {
+        uint32_t off = 0;
+        for (uint32_t j = 0; j < threadIdx.x; ++j) off += counters[j];
+        base[threadIdx.x] = off + atomicAdd(&counters[ORDER_BUCKETS + threadIdx.x], hist[threadIdx.x]);
+    }
+    __syncthreads();
+    if (i < n) order[base[b] + k] = t;
+}
+
 }  // namespace bh
+
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const uint8_t* cost, uint32_t n,
+                                                                         uint32_t L, uint32_t c,
+                                                                         uint32_t* counters, uint32_t* order,
+                                                                         hipStream_t s) {
+    if (n == 0) return 0;
+    hipError_t e = hipMemsetAsync(counters, 0, 2 * bh::ORDER_BUCKETS * sizeof(uint32_t), s);
+    if (e != hipSuccess) return (int)e;
+    const uint32_t blocks = (n + 255u) / 256u;
+    hipLaunchKernelGGL(bh::order_count_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters);
+    hipLaunchKernelGGL(bh::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters, order);
+    return (int)hipGetLastError();
+}
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
                                       uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp,

@@ -116,10 +116,14 @@ typedef enum {
 
 /* Work schedule of the march kernel (same results, different speed). */
 typedef enum {
-    BH_SCHED_PAIR = 0,       /* one wave64 per two 8x8 tiles, two interleaved rays per lane (default) */
-    BH_SCHED_TILE = 1,       /* one wave64 per 8x8 tile, exits when its slowest ray finishes */
+    BH_SCHED_TILE = 0,       /* one wave64 per 8x8 tile (default); dispatch order: the previous frame's
+                                per-tile cost, most expensive first (ties / first frame: centre-out
+                                around the black hole's screen row) */
+    BH_SCHED_PAIR = 1,       /* one wave64 per two 8x8 tiles, two interleaved rays per lane */
     BH_SCHED_PERSISTENT = 2  /* resident waves, per-lane refill from an LDS ray queue */
 } bh_schedule;
+/* OR into `schedule` to use the static centre-out order only (no per-tile cost feedback). */
+#define BH_SCHED_FLAG_STATIC_ORDER 0x100u
 
 /* Per-pixel fate codes written to dbg_fate. */
 #define BH_FATE_CAP      0u  /* loop ran out (max_iters); still shades sky with its current rd */
@@ -138,7 +142,7 @@ typedef struct {
     uint32_t layout;          /* bh_layout */
     uint32_t shard_index;     /* this rank's tile share: tile (tx,ty) belongs to shard (tx + 3*ty) % shard_count */
     uint32_t shard_count;     /* 1 = whole frame */
-    uint32_t schedule;        /* bh_schedule */
+    uint32_t schedule;        /* bh_schedule | BH_SCHED_FLAG_* (results never depend on it) */
     void* out_col;            /* target 0 (`col`), device pointer, never NULL */
     void* out_blackout;       /* target 1 (`blackout_col`), device pointer or NULL (== Option::None) */
     uint16_t* dbg_n_rk;       /* optional: completed RK4 steps per pixel (same layout as outputs, 1 elem/px) */

@@ -245,3 +245,27 @@ def test_exact_matches_golden_fixtures(torch_cuda, path, schedule):
     assert np.array_equal(nrk.cpu().numpy().view(np.uint16), z["n_rk"])
     assert np.array_equal(col.cpu().numpy().view(np.uint32), z["col"].view(np.uint32))
     scene.close()
+
+
+def test_temporal_order_never_changes_results(torch_cuda, sky_small):
+    """The tile schedule orders dispatch by the previous frame's per-tile cost.  Costs learned on
+    one camera and reused on another, and the static centre-out order, give identical bits."""
+    torch = torch_cuda
+    W, H, cap = 160, 96, 512
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
+    outs = {}
+    for name, cam, sched in [("E1", "E", bh.BH_SCHED_TILE), ("A_after_E", "A", bh.BH_SCHED_TILE),
+                             ("A_again", "A", bh.BH_SCHED_TILE),
+                             ("A_static", "A", bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER)]:
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        col = torch.full((H, W, 4), float("nan"), device="cuda")
+        nrk = torch.zeros((H, W), dtype=torch.int16, device="cuda")
+        scene.render(col, None, dbg_n_rk=nrk, schedule=sched)
+        torch.cuda.synchronize()
+        outs[name] = (col.cpu().numpy(), nrk.cpu().numpy())
+    for k in ("A_again", "A_static"):
+        assert np.array_equal(outs[k][0].view(np.uint32), outs["A_after_E"][0].view(np.uint32))
+        assert np.array_equal(outs[k][1], outs["A_after_E"][1])
+    o = oracle_render(camera_uniform("A", W, H), uniforms(), sky_small, W, H, cap, 3)
+    assert np.array_equal(outs["A_after_E"][0].view(np.uint32), o[0].view(np.uint32))
+    scene.close()

@@ -10,7 +10,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--frames", type=int, default=5)
     p.add_argument("--math", choices=["fast", "exact"], default="exact")
-    p.add_argument("--schedule", choices=["pair", "tile", "persistent"], default="pair")
+    p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
     p.add_argument("--width", type=int, default=4096)
     p.add_argument("--height", type=int, default=2048)
     p.add_argument("--max-iters", type=int, default=512)
@@ -22,7 +22,8 @@ def main():
                   math=bh.BH_MATH_FAST if a.math == "fast" else bh.BH_MATH_EXACT)
     col = torch.empty((a.height, a.width, 4), dtype=torch.float16, device="cuda")
     bo = torch.empty_like(col)
-    sched = {"pair": bh.BH_SCHED_PAIR, "tile": bh.BH_SCHED_TILE, "persistent": bh.BH_SCHED_PERSISTENT}[a.schedule]
+    sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
+             "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[a.schedule]
     for _ in range(a.frames):
         sc.render(col, bo, fmt=bh.BH_OUT_RGBA16F, schedule=sched)
     torch.cuda.synchronize()
