@@ -143,15 +143,19 @@ def main() -> None:
     kern_ms = np.array([a.elapsed_time(b) for a, b in ev])
     kern_avg_s = float(kern_ms.mean()) / 1e3
 
-    # algorithmic work of one launch: completed RK steps over this rank's pixels (deterministic)
+    # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
+    # the loop's own count (what the reference iterates); sum_steps the updates actually executed
+    # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
     nrk_buf = torch.zeros(col.shape[:-1], dtype=torch.int16, device=dev)
-    render(dbg_n_rk=nrk_buf)
+    steps_buf = torch.zeros(col.shape[:-1], dtype=torch.int16, device=dev)
+    render(dbg_n_rk=nrk_buf, dbg_steps=steps_buf)
     torch.cuda.synchronize(dev)
     sum_nrk = int(nrk_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
+    sum_steps = int(steps_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
 
     if rank == 0:
         value = W * H * args.steps / elapsed / 1e6
-        achieved_tf = sum_nrk * F_STEP[3] / kern_avg_s / 1e12
+        achieved_tf = sum_steps * F_STEP[3] / kern_avg_s / 1e12
         alg_bytes = my_px * bpp * 2 + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
         result = {
@@ -177,12 +181,12 @@ def main() -> None:
             },
             "kernel": {"name": f"bh::{args.math}::march_{args.schedule}_kernel", "launches": args.steps,
                        "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
-                       "max_ms": round(float(kern_ms.max()), 5), "sum_n_rk": sum_nrk,
+                       "max_ms": round(float(kern_ms.max()), 5), "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
                        "mean_n_rk": round(sum_nrk / my_px, 4), "frames_per_s": round(1.0 / kern_avg_s, 2)},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
                          "traffic": _pmc_traffic(W, H, cap, args),
-                         "note": f"{F_STEP[3]} flop-eq per completed RK step (SURVEY §8d) x sum(n_rk) / avg "
+                         "note": f"{F_STEP[3]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
                                  "launch time (HIP events on the render stream); FP32 VALU-bound, no "
                                  "MFMA-shaped work; traffic = HBM bytes/launch from rocprofv3 PMC "
                                  "(profiles/pmc_traffic.json)"},

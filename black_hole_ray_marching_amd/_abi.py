@@ -48,7 +48,8 @@ class bh_render_desc(C.Structure):
                 ("scene_flags", C.c_uint32), ("format", C.c_uint32), ("math", C.c_uint32),
                 ("layout", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
                 ("schedule", C.c_uint32), ("out_col", C.c_void_p), ("out_blackout", C.c_void_p),
-                ("dbg_n_rk", C.c_void_p), ("dbg_fate", C.c_void_p)]
+                ("dbg_n_rk", C.c_void_p), ("dbg_fate", C.c_void_p),
+                ("dbg_steps", C.c_void_p)]
 
 
 assert C.sizeof(bh_camera_uniform) == 112

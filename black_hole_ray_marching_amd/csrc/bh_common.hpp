@@ -38,6 +38,7 @@ struct MarchArgs {
     void* out_blackout;
     uint16_t* dbg_n_rk;
     uint8_t* dbg_fate;
+    uint16_t* dbg_steps;
 };
 
 // Shard ownership: tile (tx, ty) belongs to shard (tx + 3*ty) % S (SURVEY §8e diagonal interleave).

@@ -365,7 +365,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
         a.kfac = (a.dp * a.rs) * -1.5f;
     }
     a.out_col = d->out_col; a.out_blackout = d->out_blackout;
-    a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate;
+    a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate; a.dbg_steps = d->dbg_steps;
     if (a.n_tiles == 0) return BH_OK;
 
     int prev = 0;

@@ -196,6 +196,9 @@ struct FOps {
     __device__ __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }  // raw v_sqrt_f32
     __device__ __forceinline__ float length(v3 p) { return __builtin_amdgcn_sqrtf(dot(p, p)); }
     __device__ __forceinline__ v3 div6(v3 x) { return muls(x, 1.0f / 6.0f); }
+    __device__ __forceinline__ v3 add2(v3 a, v3 b) {  // a + 2b
+        return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
+    }
     __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
         const float iq = rsq(q), iq2 = iq * iq;
         return muls(p, s * (iq2 * iq2 * iq));
@@ -222,7 +225,10 @@ struct XOps {
     static constexpr bool kCR = CR;
     bool bad = false;
     // running unsigned min of crm::key() over every division numerator: zeros map high (the cores
-    // are exact for them; camera-A rays start on two coordinate planes), tiny values low
+    // are exact for them, and they are common: camera-A rays start on two coordinate planes, and a
+    // ray frozen at dt == 0 on the photon-sphere marker has all-zero RK sums), tiny values low.
+    // (A float min |n| guard is cheaper per step but sends those frozen rays down the IEEE path at
+    // every step: measured 7 % slower overall.)
     uint32_t kmin = 0xFFFFFFFFu;
     __device__ __forceinline__ float sqrt(float x, bool used = true) {
         if constexpr (CR) { bad |= used & crm::sqrt_bad(x); return crm::sqrt_core(x); }
@@ -234,6 +240,15 @@ struct XOps {
             return mk(crm::div6(x.x), crm::div6(x.y), crm::div6(x.z));
         } else {
             return mk(x.x / 6.0f, x.y / 6.0f, x.z / 6.0f);
+        }
+    }
+    // a + 2b (the RK4 weights): 2b is exact, so the FMA rounds once exactly like the two IEEE adds
+    // whenever 2b does not overflow, which the guarded domain rules out (|p| <= 2^12, dt <= 2^13)
+    __device__ __forceinline__ v3 add2(v3 a, v3 b) {
+        if constexpr (CR) {
+            return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
+        } else {
+            return add(a, smul(2.0f, b));
         }
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
@@ -275,7 +290,11 @@ struct XOps {
 // One iteration of the loop body (:266-328) on `st`.  Returns BH_FATE_* if the ray terminates in
 // this iteration (state then unchanged except `outside`; n_rk counts completed RK updates), or
 // 0xFF if it continues.
-template <class Ops>
+//
+// BRANCHY = true (single-ray schedules): a lane whose ray terminates before the RK update returns at
+// once and the update is committed unconditionally (saves the selects; the RK block is skipped when
+// every active lane terminates).  BRANCHY = false keeps one basic block for the pair schedule.
+template <bool BRANCHY, class Ops>
 __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, RayState& st, Ops& X) {
     const v3 ro = st.ro, rd = st.rd;
     const float r2 = dot(ro, ro);
@@ -289,6 +308,9 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const float ds = X.sdf(ro, a.rs, a.scene_flags);                   // :285
     uint32_t pre = (ds < MIN_DIST) ? (uint32_t)BH_FATE_SURFACE : 0xFFu;   // :286-288
     pre = blackout ? (uint32_t)BH_FATE_BLACKOUT : pre;
+    if constexpr (BRANCHY) {
+        if (pre != 0xFFu) return pre;
+    }
     const float dps = X.length(sub(f.cps, ro)) - 0.075f;               // :294
     const float dist = fminf(ds, dps);                                 // :299
     const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
@@ -302,8 +324,8 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const v3 rd_k3 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k2)), s));
     const v3 ro_k4 = smul(dt, add(rd, rd_k3));
     const v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
-    const v3 dro = X.div6(add(add(add(ro_k1, smul(2.0f, ro_k2)), smul(2.0f, ro_k3)), ro_k4));
-    const v3 drd = X.div6(add(add(add(rd_k1, smul(2.0f, rd_k2)), smul(2.0f, rd_k3)), rd_k4));
+    const v3 dro = X.div6(add(X.add2(X.add2(ro_k1, ro_k2), ro_k3), ro_k4));
+    const v3 drd = X.div6(add(X.add2(X.add2(rd_k1, rd_k2), rd_k3), rd_k4));
 #if !BH_FAST
     if constexpr (Ops::kCR) {
         // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
@@ -312,9 +334,17 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
         X.bad |= !(fabsf(s) <= 0x1p30f);
     }
 #endif
-    const bool go = pre == 0xFFu;
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
     const float ntr = st.travelled + dt;                               // :324
+    if constexpr (BRANCHY) {
+        st.ro = nro;
+        st.rd = nrd;
+        st.travelled = ntr;
+        st.n_rk += 1u;
+        uint32_t fate = (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;
+        return (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;
+    }
+    const bool go = pre == 0xFFu;
     st.ro = sel(go, nro, ro);
     st.rd = sel(go, nrd, rd);
     st.travelled = go ? ntr : st.travelled;
@@ -333,11 +363,11 @@ __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
 #if BH_FAST
     FOps X;
-    return step_bf(a, f, st, X);
+    return step_bf<true>(a, f, st, X);
 #else
     RayState t = st;
     XOps<true> X;
-    uint32_t fate = step_bf(a, f, t, X);
+    uint32_t fate = step_bf<true>(a, f, t, X);
     const uint64_t badm = __ballot(X.bad);
     if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
 #ifdef BH_DIAG_SLOW
@@ -349,7 +379,7 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
         if (X.bad) {
             t = st;
             XOps<false> Y;
-            fate = step_bf(a, f, t, Y);
+            fate = step_bf<true>(a, f, t, Y);
         }
     }
     st = t;
@@ -364,16 +394,16 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
     RayState t0 = s0, t1 = s1;
 #if BH_FAST
     FOps X0, X1;
-    uint32_t f0 = step_bf(a, f, t0, X0);
-    uint32_t f1 = step_bf(a, f, t1, X1);
+    uint32_t f0 = step_bf<false>(a, f, t0, X0);
+    uint32_t f1 = step_bf<false>(a, f, t1, X1);
 #else
     XOps<true> X0, X1;
-    uint32_t f0 = step_bf(a, f, t0, X0);
-    uint32_t f1 = step_bf(a, f, t1, X1);
+    uint32_t f0 = step_bf<false>(a, f, t0, X0);
+    uint32_t f1 = step_bf<false>(a, f, t1, X1);
     const bool bad0 = X0.bad & alive0, bad1 = X1.bad & alive1;
     if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
-        if (bad0) { t0 = s0; XOps<false> Y; f0 = step_bf(a, f, t0, Y); }
-        if (bad1) { t1 = s1; XOps<false> Y; f1 = step_bf(a, f, t1, Y); }
+        if (bad0) { t0 = s0; XOps<false> Y; f0 = step_bf<false>(a, f, t0, Y); }
+        if (bad1) { t1 = s1; XOps<false> Y; f1 = step_bf<false>(a, f, t1, Y); }
     }
 #endif
     // selects, not branches
@@ -427,7 +457,8 @@ __device__ __forceinline__ void store_px(void* base, uint32_t fmt, size_t idx, v
 }
 
 // fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
-__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate) {
+__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate,
+                                            uint32_t steps) {
     store_px(a.out_col, a.format, idx, col);
     if (a.out_blackout) {
         const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
@@ -435,15 +466,19 @@ __device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 c
     }
     if (a.dbg_n_rk) a.dbg_n_rk[idx] = (uint16_t)n_rk;
     if (a.dbg_fate) a.dbg_fate[idx] = (uint8_t)fate;
+    if (a.dbg_steps) a.dbg_steps[idx] = (uint16_t)steps;
+}
+__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate) {
+    write_pixel(a, idx, col, n_rk, fate, n_rk);
 }
 
 __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
     return (a.layout == BH_LAYOUT_TILES) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
 }
 
-// A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a photon-sphere
-// ray that may run to the cap: raise its issue priority so its serial chain is not stretched by the
-// SIMD's other waves (the tail of the frame, measured +34 % of kernel time at cap 512 vs cap 64).
+// Iterations after which a still-marching wave raises its issue priority (the frame's tail: measured
+// +34 % of kernel time at cap 512 vs cap 64 without it) and the tile schedule starts checking for
+// cycles (march_cycles).
 constexpr uint32_t PRIO_ITERS = 48;
 
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
@@ -452,6 +487,53 @@ constexpr uint32_t PRIO_ITERS = 48;
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
     return v;
+}
+
+// ---- cycle fast-forward ----------------------------------------------------------------------------
+// One loop iteration is a pure function of (ro, rd, travelled, outside) (s and the uniforms are
+// per-ray constants; n_rk only feeds the cap test).  Some rays stop moving in f32: dt rounds to 0 on
+// the photon-sphere marker (dps == 0 exactly, a fixed point) or flips sign every step around it (a
+// 2-cycle); they then iterate unchanged until the cap (SURVEY §8d "Zeno" rays, up to 512 steps).
+// After step j, if the state equals the state two steps back bit for bit (and `outside` did not
+// change across those two steps), the sequence is periodic with period 1 or 2 from then on; no
+// termination test can fire (both states of the cycle already passed them), so the ray ends with
+// fate CAP, n_rk = max_iters and the cycle state of matching parity: the loop's own result,
+// without running it.  Checked from PRIO_ITERS on (the cycles found start at median iteration 30).
+struct Hist { v3 ro, rd; float tr; bool outside; };
+
+__device__ __forceinline__ bool same_bits(float x, float y) { return __float_as_uint(x) == __float_as_uint(y); }
+__device__ __forceinline__ bool same_state(const RayState& st, const Hist& h) {
+    // bitwise & (no short-circuit branches)
+    return same_bits(st.ro.x, h.ro.x) & same_bits(st.ro.y, h.ro.y) & same_bits(st.ro.z, h.ro.z) &
+           same_bits(st.rd.x, h.rd.x) & same_bits(st.rd.y, h.rd.y) & same_bits(st.rd.z, h.rd.z) &
+           same_bits(st.travelled, h.tr) & (st.outside == h.outside);
+}
+
+// March `st` to termination with the fast-forward; `steps` = RK updates actually executed.  The two
+// history states live in LDS (ping-pong slots by iteration parity), not VGPRs: holding them in
+// registers takes the kernel from 61 to 73 VGPRs (8 -> 6 waves per SIMD) and measured slower.
+struct HistLds { float4 a[2][2][64]; };  // [slot][ro+tr | rd+outside][lane]
+__device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& steps,
+                                                 HistLds& H, uint32_t lane) {
+    H.a[1][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, __uint_as_float(0xFFFFFFFFu));
+    H.a[1][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+    for (uint32_t p = 0;; p ^= 1u) {
+        H.a[p][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.travelled);
+        H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+        const uint32_t fate = march_step(a, f, st);
+        if (fate != 0xFFu) { steps = st.n_rk; return fate; }
+        const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
+        const Hist h2{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w) != 0u};
+        if (same_state(st, h2)) {
+            steps = st.n_rk;
+            if ((a.max_iters - st.n_rk) & 1u) {
+                const float4 r0 = H.a[p][0][lane], r1 = H.a[p][1][lane];
+                st.ro = mk(r0.x, r0.y, r0.z); st.rd = mk(r1.x, r1.y, r1.z); st.travelled = r0.w;
+            }
+            st.n_rk = a.max_iters;
+            return BH_FATE_CAP;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
@@ -474,16 +556,23 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     st.travelled = 0.0f;
     st.n_rk = 0;
     st.outside = false;
-    uint32_t fate = 0xFFu;
+    uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
-        for (uint32_t it = 0;; ++it) {
-            if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);  // it is wave-uniform
+        for (uint32_t it = 0; it < PRIO_ITERS; ++it)
             if ((fate = march_step(a, f, st)) != 0xFFu) break;
+        steps = st.n_rk;
+        if (fate == 0xFFu) {
+            // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
+            // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
+            // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
+            __builtin_amdgcn_s_setprio(2);
+            __shared__ HistLds hist[4];  // 16 KiB per workgroup: 8 workgroups per CU still fit
+            fate = march_cycles(a, f, st, steps, hist[threadIdx.x >> 6], lane);
         }
-        write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate);
+        write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
     if (a.tile_cost) {
-        const uint32_t m = wave_max_u32(st.n_rk);
+        const uint32_t m = wave_max_u32(steps);
         if (lane == 0u) a.tile_cost[t] = (uint8_t)min(m >> 1, 255u);
     }
 }

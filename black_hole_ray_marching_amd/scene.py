@@ -180,7 +180,7 @@ class Scene:
     def render(self, output, blackout_output=None, *, fmt: int = BH_OUT_RGBA32F, stream=None,
                dbg_n_rk=None, dbg_fate=None, math: int | None = None, layout: int = BH_LAYOUT_ROWMAJOR,
                shard_index: int = 0, shard_count: int = 1, width: int | None = None,
-               height: int | None = None, schedule: int = 0) -> None:
+               height: int | None = None, schedule: int = 0, dbg_steps=None) -> None:
         """Scene::render (src/scene.rs:470-522): one pass writing `col` and optionally `blackout_col`.
 
         `output`/`blackout_output`: caller-owned device buffers (torch tensors or raw pointers).
@@ -198,7 +198,7 @@ class Scene:
         d.layout, d.shard_index, d.shard_count = layout, shard_index, shard_count
         d.schedule = schedule
         d.out_col, d.out_blackout = _ptr(output), _ptr(blackout_output)
-        d.dbg_n_rk, d.dbg_fate = _ptr(dbg_n_rk), _ptr(dbg_fate)
+        d.dbg_n_rk, d.dbg_fate, d.dbg_steps = _ptr(dbg_n_rk), _ptr(dbg_fate), _ptr(dbg_steps)
         check(self.lib.bh_render(self._ctx, C.byref(self.camera_uniform.c), C.byref(self.uniforms.to_c()),
                                  C.byref(d), _stream_handle(stream)), "bh_render")
 

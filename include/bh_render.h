@@ -147,6 +147,9 @@ typedef struct {
     void* out_blackout;       /* target 1 (`blackout_col`), device pointer or NULL (== Option::None) */
     uint16_t* dbg_n_rk;       /* optional: completed RK4 steps per pixel (same layout as outputs, 1 elem/px) */
     uint8_t* dbg_fate;        /* optional: BH_FATE_* per pixel */
+    uint16_t* dbg_steps;      /* optional: RK4 iterations actually executed per pixel; below dbg_n_rk
+                                 only where a ray that had entered an exact cycle (see DESIGN.md
+                                 "Cycle fast-forward") was advanced to the cap without iterating */
 } bh_render_desc;
 
 typedef struct bh_ctx bh_ctx;

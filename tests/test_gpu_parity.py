@@ -269,3 +269,40 @@ def test_temporal_order_never_changes_results(torch_cuda, sky_small):
     o = oracle_render(camera_uniform("A", W, H), uniforms(), sky_small, W, H, cap, 3)
     assert np.array_equal(outs["A_after_E"][0].view(np.uint32), o[0].view(np.uint32))
     scene.close()
+
+
+@pytest.mark.parametrize("cam", ["A", "B"])
+def test_cycle_fast_forward_is_exact(torch_cuda, cam):
+    """The tile schedule advances rays caught in an exact period-1/2 cycle straight to the cap
+    (DESIGN.md "Cycle fast-forward").  At the headline size: some rays are fast-forwarded
+    (dbg_steps < dbg_n_rk), only capped ones, and the frame is bit-identical to the pair schedule
+    (which iterates every step) and, on every row holding a fast-forwarded ray, to the oracle."""
+    torch = torch_cuda
+    W, H, cap = 4096, 2048, 512
+    sky = bh.synthetic_sky()
+    scene = bh.Scene(W, H, sky=sky, max_iters=cap, math=bh.BH_MATH_EXACT)
+    scene.camera_uniform = camera_uniform(cam, W, H)
+    outs = {}
+    for sched in (bh.BH_SCHED_TILE, bh.BH_SCHED_PAIR):
+        col = torch.full((H, W, 4), float("nan"), device="cuda")
+        bo = torch.full((H, W, 4), float("nan"), device="cuda")
+        nrk = torch.zeros((H, W), dtype=torch.int16, device="cuda")
+        steps = torch.zeros((H, W), dtype=torch.int16, device="cuda")
+        fate = torch.full((H, W), 0xFF, dtype=torch.uint8, device="cuda")
+        scene.render(col, bo, dbg_n_rk=nrk, dbg_fate=fate, dbg_steps=steps, schedule=sched)
+        torch.cuda.synchronize()
+        outs[sched] = (col.cpu().numpy(), bo.cpu().numpy(), nrk.cpu().numpy().view(np.uint16),
+                       fate.cpu().numpy(), steps.cpu().numpy().view(np.uint16))
+    t, p = outs[bh.BH_SCHED_TILE], outs[bh.BH_SCHED_PAIR]
+    for k in range(4):
+        assert np.array_equal(t[k].view(np.uint8), p[k].view(np.uint8)), k
+    nrk, fate, steps = t[2], t[3], t[4]
+    ff = steps != nrk
+    assert np.array_equal(p[4], p[2])            # pair: no fast-forward
+    assert ff.sum() > 100, ff.sum()              # cameras A/B: ~800 / ~1100 cycling rays
+    assert (steps <= nrk).all() and (fate[ff] == bh.BH_FATE_CAP).all() and (nrk[ff] == cap).all()
+    rows = np.unique(np.nonzero(ff)[0])
+    for r0 in rows[:: max(1, len(rows) // 12)]:
+        o = oracle_render(camera_uniform(cam, W, H), uniforms(), sky, W, H, cap, 3, int(r0), int(r0) + 1)
+        assert_bitexact(tuple(x[r0:r0 + 1] for x in t[:4]), o)
+    scene.close()
