@@ -95,29 +95,39 @@ def main() -> None:
         bo = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
         shard = dict(layout=bh.BH_LAYOUT_ROWMAJOR)
         my_px = W * H
+        pipe = None
     else:
+        # weak scaling: each rank renders its (tx + 3ty) % n tiles into a packed buffer; frame i's
+        # gather to rank 0 (col only: rank 0 can recompute blackout_col) overlaps frame i+1's render
         stride = multigpu.packed_stride(W, H, n)
         my_px = bh.shard_tile_count(W, H, rank, n) * 64
-        col = torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev)
         bo = torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev)
-        gathered = [torch.empty_like(col) for _ in range(n)] if rank == 0 else None
-        packed_all = torch.empty((n * stride * 64, 4), dtype=ch_dtype, device=dev) if rank == 0 else None
         frame = torch.empty((H, W, 4), dtype=ch_dtype, device=dev) if rank == 0 else None
         shard = dict(layout=bh.BH_LAYOUT_TILES, shard_index=rank, shard_count=n)
 
+        def on_frame(i, gathered):
+            bh.tiles_unpack(gathered, frame, W, H, n, stride, bpp, stream=stream)
+
+        pipe = multigpu.GatherPipeline(lambda: torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev),
+                                       rank, n, on_frame)
+        col = pipe.buffer(0)
+
+    frame_no = [0]
+
     def render(**kw):
-        scene.render(col, bo, fmt=fmt, stream=stream, schedule=sched, **shard, **kw)
+        scene.render(col if pipe is None else pipe.buffer(frame_no[0]), bo, fmt=fmt, stream=stream,
+                     schedule=sched, **shard, **kw)
 
     def exchange():
-        if n > 1:
-            multigpu.gather_packed(col, rank, n, gathered)
-            if rank == 0:
-                torch.cat(gathered, out=packed_all)
-                bh.tiles_unpack(packed_all, frame, W, H, n, stride, bpp, stream=stream)
+        if pipe is not None:
+            pipe.submit(frame_no[0])
+        frame_no[0] += 1
 
     for _ in range(args.warmup):
         render()
         exchange()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize(dev)
 
     # timed region: barrier + synchronize on both sides; HIP events around every render launch on
@@ -132,6 +142,8 @@ def main() -> None:
         render()
         ev[i][1].record(stream)
         exchange()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize(dev)
     if n > 1:
         dist.barrier()
@@ -174,7 +186,8 @@ def main() -> None:
             "config": {
                 "workload": f"{W}x{H} frame, cap {cap} RK steps, disc+markers+sky, camera {args.camera}, "
                             f"{args.fmt} col+blackout, {args.math} math"
-                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n} + RCCL gather of col to rank 0"),
+                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n}, RCCL gather of col to rank 0 "
+                                                  "overlapped with the next frame, unpack on rank 0"),
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
                 "schedule": args.schedule, "format": args.fmt,
                 "parallelism": "single GPU" if n == 1 else f"tile-sharded x{n}",

@@ -76,6 +76,65 @@ def gather_packed(packed, rank: int, world: int, gathered=None, group=None):
     return gathered if rank == 0 else None
 
 
+class GatherPipeline:
+    """Frame pipeline over ranks: frame i is rendered into packed buffer i % depth, its gather to
+    rank 0 is issued asynchronously right after (torch.distributed enqueues the collective on its
+    own stream behind the render), so it runs over xGMI while frame i+1 renders; rank 0 then unpacks
+    frame i.  Before frame i + depth reuses a buffer, the gather that read it is waited on (on the
+    compute stream, not the host, for RCCL).  Rank 0 receives straight into one contiguous
+    (world, stride*64, C) buffer per slot, so the unpack reads it without a concatenation.
+
+        pipe = GatherPipeline(lambda: torch.empty(...), rank, world, on_frame)
+        for i in range(K):
+            render_into(pipe.buffer(i)); pipe.submit(i)
+        pipe.drain()
+
+    `on_frame(i, gathered)` runs on rank 0 once frame i's gather is complete (stream-ordered):
+    `gathered` is the (world * stride * 64, C) buffer of all ranks' packed tiles."""
+
+    def __init__(self, make_buffer, rank: int, world: int, on_frame=None, depth: int = 2, group=None):
+        import torch
+        if depth < 1:
+            raise ValueError("depth >= 1")
+        self.rank, self.world, self.depth, self.group = rank, world, depth, group
+        self.on_frame = on_frame
+        self.bufs = [make_buffer() for _ in range(depth)]
+        self.recv = None
+        if rank == 0:
+            b = self.bufs[0]
+            self.recv = [torch.empty((world * b.shape[0], *b.shape[1:]), dtype=b.dtype, device=b.device)
+                         for _ in range(depth)]
+        self.pending = []  # (frame, work) in submission order
+
+    def buffer(self, i: int):
+        return self.bufs[i % self.depth]
+
+    def submit(self, i: int) -> None:
+        import torch.distributed as dist
+        slot = i % self.depth
+        if self.world == 1:
+            work = None
+            if self.rank == 0:
+                self.recv[slot].copy_(self.bufs[slot])
+        else:
+            gl = list(self.recv[slot].view(self.world, *self.bufs[slot].shape).unbind(0)) if self.rank == 0 else None
+            work = dist.gather(self.bufs[slot], gl, dst=0, group=self.group, async_op=True)
+        self.pending.append((i, work))
+        while len(self.pending) >= self.depth:  # the next frame's buffer must be free
+            self._finish_one()
+
+    def _finish_one(self) -> None:
+        i, work = self.pending.pop(0)
+        if work is not None:
+            work.wait()
+        if self.rank == 0 and self.on_frame is not None:
+            self.on_frame(i, self.recv[i % self.depth])
+
+    def drain(self) -> None:
+        while self.pending:
+            self._finish_one()
+
+
 def weak_scaling_frame(world: int, base_w: int = 4096, base_h: int = 2048) -> tuple[int, int]:
     """Frame for `world` GPUs with about base_w*base_h pixels per GPU at the base aspect (weak scaling)."""
     if world == 1:
