@@ -199,7 +199,7 @@ struct FOps {
     __device__ __forceinline__ v3 add2(v3 a, v3 b) {  // a + 2b
         return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
     }
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float, bool = false) {
         const float iq = rsq(q), iq2 = iq * iq;
         return muls(p, s * (iq2 * iq2 * iq));
     }
@@ -224,19 +224,29 @@ template <bool CR>
 struct XOps {
     static constexpr bool kCR = CR;
     bool bad = false;
-    // running unsigned min of crm::key() over every division numerator: zeros map high (the cores
-    // are exact for them, and they are common: camera-A rays start on two coordinate planes, and a
-    // ray frozen at dt == 0 on the photon-sphere marker has all-zero RK sums), tiny values low.
-    // (A float min |n| guard is cheaper per step but sends those frozen rays down the IEEE path at
-    // every step: measured 7 % slower overall.)
+    // Numerator domain of the division cores: 0 or >= DIV_N_MIN in magnitude.  Zeros are legal (the
+    // cores are exact for them) and occur in two places:
+    //  * k1's numerators s*ro: camera-A rays start on two coordinate planes.  Checked through
+    //    crm::key (zeros map high, tiny values low): one v_lshl_add per value + v_min3_u32;
+    //  * the x/6 numerators when dt == 0 exactly (a ray frozen on the photon-sphere marker): all RK
+    //    sums are then +-0.
+    // Everywhere else a zero numerator needs an exact cancellation, so those are checked as a float
+    // min |n| (one v_min3_f32 with |.| modifiers per three values) and a zero just takes the IEEE
+    // path; the x/6 check is waived when dt == 0.  (min |n| everywhere: measured 7 % slower, frozen
+    // rays fell back at every step.)
     uint32_t kmin = 0xFFFFFFFFu;
+    float amin = __builtin_inff();   // k2..k4 numerators
+    float amin6 = __builtin_inff();  // x/6 numerators
+    __device__ __forceinline__ static float absmin3(float m, float x, float y, float z) {
+        return fminf(m, fminf(fabsf(x), fminf(fabsf(y), fabsf(z))));
+    }
     __device__ __forceinline__ float sqrt(float x, bool used = true) {
         if constexpr (CR) { bad |= used & crm::sqrt_bad(x); return crm::sqrt_core(x); }
         else return __builtin_sqrtf(x);
     }
     __device__ __forceinline__ v3 div6(v3 x) {
         if constexpr (CR) {
-            kmin = min(kmin, crm::kmin3(crm::key(x.x), crm::key(x.y), crm::key(x.z)));
+            amin6 = absmin3(amin6, x.x, x.y, x.z);
             return mk(crm::div6(x.x), crm::div6(x.y), crm::div6(x.z));
         } else {
             return mk(x.x / 6.0f, x.y / 6.0f, x.z / 6.0f);
@@ -253,12 +263,13 @@ struct XOps {
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
     // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq) {
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq, bool zeros = false) {
         const float Q = (q * q) * sq;
         const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
         if constexpr (CR) {
             bad |= crm::div_d_bad(Q);
-            kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
+            if (zeros) kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
+            else amin = absmin3(amin, nx, ny, nz);
             const crm::Rcp R = crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
         } else {
@@ -317,7 +328,7 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const float s = st.s;
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
-    const v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r));
+    const v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r, true));
     const v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
     const v3 rd_k2 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k1)), s));
     const v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
@@ -331,6 +342,8 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
         // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
         // |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds every |s*p_i| <= 2^42.
         X.bad |= X.kmin < crm::KEY_MIN;
+        X.bad |= !(X.amin >= crm::DIV_N_MIN);
+        X.bad |= !(X.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
         X.bad |= !(fabsf(s) <= 0x1p30f);
     }
 #endif
