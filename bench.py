@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
     p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
-    p.add_argument("--fmt", choices=["rgba16f", "rgba32f"], default="rgba16f")
+    p.add_argument("--fmt", choices=["rgba16f", "rgba32f", "bgra8"], default="rgba16f")
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--max-iters", type=int, default=512)
@@ -77,8 +77,9 @@ def main() -> None:
 
     W, H = (args.width, args.height) if args.width and args.height else multigpu.weak_scaling_frame(n)
     cap = args.max_iters
-    fmt = bh.BH_OUT_RGBA16F if args.fmt == "rgba16f" else bh.BH_OUT_RGBA32F
-    ch_dtype = torch.float16 if fmt == bh.BH_OUT_RGBA16F else torch.float32
+    fmt = {"rgba16f": bh.BH_OUT_RGBA16F, "rgba32f": bh.BH_OUT_RGBA32F, "bgra8": bh.BH_OUT_BGRA8_SRGB}[args.fmt]
+    ch_dtype = {bh.BH_OUT_RGBA16F: torch.float16, bh.BH_OUT_RGBA32F: torch.float32,
+                bh.BH_OUT_BGRA8_SRGB: torch.uint8}[fmt]
     bpp = bh.BYTES_PER_PIXEL[fmt]
     math_mode = bh.BH_MATH_EXACT if args.math == "exact" else bh.BH_MATH_FAST
     sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
@@ -192,7 +193,7 @@ def main() -> None:
                 "schedule": args.schedule, "format": args.fmt,
                 "parallelism": "single GPU" if n == 1 else f"tile-sharded x{n}",
             },
-            "kernel": {"name": f"bh::{args.math}::march_{args.schedule}_kernel", "launches": args.steps,
+            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u>", "launches": args.steps,
                        "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
                        "max_ms": round(float(kern_ms.max()), 5), "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
                        "mean_n_rk": round(sum_nrk / my_px, 4), "frames_per_s": round(1.0 / kern_avg_s, 2)},

@@ -72,6 +72,7 @@ SIGNATURES = {
     "bh_shard_tile_count": (C.c_int64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
+    "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
 }
 
@@ -97,6 +98,8 @@ def load() -> C.CDLL:
             pass
     lib = C.CDLL(str(LIB_PATH))
     for name, (res, args) in SIGNATURES.items():
+        if "BH_LIB" in os.environ and not hasattr(lib, name):
+            continue  # development override (A/B of an older build): bind what it exports
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

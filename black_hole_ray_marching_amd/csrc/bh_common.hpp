@@ -32,6 +32,7 @@ struct MarchArgs {
     // sky (Rgba8UnormSrgb texels as packed u32, little endian: r | g<<8 | b<<16 | a<<24)
     const uint32_t* sky;
     const float* srgb_lut;     // 256 entries, sRGB byte -> linear
+    const float* srgb_enc;     // 257 thresholds of the BGRA8 sRGB encode (bh_srgb.hpp)
     uint32_t sky_w, sky_h;
     // outputs
     void* out_col;

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <string>
 #include <thread>
@@ -17,6 +18,7 @@ struct bh_ctx {
     int device = 0;
     uint32_t* sky = nullptr;       // device RGBA8 texels
     float* lut = nullptr;          // device sRGB->linear table (256 floats)
+    float* enc = nullptr;          // device linear->sRGB threshold table (257 floats)
     uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
@@ -53,6 +55,34 @@ void srgb_lut(float lut[256]) {
         double c = (double)i / 255.0;
         lut[i] = (float)(c <= 0.04045 ? c / 12.92 : std::pow((c + 0.055) / 1.055, 2.4));
     }
+}
+
+// linear -> sRGB byte of a Bgra8UnormSrgb store: clamp to [0, 1] (NaN -> 0), the sRGB OETF in double,
+// round half up (the normative encode, DESIGN.md "Output formats").
+uint8_t srgb_encode_ref(float x) {
+    if (!(x > 0.0f)) return 0;
+    if (x >= 1.0f) return 255;
+    const double v = (double)x;
+    const double e = v <= 0.0031308 ? 12.92 * v : 1.055 * std::pow(v, 1.0 / 2.4) - 0.055;
+    const double q = std::floor(e * 255.0 + 0.5);
+    return (uint8_t)(q > 255.0 ? 255.0 : q);
+}
+
+// Thresholds of the encode (bh_srgb.hpp): T[k] = the smallest float in (0, 1] with code >= k,
+// found by bisection over the ordered bit patterns of positive floats.
+void srgb_encode_table(float T[257]) {
+    T[0] = 0.0f;
+    for (int k = 1; k < 256; ++k) {
+        uint32_t lo = 0u, hi = 0x3F800000u;  // code(lo) < k <= code(hi)
+        while (hi - lo > 1u) {
+            const uint32_t mid = lo + (hi - lo) / 2u;
+            float x;
+            std::memcpy(&x, &mid, 4);
+            if (srgb_encode_ref(x) >= k) hi = mid; else lo = mid;
+        }
+        std::memcpy(&T[k], &hi, 4);
+    }
+    T[256] = std::numeric_limits<float>::infinity();
 }
 
 // Screen row (in tiles) of the black hole's projection: solve C1 + l0 (C0 - C1) + l2 (C2 - C1) = -t ro0
@@ -143,6 +173,12 @@ const char* bh_last_error(void) { return g_last_error.c_str(); }
 
 // Scene::new defaults, src/scene.rs:89-137 (RS 1.0, max dt 0.5, bg 0.5, blackout PodBool::r#false()
 // whose inner is 1 (src/podbool.rs:24-26), max dist 250, distortion 1.0); 24 B padded to 32.
+int bh_srgb_encode_table(float* out257) {
+    if (!out257) return BH_ERR_INVALID_ARG;
+    srgb_encode_table(out257);
+    return BH_OK;
+}
+
 int bh_uniforms_default(bh_uniforms* out) {
     if (!out) return BH_ERR_INVALID_ARG;
     std::memset(out, 0, sizeof(*out));
@@ -277,13 +313,16 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     c->sky_w = sky_w;
     c->sky_h = sky_h;
     const size_t bytes = (size_t)sky_w * sky_h * 4u;
-    float lut[256];
+    float lut[256], enc[257];
     srgb_lut(lut);
+    srgb_encode_table(enc);
     int st = BH_OK;
     if ((e = hipMalloc(&c->sky, bytes)) != hipSuccess) st = (e == hipErrorOutOfMemory) ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "hipMalloc(sky)");
     else if ((e = hipMalloc(&c->lut, sizeof(lut))) != hipSuccess) st = hip_fail(e, "hipMalloc(lut)");
     else if ((e = hipMemcpy(c->sky, sky, bytes, hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(sky)");
     else if ((e = hipMemcpy(c->lut, lut, sizeof(lut), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(lut)");
+    else if ((e = hipMalloc(&c->enc, sizeof(enc))) != hipSuccess) st = hip_fail(e, "hipMalloc(enc)");
+    else if ((e = hipMemcpy(c->enc, enc, sizeof(enc), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc)");
     else if ((e = hipMalloc(&c->counters, 1024)) != hipSuccess) st = hip_fail(e, "hipMalloc(counters)");
     if (st == BH_OK) {
         int cus = 0;
@@ -307,6 +346,7 @@ int bh_destroy(bh_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->sky) (void)hipFree(c->sky);
     if (c->lut) (void)hipFree(c->lut);
+    if (c->enc) (void)hipFree(c->enc);
     if (c->counters) (void)hipFree(c->counters);
     if (c->tile_cost) (void)hipFree(c->tile_cost);
     if (c->order) (void)hipFree(c->order);
@@ -331,7 +371,6 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
-    if (d->format == BH_OUT_BGRA8_SRGB) { g_last_error = "BGRA8 sRGB output not implemented yet"; return BH_ERR_UNSUPPORTED; }
     if (!screen_tri_default(cam)) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
 
     bh::MarchArgs a;
@@ -354,7 +393,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     // centre-out dispatch blocks of ~one tile row of this shard, centred on the black hole's row
     a.order_block = (uint32_t)((nt + a.tiles_y - 1u) / a.tiles_y);
     a.order_centre = bh_tile_row(cam, d->height);
-    a.sky = c->sky; a.srgb_lut = c->lut; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
+    a.sky = c->sky; a.srgb_lut = c->lut; a.srgb_enc = c->enc; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
     // per-frame invariants with the oracle's op sequence (correctly rounded f32, no contraction):
     // c_ps = ((-normalize(ro0)) * 1.5) * RS (src/black_hole_maybe.wgsl:294), k = (DP * RS) * -1.5 (:126)
     {

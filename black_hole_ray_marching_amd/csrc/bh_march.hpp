@@ -17,6 +17,7 @@
 
 #include "bh_common.hpp"
 #include "bh_crmath.hpp"
+#include "bh_srgb.hpp"
 
 #ifndef BH_FAST
 #error "define BH_FAST to 0 or 1"
@@ -456,33 +457,55 @@ __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32
     return col;
 }
 
-__device__ __forceinline__ void store_px(void* base, uint32_t fmt, size_t idx, v3 c) {
-    if (fmt == BH_OUT_RGBA32F) {
+// Output texel store; the format is a template parameter (one kernel instantiation per format keeps
+// the BGRA8 encoder out of the other formats' code: it measured 1.8 % on the RGBA16F kernel).
+template <uint32_t FMT>
+__device__ __forceinline__ void store_px(void* base, size_t idx, v3 c, const float* enc) {
+    if constexpr (FMT == BH_OUT_RGBA32F) {
         reinterpret_cast<float4*>(base)[idx] = make_float4(c.x, c.y, c.z, 1.0f);
-    } else if (fmt == BH_OUT_RGBA16F) {
+    } else if constexpr (FMT == BH_OUT_RGBA16F) {
         __half2 lo = __floats2half2_rn(c.x, c.y);
         __half2 hi = __floats2half2_rn(c.z, 1.0f);
         uint2 w;
         w.x = *reinterpret_cast<uint32_t*>(&lo);
         w.y = *reinterpret_cast<uint32_t*>(&hi);
         reinterpret_cast<uint2*>(base)[idx] = w;
+    } else {
+        static_assert(FMT == BH_OUT_BGRA8_SRGB, "output format");
+        reinterpret_cast<uint32_t*>(base)[idx] = srgb_bgra8(c.x, c.y, c.z, enc);
+    }
+}
+
+// LDS tables of a workgroup: [0, 256) the sRGB decode of sky texels, then for BGRA8 output the
+// encoder's 257 thresholds.  Needs blockDim.x >= 256.
+template <uint32_t FMT>
+constexpr int lds_tables() { return FMT == BH_OUT_BGRA8_SRGB ? 256 + SRGB_TABLE : 256; }
+template <uint32_t FMT>
+__device__ __forceinline__ void load_tables(const MarchArgs& a, float* tab) {
+    tab[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    if constexpr (FMT == BH_OUT_BGRA8_SRGB) {
+        tab[256 + threadIdx.x] = a.srgb_enc[threadIdx.x];
+        if (threadIdx.x == 0) tab[256 + 256] = a.srgb_enc[256];
     }
 }
 
 // fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
-__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate,
-                                            uint32_t steps) {
-    store_px(a.out_col, a.format, idx, col);
+template <uint32_t FMT>
+__device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab, size_t idx, v3 col, uint32_t n_rk,
+                                            uint32_t fate, uint32_t steps) {
+    store_px<FMT>(a.out_col, idx, col, tab + 256);
     if (a.out_blackout) {
         const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
-        store_px(a.out_blackout, a.format, idx, bo);
+        store_px<FMT>(a.out_blackout, idx, bo, tab + 256);
     }
     if (a.dbg_n_rk) a.dbg_n_rk[idx] = (uint16_t)n_rk;
     if (a.dbg_fate) a.dbg_fate[idx] = (uint8_t)fate;
     if (a.dbg_steps) a.dbg_steps[idx] = (uint16_t)steps;
 }
-__device__ __forceinline__ void write_pixel(const MarchArgs& a, size_t idx, v3 col, uint32_t n_rk, uint32_t fate) {
-    write_pixel(a, idx, col, n_rk, fate, n_rk);
+template <uint32_t FMT>
+__device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab, size_t idx, v3 col, uint32_t n_rk,
+                                            uint32_t fate) {
+    write_pixel<FMT>(a, tab, idx, col, n_rk, fate, n_rk);
 }
 
 __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
@@ -549,9 +572,10 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
     }
 }
 
+template <uint32_t FMT>
 __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
-    __shared__ float lut[256];
-    lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    __shared__ float lut[lds_tables<FMT>()];
+    load_tables<FMT>(a, lut);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -582,7 +606,7 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
             __shared__ HistLds hist[4];  // 16 KiB per workgroup: 8 workgroups per CU still fit
             fate = march_cycles(a, f, st, steps, hist[threadIdx.x >> 6], lane);
         }
-        write_pixel(a, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
+        write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
     if (a.tile_cost) {
         const uint32_t m = wave_max_u32(steps);
@@ -615,10 +639,11 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set lanes bel
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+template <uint32_t FMT>
 __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint32_t* __restrict__ counters) {
-    __shared__ float lut[256];
+    __shared__ float lut[lds_tables<FMT>()];
     __shared__ WaveQueues queues[4];
-    lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    load_tables<FMT>(a, lut);
     __syncthreads();  // the only workgroup barrier: waves run independently afterwards
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -704,7 +729,7 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
                 const uint32_t e = n_done - 64u + lane;
                 const uint32_t meta = Q.d_meta[e];
                 const v3 col = shade(a, lut, meta >> 16, mk(Q.d_x[e], Q.d_y[e], Q.d_z[e]));
-                write_pixel(a, Q.d_idx[e], col, meta & 0xFFFFu, meta >> 16);
+                write_pixel<FMT>(a, lut, Q.d_idx[e], col, meta & 0xFFFFu, meta >> 16);
                 n_done -= 64u;
                 __builtin_amdgcn_wave_barrier();
             }
@@ -714,7 +739,7 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
     if (lane < n_done) {
         const uint32_t meta = Q.d_meta[lane];
         const v3 col = shade(a, lut, meta >> 16, mk(Q.d_x[lane], Q.d_y[lane], Q.d_z[lane]));
-        write_pixel(a, Q.d_idx[lane], col, meta & 0xFFFFu, meta >> 16);
+        write_pixel<FMT>(a, lut, Q.d_idx[lane], col, meta & 0xFFFFu, meta >> 16);
     }
 }
 
@@ -724,9 +749,10 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
 // interleaves the two rays' iterations: on gfx950 one dependent chain per wave issues only every
 // ~4-5 cycles however many waves share the SIMD, two chains reach the ~2.3-cycle peak
 // (tools/ubench/latency.hip).
+template <uint32_t FMT>
 __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
-    __shared__ float lut[256];
-    lut[threadIdx.x] = a.srgb_lut[threadIdx.x];
+    __shared__ float lut[lds_tables<FMT>()];
+    load_tables<FMT>(a, lut);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t pair = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -761,8 +787,8 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
         if (it == PRIO_ITERS) __builtin_amdgcn_s_setprio(2);
         march_step2(a, f, s0, s1, alive0, alive1, fate0, fate1);
     }
-    if (valid0) write_pixel(a, out_index(a, t0, lane, px0, py0), shade(a, lut, fate0, s0.rd), s0.n_rk, fate0);
-    if (valid1) write_pixel(a, out_index(a, t1, lane, px1, py1), shade(a, lut, fate1, s1.rd), s1.n_rk, fate1);
+    if (valid0) write_pixel<FMT>(a, lut, out_index(a, t0, lane, px0, py0), shade(a, lut, fate0, s0.rd), s0.n_rk, fate0);
+    if (valid1) write_pixel<FMT>(a, lut, out_index(a, t1, lane, px1, py1), shade(a, lut, fate1, s1.rd), s1.n_rk, fate1);
 }
 
 }  // namespace BH_NS

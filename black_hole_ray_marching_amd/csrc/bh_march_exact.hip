@@ -4,27 +4,38 @@
 #define BH_NS exact
 #include "bh_march.hpp"
 
-extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
-                                                                             uint32_t* counters, uint32_t grid,
-                                                                             hipStream_t s) {
+namespace {
+template <uint32_t FMT>
+int launch(const bh::MarchArgs& a, uint32_t schedule, uint32_t* counters, uint32_t grid, hipStream_t s) {
     if (schedule == BH_SCHED_TILE) {
         const uint32_t blocks = (a.n_tiles + 3u) / 4u;
-        hipLaunchKernelGGL(bh::exact::march_tile_kernel, dim3(blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(bh::exact::march_tile_kernel<FMT>, dim3(blocks), dim3(256), 0, s, a);
     } else if (schedule == BH_SCHED_PAIR) {
         const uint32_t pairs = (a.n_tiles + 1u) / 2u;
-        hipLaunchKernelGGL(bh::exact::march_pair_kernel, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(bh::exact::march_pair_kernel<FMT>, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
     } else {
         hipError_t e = hipMemsetAsync(counters, 0, bh::exact::NQ * bh::exact::CTR_STRIDE * sizeof(uint32_t), s);
         if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(bh::exact::march_persistent_kernel, dim3(grid), dim3(256), 0, s, a, counters);
+        hipLaunchKernelGGL(bh::exact::march_persistent_kernel<FMT>, dim3(grid), dim3(256), 0, s, a, counters);
     }
     return (int)hipGetLastError();
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
+                                                                             uint32_t* counters, uint32_t grid,
+                                                                             hipStream_t s) {
+    switch (a.format) {
+        case BH_OUT_RGBA32F: return launch<BH_OUT_RGBA32F>(a, schedule, counters, grid, s);
+        case BH_OUT_RGBA16F: return launch<BH_OUT_RGBA16F>(a, schedule, counters, grid, s);
+        default: return launch<BH_OUT_BGRA8_SRGB>(a, schedule, counters, grid, s);
+    }
 }
 
 // Resident 256-thread blocks per CU of the persistent kernel (sizes its grid: every block resident).
 extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exact(void) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::exact::march_persistent_kernel, 256, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::exact::march_persistent_kernel<BH_OUT_BGRA8_SRGB>, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
 

@@ -3,6 +3,7 @@
 // Exposed as bh_selftest_crmath (diagnostics API of include/bh_render.h).
 #include "bh_common.hpp"
 #include "bh_crmath.hpp"
+#include "bh_srgb.hpp"
 
 namespace bh {
 
@@ -30,8 +31,9 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 1: div6 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
 // op 2: div_core on `count` random (n, d) pairs from the guarded domain, seeded by base
 // op 3: div_core with n = d * m for random small integers m (exact quotients) and n = d*q +- ulps
+// op 4: srgb_encode over every 32-bit pattern in [base, base + count) against a binary search of T
 __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, uint64_t count,
-                                                      unsigned long long* cnt, uint32_t* ex) {
+                                                      unsigned long long* cnt, uint32_t* ex, const float* T) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         if (op == 0) {
@@ -49,6 +51,17 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             const float got = crm::div6(x), want = x / 6.0f;
             if (__float_as_uint(got) != __float_as_uint(want))
                 record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 4) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            const float xc = fminf(fmaxf(x, 0.0f), 1.0f);
+            int lo = 0, hi = 256;  // largest k in [0, 255] with xc >= T[k]
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (xc >= T[mid]) lo = mid; else hi = mid;
+            }
+            const uint32_t got = srgb_encode(x, T);
+            if (got != (uint32_t)lo) record(cnt, ex, bits, 0, got, (uint32_t)lo);
         } else if (op == 2 || op == 3) {
             const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
             float d = fabsf(rnd_float(h1, -40, 59));
@@ -74,21 +87,26 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 3 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 4 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;
     unsigned long long* cnt = nullptr;
     uint32_t* ex = nullptr;
+    float* T = nullptr;
+    float table[bh::SRGB_TABLE];
+    (void)bh_srgb_encode_table(table);
     int st = BH_OK;
-    if (hipMalloc(&cnt, sizeof(*cnt)) != hipSuccess || hipMalloc(&ex, 8 * sizeof(uint32_t)) != hipSuccess) {
+    if (hipMalloc(&cnt, sizeof(*cnt)) != hipSuccess || hipMalloc(&ex, 8 * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&T, sizeof(table)) != hipSuccess) {
         st = BH_ERR_OUT_OF_MEMORY;
     } else {
         (void)hipMemset(cnt, 0, sizeof(*cnt));
         (void)hipMemset(ex, 0, 8 * sizeof(uint32_t));
+        (void)hipMemcpy(T, table, sizeof(table), hipMemcpyHostToDevice);
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex);
+        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex, T);
         if (hipDeviceSynchronize() != hipSuccess) st = BH_ERR_HIP;
         unsigned long long h = 0;
         (void)hipMemcpy(&h, cnt, sizeof(h), hipMemcpyDeviceToHost);
@@ -97,6 +115,7 @@ extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_
     }
     if (cnt) (void)hipFree(cnt);
     if (ex) (void)hipFree(ex);
+    if (T) (void)hipFree(T);
     (void)hipSetDevice(prev);
     return st;
 }

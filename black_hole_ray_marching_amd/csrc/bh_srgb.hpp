@@ -1,0 +1,34 @@
+// bh_srgb.hpp — linear f32 -> sRGB byte, the store of a Bgra8UnormSrgb render target (the reference's
+// surface/consumer format: src/scene.rs:259-274, src/copy.rs:132, src/remix.rs:160).
+//
+// Normative encode (oracle/bh_oracle.c bho_srgb_encode): clamp to [0, 1] (NaN -> 0), the sRGB OETF in
+// double, round half up to 0..255.  It is monotone in x, so it is fully described by 255 thresholds:
+// T[k] = the smallest float with code >= k (bh_host.cpp builds them from the definition; T[0] = 0,
+// T[256] = +inf).  On the GPU a hardware-log2/exp2 evaluation of the OETF lands within one code of
+// the answer, and the two neighbouring thresholds fix it: exact for every float (checked
+// exhaustively on the device, bh_selftest_crmath op 4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bh {
+
+constexpr int SRGB_TABLE = 257;
+
+__device__ __forceinline__ uint32_t srgb_encode(float x, const float* T) {
+    const float xc = fminf(fmaxf(x, 0.0f), 1.0f);  // fmaxf(NaN, 0) = 0
+    const float s = xc <= 0.0031308f ? 12.92f * xc
+                                     : 1.055f * __builtin_amdgcn_exp2f(__builtin_amdgcn_logf(xc) * (1.0f / 2.4f)) - 0.055f;
+    int c = (int)(s * 255.0f + 0.5f);
+    c = c < 0 ? 0 : (c > 255 ? 255 : c);
+    c = (xc < T[c]) ? c - 1 : c;        // T[0] = 0 <= xc: never below 0
+    c = (xc >= T[c + 1]) ? c + 1 : c;   // T[256] = +inf: never above 255
+    return (uint32_t)c;
+}
+
+// BGRA8 texel (byte 0 = B) of linear rgb, alpha 1.
+__device__ __forceinline__ uint32_t srgb_bgra8(float r, float g, float b, const float* T) {
+    return srgb_encode(b, T) | (srgb_encode(g, T) << 8) | (srgb_encode(r, T) << 16) | 0xFF000000u;
+}
+
+}  // namespace bh

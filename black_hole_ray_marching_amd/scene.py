@@ -20,7 +20,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
-                   BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
+                   BH_OUT_RGBA32F, BH_OUT_BGRA8_SRGB, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
 
 MAX_ITERATIONS = 1000  # src/black_hole_maybe.wgsl:85
 
@@ -112,6 +112,13 @@ def synthetic_sky(width: int = 4096, height: int = 2048, seed: int = 0x5EED_B1AC
     """Deterministic RGBA8 sRGB equirectangular sky, (height, width, 4) uint8."""
     out = np.empty((height, width, 4), dtype=np.uint8)
     check(load().bh_synthetic_sky(out.ctypes.data, width, height, seed), "bh_synthetic_sky")
+    return out
+
+
+def srgb_encode_table() -> np.ndarray:
+    """The 257 thresholds of the BGRA8 sRGB encoder (bh_srgb.hpp): code(x) = max k with x >= T[k]."""
+    out = np.empty(257, np.float32)
+    check(load().bh_srgb_encode_table(out.ctypes.data), "bh_srgb_encode_table")
     return out
 
 
@@ -224,5 +231,6 @@ def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_s
 
 
 __all__ = ["Camera", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+           "srgb_encode_table", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -91,7 +91,8 @@ typedef struct {
 typedef enum {
     BH_OUT_RGBA32F = 0,     /* 16 B / pixel, linear */
     BH_OUT_RGBA16F = 1,     /*  8 B / pixel, linear, round-to-nearest-even from the fp32 result */
-    BH_OUT_BGRA8_SRGB = 2   /*  4 B / pixel, sRGB-encoded, clamped, byte order B,G,R,A */
+    BH_OUT_BGRA8_SRGB = 2   /*  4 B / pixel, sRGB-encoded (round(255 * OETF(clamp(x, 0, 1))), NaN -> 0),
+                               byte order B,G,R,A: the Bgra8UnormSrgb store of the reference */
 } bh_out_format;
 
 /* Arithmetic mode of the integrator (see DESIGN.md "Math modes"). */
@@ -192,11 +193,16 @@ int bh_tiles_unpack(const void* packed, void* out_rowmajor, uint32_t width, uint
                     uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t bytes_per_pixel,
                     void* hip_stream);
 
+/* The BGRA8 sRGB encoder's threshold table: out[k] (k = 1..255) = the smallest float x with
+ * encode(x) >= k, out[0] = 0, out[256] = +inf; encode(x) = the largest k with x >= out[k]. */
+int bh_srgb_encode_table(float* out257);
+
 /* Diagnostics: check the correctly rounded division/sqrt cores the exact kernel uses against IEEE
  * results on `device` (op 0: sqrt over float bit patterns [base, base+count); op 1: x/6 over bit
  * patterns [base, base+count); op 2: n/d on `count` random pairs seeded by base; op 3: n/d near exact
- * quotients).  *out_mismatches = number of differing results; out_examples (8 u32, optional) = up
- * to two (a, b, got, want) bit patterns.  Synchronous. */
+ * quotients; op 4: the BGRA8 sRGB encoder over float bit patterns [base, base+count) against a
+ * binary search of bh_srgb_encode_table).  *out_mismatches = number of differing results;
+ * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);
 

@@ -33,6 +33,10 @@ def load() -> C.CDLL:
         lib.bho_srgb_lut.argtypes = [C.c_void_p]
         lib.bho_srgb_encode.restype = C.c_uint8
         lib.bho_srgb_encode.argtypes = [C.c_float]
+        lib.bho_srgb_encode_array.restype = None
+        lib.bho_srgb_encode_array.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        lib.bho_srgb_table_mismatches.restype = C.c_uint64
+        lib.bho_srgb_table_mismatches.argtypes = [C.c_void_p, C.c_int]
         _lib = lib
     return _lib
 
@@ -75,6 +79,20 @@ def trace_ray(ro0, rd0, uniforms: bytes, sky: np.ndarray, max_iters: int, scene_
                       sky.shape[0], max_iters, scene_flags, out, C.byref(n), C.byref(f), st)
     s = np.array(st, np.float32)
     return np.array(out, np.float32), int(n.value), int(f.value), s[:3], s[3:]
+
+
+def srgb_encode(x: np.ndarray, threads: int = 0) -> np.ndarray:
+    """Linear f32 -> sRGB byte (the Bgra8UnormSrgb store), element-wise."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty(x.shape, np.uint8)
+    load().bho_srgb_encode_array(x.ctypes.data, out.ctypes.data, x.size, threads)
+    return out
+
+
+def srgb_table_mismatches(table: np.ndarray, threads: int = 0) -> int:
+    t = np.ascontiguousarray(table, np.float32)
+    assert t.shape == (257,)
+    return int(load().bho_srgb_table_mismatches(t.ctypes.data, threads))
 
 
 def srgb_lut() -> np.ndarray:

@@ -218,6 +218,34 @@ uint8_t bho_srgb_encode(float x) {
     return (uint8_t)(q > 255.0 ? 255.0 : q);
 }
 
+/* The encode over an array (test helper: the BGRA8 output's expected bytes). */
+void bho_srgb_encode_array(const float* x, uint8_t* out, size_t n, int threads) {
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+    for (long long i = 0; i < (long long)n; i++) out[i] = bho_srgb_encode(x[i]);
+}
+
+/* Test helper: the number of floats x in [0, 1] (every bit pattern 0 .. 0x3F800000) whose
+ * threshold-table code (largest k with x >= T[k], T[0] = 0, T[256] = +inf) differs from
+ * bho_srgb_encode(x) -- i.e. checks a 257-entry threshold table against the definition. */
+uint64_t bho_srgb_table_mismatches(const float T[257], int threads) {
+    uint64_t bad = 0;
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static) reduction(+ : bad)
+    for (long long b = 0; b <= 0x3F800000LL; b++) {
+        float x;
+        uint32_t u = (uint32_t)b;
+        memcpy(&x, &u, 4);
+        int lo = 0, hi = 256;  /* largest k in [0, 255] with x >= T[k] */
+        while (hi - lo > 1) {
+            int mid = (lo + hi) / 2;
+            if (x >= T[mid]) lo = mid; else hi = mid;
+        }
+        bad += (uint8_t)lo != bho_srgb_encode(x);
+    }
+    return bad;
+}
+
 /* vs_main + rasteriser + fs_main ray setup (:37-55, :360-363): the per-vertex world ray vectors are
  * interpolated at the pixel centre with barycentrics of the fixed screen triangle
  * (3,1), (-1,1), (-1,-3) (src/uniforms.rs:114-118):  l0 = (x+.5)/(2W), l2 = (y+.5)/(2H), l1 = 1-l0-l2. */

@@ -47,3 +47,9 @@ def test_div_core_random(lib):
 def test_div_core_near_exact_quotients(lib):
     m, ex = run(lib, 3, 777, 1 << 30)
     assert m == 0, ex
+
+
+def test_srgb_encode_exhaustive(lib):
+    # the BGRA8 encoder (hardware log2/exp2 estimate + threshold fix-up) over all 2^32 patterns
+    m, ex = run(lib, 4, 0, 1 << 32)
+    assert m == 0, ex

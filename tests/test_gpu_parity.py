@@ -306,3 +306,29 @@ def test_cycle_fast_forward_is_exact(torch_cuda, cam):
         o = oracle_render(camera_uniform(cam, W, H), uniforms(), sky, W, H, cap, 3, int(r0), int(r0) + 1)
         assert_bitexact(tuple(x[r0:r0 + 1] for x in t[:4]), o)
     scene.close()
+
+
+def _bgra8_expected(col_f32):
+    enc = oracle.srgb_encode(col_f32[..., :3])
+    out = np.empty(col_f32.shape[:-1] + (4,), np.uint8)
+    out[..., 0], out[..., 1], out[..., 2], out[..., 3] = enc[..., 2], enc[..., 1], enc[..., 0], 255
+    return out
+
+
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("cam", ["A", "D"])
+def test_bgra8_srgb_output_is_encoded_exact_result(torch_cuda, sky_small, cam, schedule):
+    """BH_OUT_BGRA8_SRGB (the reference's Bgra8UnormSrgb targets): every byte equals the normative
+    encode (oracle bho_srgb_encode) of the oracle's fp32 colour, for col and blackout_col."""
+    torch = torch_cuda
+    W, H, cap = 136, 72, 512
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
+    scene.camera_uniform = camera_uniform(cam, W, H)
+    col = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    bo = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    scene.render(col, bo, fmt=bh.BH_OUT_BGRA8_SRGB, schedule=schedule)
+    torch.cuda.synchronize()
+    o = oracle_render(camera_uniform(cam, W, H), uniforms(), sky_small, W, H, cap, 3)
+    assert np.array_equal(col.cpu().numpy(), _bgra8_expected(o[0]))
+    assert np.array_equal(bo.cpu().numpy(), _bgra8_expected(o[1]))
+    scene.close()
