@@ -38,8 +38,8 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=50)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)   # SURVEY §8d timing protocol: 10 warm-up + 100 timed
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
     p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
     p.add_argument("--fmt", choices=["rgba16f", "rgba32f", "bgra8"], default="rgba16f")
@@ -167,6 +167,7 @@ def main() -> None:
     sum_steps = int(steps_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
 
     if rank == 0:
+        pmc = _pmc_entry(W, H, cap, args)
         value = W * H * args.steps / elapsed / 1e6
         achieved_tf = sum_steps * F_STEP[3] / kern_avg_s / 1e12
         alg_bytes = my_px * bpp * 2 + sky.nbytes
@@ -199,10 +200,12 @@ def main() -> None:
                        "mean_n_rk": round(sum_nrk / my_px, 4), "frames_per_s": round(1.0 / kern_avg_s, 2)},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
-                         "traffic": _pmc_traffic(W, H, cap, args),
+                         "traffic": pmc.get("hbm_bytes_per_launch"),
+                         "valu_busy": pmc.get("valu_busy_est"),
                          "note": f"{F_STEP[3]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
                                  "launch time (HIP events on the render stream); FP32 VALU-bound, no "
-                                 "MFMA-shaped work; traffic = HBM bytes/launch from rocprofv3 PMC "
+                                 "MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU issue "
+                                 "cycles / SIMD cycles, both from rocprofv3 PMC passes of this configuration "
                                  "(profiles/pmc_traffic.json)"},
             "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(achieved_gbs / PEAK_HBM_GBS, 5),
@@ -219,15 +222,13 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-def _pmc_traffic(W, H, cap, args):
-    """HBM bytes per launch measured by rocprofv3 PMC passes (profiles/pmc_traffic.json), or None."""
+def _pmc_entry(W, H, cap, args):
+    """This configuration's entry of profiles/pmc_traffic.json (rocprofv3 PMC passes), or {}."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     try:
-        d = json.loads(p.read_text())
-        e = d.get(f"{W}x{H}_cap{cap}_{args.math}_{args.schedule}_{args.fmt}")
-        return None if e is None else e["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        return None
+        return json.loads(p.read_text()).get(f"{W}x{H}_cap{cap}_{args.math}_{args.schedule}_{args.fmt}") or {}
+    except (OSError, ValueError):
+        return {}
 
 
 def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
