@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores in this process's affinity)")
     p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--verify-gather", action="store_true",
+                   help="N>1: rank 0 compares the assembled frame with its own full-frame render (bitwise)")
     return p.parse_args()
 
 
@@ -70,10 +72,18 @@ def main() -> None:
     if world > 1 and world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     n = max(world, 1)
+    # BH_BENCH_REHEARSAL=1 (development only, never set by the driver): all ranks share cuda:0 and
+    # the gloo backend, to exercise the N>1 path (sharding, pipelined gather, unpack) on a 1-GPU box
+    rehearsal = os.environ.get("BH_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if n > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     W, H = (args.width, args.height) if args.width and args.height else multigpu.weak_scaling_frame(n)
     cap = args.max_iters
@@ -156,6 +166,14 @@ def main() -> None:
     kern_ms = np.array([a.elapsed_time(b) for a, b in ev])
     kern_avg_s = float(kern_ms.mean()) / 1e3
 
+    gather_ok = None
+    if args.verify_gather and n > 1 and rank == 0:
+        ref = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
+        scene.render(ref, None, fmt=fmt, stream=stream, schedule=sched)
+        torch.cuda.synchronize(dev)
+        gather_ok = bool(torch.equal(ref.view(torch.uint8), frame.view(torch.uint8)))
+        del ref
+
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
     # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
@@ -192,7 +210,8 @@ def main() -> None:
                                                   "overlapped with the next frame, unpack on rank 0"),
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
                 "schedule": args.schedule, "format": args.fmt,
-                "parallelism": "single GPU" if n == 1 else f"tile-sharded x{n}",
+                "parallelism": "single GPU" if n == 1 else f"tile-sharded x{n}"
+                               + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
             },
             "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u>", "launches": args.steps,
                        "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
@@ -216,6 +235,8 @@ def main() -> None:
             result["cpu_baseline"] = None
         else:
             result["cpu_baseline"], result["parity"] = _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched)
+        if gather_ok is not None:
+            result["gather_verified_bit_exact"] = gather_ok
         print(json.dumps(result))
     if n > 1:
         dist.barrier()
