@@ -15,6 +15,7 @@ BH_ERR_NO_DEVICE = -4
 BH_ERR_OUT_OF_MEMORY = -5
 
 BH_OUT_RGBA32F, BH_OUT_RGBA16F, BH_OUT_BGRA8_SRGB = 0, 1, 2
+BH_BLOOM_AUTO, BH_BLOOM_LITERAL = 0, 1
 BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
@@ -73,6 +74,8 @@ SIGNATURES = {
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
+    "bh_bloom": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                           C.c_void_p, C.c_void_p]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
 }
 

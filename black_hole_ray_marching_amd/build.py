@@ -18,7 +18,7 @@ ROOT = PKG.parent
 CSRC = PKG / "csrc"
 OBJ = PKG / "_build"
 LIB = PKG / "libbh_render.so"
-ORACLE_SRC = ROOT / "oracle" / "bh_oracle.c"
+ORACLE_SRCS = [ROOT / "oracle" / "bh_oracle.c", ROOT / "oracle" / "bh_bloom_oracle.c"]
 ORACLE_LIB = ROOT / "oracle" / "libbh_oracle.so"
 
 ARCH = os.environ.get("BH_OFFLOAD_ARCH", "gfx950")
@@ -31,6 +31,7 @@ TU_FLAGS = {
     "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
     "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
     "bh_tiles.hip": [],
+    "bh_bloom.hip": ["-ffp-contract=off"],
     "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
 }
@@ -67,10 +68,10 @@ def build_product(force: bool = False) -> Path:
 
 
 def build_oracle(force: bool = False) -> Path:
-    if force or _stale(ORACLE_LIB, [ORACLE_SRC, ROOT / "include" / "bh_render.h", Path(__file__)]):
+    if force or _stale(ORACLE_LIB, [*ORACLE_SRCS, ROOT / "include" / "bh_render.h", Path(__file__)]):
         tmp = ORACLE_LIB.with_suffix(".so.tmp")
         _run(["gcc", "-O2", "-std=c11", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC",
-              "-shared", "-o", str(tmp), str(ORACLE_SRC), "-lm"])
+              "-shared", "-o", str(tmp), *map(str, ORACLE_SRCS), "-lm"])
         os.replace(tmp, ORACLE_LIB)
     return ORACLE_LIB
 

@@ -79,6 +79,10 @@ __device__ __forceinline__ float div6(float x) {
 }
 
 // ---- numerator magnitude guard ----------------------------------------------------------------
+// x / 12 = (x / 6) / 2: halving is exact for the normal quotients of the div6 domain, so this is
+// RN(x / 12) wherever div6 is RN(x / 6) (checked exhaustively as selftest op 5).
+__device__ __forceinline__ float div12(float x) { return div6(x) * 0.5f; }
+
 // key(n) = 2*bits(|n|) - 1 (mod 2^32): +-0 -> 0xFFFFFFFF, tiny -> small, so key(n) < KEY_MIN iff
 // 0 < |n| < DIV_N_MIN; a running v_min3_u32 over keys needs one compare per step.  (A float
 // min of |n| would be one op cheaper but cannot tell 0 from tiny: measured 2x slower overall,

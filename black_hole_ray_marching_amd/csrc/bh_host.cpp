@@ -13,12 +13,14 @@
 #include <vector>
 
 #include "bh_common.hpp"
+#include "bh_srgb.hpp"
 
 struct bh_ctx {
     int device = 0;
     uint32_t* sky = nullptr;       // device RGBA8 texels
     float* lut = nullptr;          // device sRGB->linear table (256 floats)
     float* enc = nullptr;          // device linear->sRGB threshold table (257 floats)
+    uint8_t* enc_b = nullptr;      // device base codes of the table-form encoder (SRGB_BUCKETS bytes)
     uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
@@ -28,6 +30,9 @@ struct bh_ctx {
     uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS words
     uint64_t order_cap = 0;              // tiles the two buffers hold
     uint64_t order_key = ~0ull;          // (width, height, shard) the costs belong to
+    // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
+    std::vector<uint32_t*> bloom_tex;
+    uint64_t bloom_key = ~0ull;
 };
 
 namespace {
@@ -84,6 +89,21 @@ void srgb_encode_table(float T[257]) {
     }
     T[256] = std::numeric_limits<float>::infinity();
 }
+
+}  // namespace
+
+extern "C" __attribute__((visibility("hidden"))) void bh_srgb_bucket_table(const float* T, uint8_t* B) {
+    for (int i = 0; i < bh::SRGB_BUCKETS; ++i) {
+        const uint32_t bits = (bh::SRGB_BUCKET_BASE + (uint32_t)i) << bh::SRGB_BUCKET_SHIFT;
+        float lo;
+        std::memcpy(&lo, &bits, 4);
+        int k = 0;  // code of the bucket's lower end: the largest k with T[k] <= lo
+        while (k < 255 && lo >= T[k + 1]) ++k;
+        B[i] = (uint8_t)k;
+    }
+}
+
+namespace {
 
 // Screen row (in tiles) of the black hole's projection: solve C1 + l0 (C0 - C1) + l2 (C2 - C1) = -t ro0
 // (t > 0) for the barycentrics of the pixel looking at the origin; py = 2 H l2 - 0.5.  Falls back to
@@ -314,8 +334,10 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     c->sky_h = sky_h;
     const size_t bytes = (size_t)sky_w * sky_h * 4u;
     float lut[256], enc[257];
+    uint8_t enc_b[bh::SRGB_BUCKETS];
     srgb_lut(lut);
     srgb_encode_table(enc);
+    bh_srgb_bucket_table(enc, enc_b);
     int st = BH_OK;
     if ((e = hipMalloc(&c->sky, bytes)) != hipSuccess) st = (e == hipErrorOutOfMemory) ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "hipMalloc(sky)");
     else if ((e = hipMalloc(&c->lut, sizeof(lut))) != hipSuccess) st = hip_fail(e, "hipMalloc(lut)");
@@ -323,6 +345,8 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     else if ((e = hipMemcpy(c->lut, lut, sizeof(lut), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(lut)");
     else if ((e = hipMalloc(&c->enc, sizeof(enc))) != hipSuccess) st = hip_fail(e, "hipMalloc(enc)");
     else if ((e = hipMemcpy(c->enc, enc, sizeof(enc), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc)");
+    else if ((e = hipMalloc(&c->enc_b, sizeof(enc_b))) != hipSuccess) st = hip_fail(e, "hipMalloc(enc_b)");
+    else if ((e = hipMemcpy(c->enc_b, enc_b, sizeof(enc_b), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc_b)");
     else if ((e = hipMalloc(&c->counters, 1024)) != hipSuccess) st = hip_fail(e, "hipMalloc(counters)");
     if (st == BH_OK) {
         int cus = 0;
@@ -347,12 +371,162 @@ int bh_destroy(bh_ctx* c) {
     if (c->sky) (void)hipFree(c->sky);
     if (c->lut) (void)hipFree(c->lut);
     if (c->enc) (void)hipFree(c->enc);
+    if (c->enc_b) (void)hipFree(c->enc_b);
     if (c->counters) (void)hipFree(c->counters);
     if (c->tile_cost) (void)hipFree(c->tile_cost);
     if (c->order) (void)hipFree(c->order);
     if (c->order_counters) (void)hipFree(c->order_counters);
+    for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
     (void)hipSetDevice(prev);
     delete c;
+    return BH_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// A same-size pass samples texel centres exactly iff u = RN((x+0.5)/n), RN(u*n) - 0.5 == x for every
+// x < n (then the bilinear weights are exactly 0/1: the pass is the identity on stored texels).
+bool same_size_exact(uint32_t n) {
+    for (uint32_t x = 0; x < n; ++x) {
+        const float u = ((float)x + 0.5f) / (float)n;
+        const float t = u * (float)n - 0.5f;
+        if (t != (float)x) return false;
+    }
+    return true;
+}
+
+struct BloomPlan {
+    uint32_t W, H, levels;
+    uint32_t res[16][2];
+};
+
+// kawase_*sampling.rs:30-39: level l is (W, H) halved l times (integer), at least 1
+BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
+    BloomPlan p{W, H, levels, {}};
+    uint32_t w = W, h = H;
+    for (uint32_t l = 0; l < levels; ++l) {
+        w = w ? w : 1u;
+        h = h ? h : 1u;
+        p.res[l][0] = w;
+        p.res[l][1] = h;
+        w /= 2u;
+        h /= 2u;
+    }
+    return p;
+}
+
+struct BloomRun {
+    bh_ctx* c;
+    hipStream_t s;
+    int err = 0;
+    void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
+              uint32_t* out, uint32_t ow, uint32_t oh) {
+        if (err == 0)
+            err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, a, aw, ah, b, res[0], res[1], out, ow, oh, s);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint32_t H, uint32_t levels,
+             uint32_t schedule, void* out, void* stream) {
+    if (!c || !col || !blackout || !out || W == 0 || H == 0 || levels < 1 || levels > 12 || schedule > BH_BLOOM_LITERAL)
+        return BH_ERR_INVALID_ARG;
+    hipError_t e;
+    if ((e = hipSetDevice(c->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipStream_t s = (hipStream_t)stream;
+    const BloomPlan P = bloom_plan(W, H, levels);
+    const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) &&
+                       same_size_exact(P.res[levels - 1][0]) && same_size_exact(P.res[levels - 1][1]);
+    // scratch: [0, 3*levels) copy_in / remix_in0 / remix_in1 (full), then blur_in, final_in1 (full),
+    // then down[levels], up[levels] at res[l]
+    const uint64_t key = ((uint64_t)W << 40) ^ ((uint64_t)H << 16) ^ levels;
+    if (c->bloom_key != key) {
+        for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
+        c->bloom_tex.clear();
+        c->bloom_key = ~0ull;
+        const size_t full = (size_t)W * H * 4u;
+        for (uint32_t i = 0; i < 3u * levels + 2u; ++i) {
+            uint32_t* t = nullptr;
+            if ((e = hipMalloc(&t, full)) != hipSuccess) return hip_fail(e, "hipMalloc(bloom)");
+            c->bloom_tex.push_back(t);
+        }
+        for (uint32_t k = 0; k < 2; ++k)
+            for (uint32_t l = 0; l < levels; ++l) {
+                uint32_t* t = nullptr;
+                if ((e = hipMalloc(&t, (size_t)P.res[l][0] * P.res[l][1] * 4u)) != hipSuccess)
+                    return hip_fail(e, "hipMalloc(bloom)");
+                c->bloom_tex.push_back(t);
+            }
+        c->bloom_key = key;
+    }
+    uint32_t** T = c->bloom_tex.data();
+    uint32_t **copy_in = T, **remix_in0 = T + levels, **remix_in1 = T + 2 * levels;
+    uint32_t* blur_in = T[3 * levels];
+    uint32_t* final_in1 = T[3 * levels + 1];
+    uint32_t **down = T + 3 * levels + 2, **up = T + 4 * levels + 2;
+    const uint32_t* X = (const uint32_t*)blackout;
+    const uint32_t* C = (const uint32_t*)col;
+    uint32_t* O = (uint32_t*)out;
+    const uint32_t full[2] = {W, H};
+    BloomRun R{c, s};
+    const uint32_t L = levels - 1;
+    if (fused) {
+        // same-size passes are identities (same_size_exact): see bh_bloom.hip
+        const uint32_t* S = X;
+        if (levels > 1) {
+            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, X, copy_in[1], W, H, s);
+            S = copy_in[1];
+        }
+        const uint32_t* dn = S;  // down[0] == S
+        for (uint32_t l = 1; l < levels; ++l) {
+            R.pass(bh_bloom_shader_down, dn, P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1], down[l],
+                   P.res[l][0], P.res[l][1]);
+            dn = down[l];
+        }
+        const uint32_t* u_src = dn;  // up[levels-1] == down[levels-1]
+        for (uint32_t l = 0; l + 1 < levels; ++l) {
+            const uint32_t ti = levels - l - 2;
+            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
+                   P.res[ti][0], P.res[ti][1]);
+            u_src = up[ti];
+        }
+        if (R.err == 0)
+            R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
+    } else {
+        // literal: the reference's render passes in order (oracle/bh_bloom_oracle.c, bho_bloom)
+        if ((e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync(bloom)");
+        auto blur = [&](uint32_t lv, uint32_t* dst) {
+            // blurs[k] with `lv` levels; its input (down[0]) was written by the copy pass
+            for (uint32_t l = 1; l < lv; ++l)
+                R.pass(bh_bloom_shader_down, down[l - 1], P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1],
+                       down[l], P.res[l][0], P.res[l][1]);
+            R.pass(bh_bloom_shader_down, down[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1], nullptr, P.res[lv - 1],
+                   up[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1]);
+            for (uint32_t l = 0; l + 1 < lv; ++l)
+                R.pass(bh_bloom_shader_up, up[lv - l - 1], P.res[lv - l - 1][0], P.res[lv - l - 1][1], nullptr, P.res[l],
+                       up[lv - l - 2], P.res[lv - l - 2][0], P.res[lv - l - 2][1]);
+            R.pass(bh_bloom_shader_up, up[0], W, H, nullptr, P.res[lv - 1], dst, W, H);
+        };
+        for (uint32_t level = 0; level + 1 < levels; ++level) {
+            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, down[0], W, H);
+            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, remix_in0[0], W, H);
+            blur(1, remix_in1[0]);
+            R.pass(bh_bloom_shader_remix, remix_in0[0], W, H, remix_in1[0], full, copy_in[level + 1], W, H);
+        }
+        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, down[0], W, H);
+        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, remix_in0[L], W, H);
+        blur(levels, remix_in1[L]);
+        R.pass(bh_bloom_shader_remix, remix_in0[L], W, H, remix_in1[L], full, final_in1, W, H);
+        R.pass(bh_bloom_shader_remix, C, W, H, final_in1, full, O, W, H);
+        (void)blur_in;
+    }
+    if (R.err != 0) return hip_fail((hipError_t)R.err, "bloom launch");
     return BH_OK;
 }
 

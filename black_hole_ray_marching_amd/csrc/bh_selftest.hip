@@ -32,8 +32,11 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 2: div_core on `count` random (n, d) pairs from the guarded domain, seeded by base
 // op 3: div_core with n = d * m for random small integers m (exact quotients) and n = d*q +- ulps
 // op 4: srgb_encode over every 32-bit pattern in [base, base + count) against a binary search of T
+// op 6: srgb_encode_lut (table form) against srgb_encode over every 32-bit pattern in [base, base + count)
+// op 5: div12 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
 __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, uint64_t count,
-                                                      unsigned long long* cnt, uint32_t* ex, const float* T) {
+                                                      unsigned long long* cnt, uint32_t* ex, const float* T,
+                                                      const uint8_t* B) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         if (op == 0) {
@@ -51,6 +54,19 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             const float got = crm::div6(x), want = x / 6.0f;
             if (__float_as_uint(got) != __float_as_uint(want))
                 record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 5) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            if (crm::key(x) < crm::KEY_MIN) continue;
+            if (x != x || __builtin_isinf(x)) continue;
+            const float got = crm::div12(x), want = x / 12.0f;
+            if (__float_as_uint(got) != __float_as_uint(want))
+                record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 6) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            const uint32_t got = srgb_encode_lut(x, B, T), want = srgb_encode(x, T);  // op 4 pins srgb_encode
+            if (got != want) record(cnt, ex, bits, 0, got, want);
         } else if (op == 4) {
             const uint32_t bits = (uint32_t)(base + i);
             const float x = __uint_as_float(bits);
@@ -87,26 +103,30 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 4 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 6 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;
     unsigned long long* cnt = nullptr;
     uint32_t* ex = nullptr;
     float* T = nullptr;
+    uint8_t* Bd = nullptr;
     float table[bh::SRGB_TABLE];
+    uint8_t btab[bh::SRGB_BUCKETS];
     (void)bh_srgb_encode_table(table);
+    bh_srgb_bucket_table(table, btab);
     int st = BH_OK;
     if (hipMalloc(&cnt, sizeof(*cnt)) != hipSuccess || hipMalloc(&ex, 8 * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&T, sizeof(table)) != hipSuccess) {
+        hipMalloc(&T, sizeof(table)) != hipSuccess || hipMalloc(&Bd, sizeof(btab)) != hipSuccess) {
         st = BH_ERR_OUT_OF_MEMORY;
     } else {
         (void)hipMemset(cnt, 0, sizeof(*cnt));
         (void)hipMemset(ex, 0, 8 * sizeof(uint32_t));
         (void)hipMemcpy(T, table, sizeof(table), hipMemcpyHostToDevice);
+        (void)hipMemcpy(Bd, btab, sizeof(btab), hipMemcpyHostToDevice);
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex, T);
+        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex, T, Bd);
         if (hipDeviceSynchronize() != hipSuccess) st = BH_ERR_HIP;
         unsigned long long h = 0;
         (void)hipMemcpy(&h, cnt, sizeof(h), hipMemcpyDeviceToHost);
@@ -116,6 +136,7 @@ extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_
     if (cnt) (void)hipFree(cnt);
     if (ex) (void)hipFree(ex);
     if (T) (void)hipFree(T);
+    if (Bd) (void)hipFree(Bd);
     (void)hipSetDevice(prev);
     return st;
 }

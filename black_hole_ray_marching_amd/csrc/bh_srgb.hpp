@@ -26,6 +26,23 @@ __device__ __forceinline__ uint32_t srgb_encode(float x, const float* T) {
     return (uint32_t)c;
 }
 
+// Table form without log2/exp2 (the bloom chain stores ~9 channels per pixel): on [2^-13, 1) every
+// bucket of 2^-7 relative width (7 mantissa bits) spans at most one code boundary, so the code is
+// the bucket's base code B[i] (the code of its lower end) plus one where x reaches T[B[i] + 1].
+// Below 2^-13 the code is 0 (T[1] > 2^-13), which bucket 0 already gives.  Exhaustively checked on
+// the device (bh_selftest_crmath op 6).  The host builds B from T (bh_host.cpp).
+constexpr uint32_t SRGB_BUCKET_SHIFT = 16;
+constexpr uint32_t SRGB_BUCKET_BASE = (127u - 13u) << 7;  // bucket index of 2^-13
+constexpr int SRGB_BUCKETS = 13 * 128;                   // [2^-13, 1)
+
+__device__ __forceinline__ uint32_t srgb_encode_lut(float x, const uint8_t* B, const float* T) {
+    const float xc = fminf(fmaxf(x, 0.0f), 1.0f);  // fmaxf(NaN, 0) = 0
+    int32_t i = (int32_t)(__float_as_uint(xc) >> SRGB_BUCKET_SHIFT) - (int32_t)SRGB_BUCKET_BASE;
+    i = i < 0 ? 0 : (i > SRGB_BUCKETS - 1 ? SRGB_BUCKETS - 1 : i);
+    const uint32_t c = B[i];
+    return c + (xc >= T[c + 1] ? 1u : 0u);
+}
+
 // BGRA8 texel (byte 0 = B) of linear rgb, alpha 1.
 __device__ __forceinline__ uint32_t srgb_bgra8(float r, float g, float b, const float* T) {
     return srgb_encode(b, T) | (srgb_encode(g, T) << 8) | (srgb_encode(r, T) << 16) | 0xFF000000u;

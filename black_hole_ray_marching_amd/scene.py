@@ -210,6 +210,17 @@ class Scene:
                                  C.byref(d), _stream_handle(stream)), "bh_render")
 
 
+    def bloom(self, col, blackout, out, *, levels: int = 3, schedule: int = 0, width: int | None = None,
+              height: int | None = None, stream=None) -> None:
+        """Bloom::render (src/bloom.rs:53-71): the Kawase bloom + remix chain over this scene's two
+        BGRA8-sRGB targets (render with fmt=BH_OUT_BGRA8_SRGB) into `out` (the surface).  levels=3 is
+        the reference's (src/state.rs:125)."""
+        if col is None or blackout is None or out is None:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, "bloom: col, blackout and out are required")
+        check(self.lib.bh_bloom(self._ctx, _ptr(col), _ptr(blackout), width or self.width, height or self.height,
+                                levels, schedule, _ptr(out), _stream_handle(stream)), "bh_bloom")
+
+
 def _stream_handle(stream) -> int | None:
     if stream is None:
         try:

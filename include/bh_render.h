@@ -183,6 +183,18 @@ int bh_destroy(bh_ctx* ctx);
 int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* uniforms,
               const bh_render_desc* desc, void* hip_stream);
 
+/* Bloom::render (src/bloom.rs:53-71): the reference's Kawase bloom + remix chain over the scene's two
+ * targets, on BGRA8-sRGB images (bh_render with BH_OUT_BGRA8_SRGB): `col` (full_image_input),
+ * `blackout` (blackout_input) -> `out` (the surface), all width x height, row-major, device memory.
+ * `levels` = the Bloom's level count (src/state.rs:125 uses 3; 1..12).  Scratch textures live in
+ * the context (allocated at the first call for a size).  `schedule`: BH_BLOOM_AUTO fuses passes
+ * whenever that gives identical bytes (always for power-of-two sizes), BH_BLOOM_LITERAL runs the
+ * reference's render passes one by one.  Asynchronous on `hip_stream`. */
+#define BH_BLOOM_AUTO    0u
+#define BH_BLOOM_LITERAL 1u
+int bh_bloom(bh_ctx* ctx, const void* col_bgra8, const void* blackout_bgra8, uint32_t width, uint32_t height,
+             uint32_t levels, uint32_t schedule, void* out_bgra8, void* hip_stream);
+
 /* Number of 8x8 tiles owned by `shard_index` of `shard_count` in a width x height frame. */
 int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);
 
@@ -201,7 +213,8 @@ int bh_srgb_encode_table(float* out257);
  * results on `device` (op 0: sqrt over float bit patterns [base, base+count); op 1: x/6 over bit
  * patterns [base, base+count); op 2: n/d on `count` random pairs seeded by base; op 3: n/d near exact
  * quotients; op 4: the BGRA8 sRGB encoder over float bit patterns [base, base+count) against a
- * binary search of bh_srgb_encode_table).  *out_mismatches = number of differing results;
+ * binary search of bh_srgb_encode_table; op 5: x/12 as the bloom chain computes it, over bit
+ * patterns [base, base+count); op 6: the bloom chain's table-form sRGB encoder against op 4's).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

@@ -35,6 +35,8 @@ def load() -> C.CDLL:
         lib.bho_srgb_encode.argtypes = [C.c_float]
         lib.bho_srgb_encode_array.restype = None
         lib.bho_srgb_encode_array.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        lib.bho_bloom.restype = C.c_int
+        lib.bho_bloom.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]
         lib.bho_srgb_table_mismatches.restype = C.c_uint64
         lib.bho_srgb_table_mismatches.argtypes = [C.c_void_p, C.c_int]
         _lib = lib
@@ -93,6 +95,20 @@ def srgb_table_mismatches(table: np.ndarray, threads: int = 0) -> int:
     t = np.ascontiguousarray(table, np.float32)
     assert t.shape == (257,)
     return int(load().bho_srgb_table_mismatches(t.ctypes.data, threads))
+
+
+def bloom(col: np.ndarray, blackout: np.ndarray, levels: int = 3, threads: int = 0) -> np.ndarray:
+    """bho_bloom (oracle/bh_bloom_oracle.c): the reference's Kawase bloom + remix chain on (H, W, 4)
+    BGRA8 images -> the (H, W, 4) BGRA8 surface."""
+    col = np.ascontiguousarray(col, np.uint8)
+    blackout = np.ascontiguousarray(blackout, np.uint8)
+    assert col.shape == blackout.shape and col.ndim == 3 and col.shape[2] == 4
+    H, W = col.shape[:2]
+    out = np.empty_like(col)
+    st = load().bho_bloom(col.ctypes.data, blackout.ctypes.data, W, H, levels, out.ctypes.data, threads)
+    if st != 0:
+        raise ValueError(f"bho_bloom: {st}")
+    return out
 
 
 def srgb_lut() -> np.ndarray:

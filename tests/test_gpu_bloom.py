@@ -1,0 +1,83 @@
+"""GPU parity of the post-processing chain (bh_bloom: Kawase bloom + remix)
+against oracle/bh_bloom_oracle.c: bit-exact BGRA8 bytes, fused and literal schedules."""
+import numpy as np
+import pytest
+
+import black_hole_ray_marching_amd as bh
+import oracle
+from tests._cases import camera_uniform, uniforms
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _img(rng, H, W, sparse=False):
+    t = rng.integers(0, 256, size=(H, W, 4), dtype=np.uint8)
+    if sparse:
+        t[..., :3] = np.where(rng.random((H, W, 1)) < 0.05, t[..., :3], 0)
+    t[..., 3] = 255
+    return t
+
+
+def _gpu_bloom(torch, scene, col, bo, levels, schedule):
+    H, W = col.shape[:2]
+    c, b = torch.from_numpy(col).cuda(), torch.from_numpy(bo).cuda()
+    out = torch.zeros_like(c)
+    scene.bloom(c, b, out, levels=levels, schedule=schedule, width=W, height=H)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
+@pytest.mark.parametrize("H,W,levels", [(128, 256, 3), (64, 64, 1), (64, 128, 2), (120, 200, 3), (37, 53, 3),
+                                        (256, 512, 5)])
+def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
+    """AUTO fuses passes for sizes whose same-size sampling is exact (powers of two) and runs the
+    literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes."""
+    rng = np.random.default_rng(W * 7 + H + levels)
+    col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
+    scene = bh.Scene(16, 16, sky=sky_small)
+    got = _gpu_bloom(torch_cuda, scene, col, bo, levels, schedule)
+    want = oracle.bloom(col, bo, levels)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    scene.close()
+
+
+def test_render_then_bloom_matches_oracle_chain(torch_cuda, sky_small):
+    """The reference's frame: Scene::render into the two Bgra8UnormSrgb targets, then
+    Bloom::render to the surface -- GPU end to end vs the two oracles end to end."""
+    torch = torch_cuda
+    W, H, cap = 512, 256, 512
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
+    col = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    bo = torch.zeros_like(col)
+    out = torch.zeros_like(col)
+    scene.render(col, bo, fmt=bh.BH_OUT_BGRA8_SRGB)
+    scene.bloom(col, bo, out)
+    torch.cuda.synchronize()
+    o = oracle.render_rows(camera_uniform("A", W, H).to_bytes(), bytes(uniforms().to_c()), sky_small, W, H, cap, 3)
+
+    def bgra(c):
+        e = oracle.srgb_encode(c[..., :3])
+        return np.stack([e[..., 2], e[..., 1], e[..., 0], np.full(e.shape[:2], 255, np.uint8)], -1)
+    oc, ob = bgra(o[0]), bgra(o[1])
+    assert np.array_equal(col.cpu().numpy(), oc) and np.array_equal(bo.cpu().numpy(), ob)
+    assert np.array_equal(out.cpu().numpy(), oracle.bloom(oc, ob, 3))
+    scene.close()
+
+
+def test_bloom_invalid_arguments(torch_cuda, sky_small):
+    scene = bh.Scene(16, 16, sky=sky_small)
+    t = torch_cuda.zeros((16, 16, 4), dtype=torch_cuda.uint8, device="cuda")
+    with pytest.raises(bh.BhError):
+        scene.bloom(t, t, t, levels=0)
+    with pytest.raises(bh.BhError):
+        scene.bloom(t, t, t, schedule=7)
+    scene.close()

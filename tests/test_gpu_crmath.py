@@ -53,3 +53,15 @@ def test_srgb_encode_exhaustive(lib):
     # the BGRA8 encoder (hardware log2/exp2 estimate + threshold fix-up) over all 2^32 patterns
     m, ex = run(lib, 4, 0, 1 << 32)
     assert m == 0, ex
+
+
+def test_div12_exhaustive(lib):
+    # x / 12 of the bloom chain's up-sampling filter, over all 2^32 patterns in the guarded domain
+    m, ex = run(lib, 5, 0, 1 << 32)
+    assert m == 0, ex
+
+
+def test_srgb_encode_table_form_exhaustive(lib):
+    # the bloom chain's log-free encoder (bucket base codes + one threshold) over all 2^32 patterns
+    m, ex = run(lib, 6, 0, 1 << 32)
+    assert m == 0, ex

@@ -1,0 +1,50 @@
+"""Post-processing chain (bh_bloom) on one GPU: time per frame of the Kawase
+bloom + remix over a 4096x2048 BGRA8 frame (the march kernel's own two targets), HIP events on the
+stream, fused (AUTO) and literal schedules; HBM roofline with the chain's algorithmic bytes
+(read col + blackout, write the surface: 12 B/pixel).
+    python tools/bench_bloom.py [--width 4096 --height 2048 --levels 3 --steps 100]"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch  # noqa: E402
+
+import black_hole_ray_marching_amd as bh  # noqa: E402
+
+p = argparse.ArgumentParser()
+p.add_argument("--width", type=int, default=4096)
+p.add_argument("--height", type=int, default=2048)
+p.add_argument("--levels", type=int, default=3)
+p.add_argument("--steps", type=int, default=100)
+p.add_argument("--warmup", type=int, default=10)
+args = p.parse_args()
+W, H = args.width, args.height
+scene = bh.Scene(W, H, sky=bh.synthetic_sky(), max_iters=512, math=bh.BH_MATH_EXACT)
+col = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+bo = torch.empty_like(col)
+out = torch.empty_like(col)
+scene.render(col, bo, fmt=bh.BH_OUT_BGRA8_SRGB)
+stream = torch.cuda.current_stream()
+for name, sched in (("auto", bh.BH_BLOOM_AUTO), ("literal", bh.BH_BLOOM_LITERAL)):
+    for _ in range(args.warmup):
+        scene.bloom(col, bo, out, levels=args.levels, schedule=sched, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for a, b in ev:
+        a.record(stream)
+        scene.bloom(col, bo, out, levels=args.levels, schedule=sched, stream=stream)
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    alg = W * H * 12
+    print(json.dumps({"bloom_schedule": name, "width": W, "height": H, "levels": args.levels,
+                      "avg_ms": round(float(ms.mean()), 5), "min_ms": round(float(ms.min()), 5),
+                      "mpix_per_s": round(W * H / (ms.mean() / 1e3) / 1e6, 1),
+                      "roofline_hbm": {"bound": "hbm", "achieved": round(alg / (ms.mean() / 1e3) / 1e9, 1),
+                                       "peak": 8000.0, "unit": "GB/s",
+                                       "frac": round(alg / (ms.mean() / 1e3) / 1e9 / 8000.0, 4),
+                                       "algorithmic_bytes": alg,
+                                       "note": "read col + blackout, write the surface (BGRA8)"}}))
