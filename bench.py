@@ -116,11 +116,11 @@ def main() -> None:
         frame = torch.empty((H, W, 4), dtype=ch_dtype, device=dev) if rank == 0 else None
         shard = dict(layout=bh.BH_LAYOUT_TILES, shard_index=rank, shard_count=n)
 
-        def on_frame(i, gathered):
-            bh.tiles_unpack(gathered, frame, W, H, n, stride, bpp, stream=stream)
+        def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
+            bh.tiles_unpack(gathered, frame, W, H, n, stride, bpp, stream=torch.cuda.current_stream(dev))
 
         pipe = multigpu.GatherPipeline(lambda: torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev),
-                                       rank, n, on_frame)
+                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
         col = pipe.buffer(0)
 
     frame_no = [0]

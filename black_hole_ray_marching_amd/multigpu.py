@@ -90,9 +90,14 @@ class GatherPipeline:
         pipe.drain()
 
     `on_frame(i, gathered)` runs on rank 0 once frame i's gather is complete (stream-ordered):
-    `gathered` is the (world * stride * 64, C) buffer of all ranks' packed tiles."""
+    `gathered` is the (world * stride * 64, C) buffer of all ranks' packed tiles.  With
+    `side_stream` (rank 0, CUDA), on_frame is issued on that stream -- the unpack (HBM-bound) then
+    overlaps the next frame's render (VALU-bound) instead of queueing behind it on the render
+    stream; before a receive buffer is gathered into again, the render stream waits for the unpack
+    that read it (and RCCL's stream follows the render stream)."""
 
-    def __init__(self, make_buffer, rank: int, world: int, on_frame=None, depth: int = 2, group=None):
+    def __init__(self, make_buffer, rank: int, world: int, on_frame=None, depth: int = 2, group=None,
+                 side_stream=None):
         import torch
         if depth < 1:
             raise ValueError("depth >= 1")
@@ -105,6 +110,8 @@ class GatherPipeline:
             self.recv = [torch.empty((world * b.shape[0], *b.shape[1:]), dtype=b.dtype, device=b.device)
                          for _ in range(depth)]
         self.pending = []  # (frame, work) in submission order
+        self.side = side_stream if rank == 0 else None
+        self.consumed = [None] * depth  # per slot: event after the on_frame that read recv[slot]
 
     def buffer(self, i: int):
         return self.bufs[i % self.depth]
@@ -117,6 +124,10 @@ class GatherPipeline:
             if self.rank == 0:
                 self.recv[slot].copy_(self.bufs[slot])
         else:
+            if self.consumed[slot] is not None:
+                import torch
+                torch.cuda.current_stream().wait_event(self.consumed[slot])
+                self.consumed[slot] = None
             gl = list(self.recv[slot].view(self.world, *self.bufs[slot].shape).unbind(0)) if self.rank == 0 else None
             work = dist.gather(self.bufs[slot], gl, dst=0, group=self.group, async_op=True)
         self.pending.append((i, work))
@@ -125,10 +136,21 @@ class GatherPipeline:
 
     def _finish_one(self) -> None:
         i, work = self.pending.pop(0)
+        slot = i % self.depth
         if work is not None:
-            work.wait()
+            work.wait()  # the current stream: the send buffer may be rendered into again
         if self.rank == 0 and self.on_frame is not None:
-            self.on_frame(i, self.recv[i % self.depth])
+            if self.side is None:
+                self.on_frame(i, self.recv[slot])
+            else:
+                import torch
+                with torch.cuda.stream(self.side):
+                    if work is not None:
+                        work.wait()  # the side stream: the received frame is complete
+                    self.on_frame(i, self.recv[slot])
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                    self.consumed[slot] = ev
 
     def drain(self) -> None:
         while self.pending:
