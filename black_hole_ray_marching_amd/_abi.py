@@ -44,6 +44,15 @@ class bh_camera(C.Structure):
                 ("aspect", C.c_float), ("fovy", C.c_float), ("znear", C.c_float), ("zfar", C.c_float)]
 
 
+class bh_controller(C.Structure):
+    _fields_ = [(n, C.c_uint8) for n in ("forward", "backward", "left", "right", "up", "down", "pan_up",
+                                          "pan_down", "pan_left", "pan_right", "exp_towards_origin",
+                                          "exp_away_origin", "mouse_pressed", "has_prev_cursor",
+                                          "has_curr_cursor", "_pad")] + \
+              [("prev_cursor", C.c_float * 2), ("curr_cursor", C.c_float * 2), ("speed", C.c_float),
+               ("pan_speed", C.c_float)]
+
+
 class bh_render_desc(C.Structure):
     _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("max_iters", C.c_uint32),
                 ("scene_flags", C.c_uint32), ("format", C.c_uint32), ("math", C.c_uint32),
@@ -74,6 +83,8 @@ SIGNATURES = {
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
+    "bh_controller_update": (C.c_int, [C.POINTER(bh_controller), C.POINTER(bh_camera), C.c_float, C.c_int,
+                                       C.POINTER(C.c_int)]),
     "bh_bloom": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_void_p, C.c_void_p]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),

@@ -220,6 +220,69 @@ int bh_camera_default(uint32_t width, uint32_t height, bh_camera* out) {
     return BH_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// glam 0.24 Quat (f32): from_axis_angle and mul_vec3 (the SSE2 path evaluates the same formula with
+// the same operand order: dot = (x + y) + z, no FMA)
+struct Q4 { float x, y, z, w; };
+Q4 q_from_axis_angle(V3 axis, float angle) {
+    const float h = angle * 0.5f;
+    const float s = std::sin(h), c = std::cos(h);  // f32::sin_cos
+    const V3 v = v_mul(axis, s);
+    return {v.x, v.y, v.z, c};
+}
+V3 q_mul_vec3(Q4 q, V3 rhs) {
+    const float w = q.w;
+    const V3 b{q.x, q.y, q.z};
+    const float b2 = v_dot(b, b);
+    return v_add(v_add(v_mul(rhs, w * w - b2), v_mul(b, v_dot(rhs, b) * 2.0f)), v_mul(v_cross(b, rhs), w * 2.0f));
+}
+float axis_norm(uint8_t neg, uint8_t pos) { return (neg == pos) ? 0.0f : (pos ? 1.0f : -1.0f); }
+}  // namespace
+
+extern "C" {
+
+int bh_controller_update(const bh_controller* k, bh_camera* cam, float dt, int do_pan, int* moved) {
+    if (!k || !cam) return BH_ERR_INVALID_ARG;
+    V3 pos{cam->pos[0], cam->pos[1], cam->pos[2]};
+    V3 dir{cam->dir[0], cam->dir[1], cam->dir[2]};
+    V3 up{cam->up[0], cam->up[1], cam->up[2]};
+    auto right = [&] { return v_cross(up, dir); };  // Camera::right = up x dir (camera.rs:32)
+    const float xn = axis_norm(k->left, k->right), zn = axis_norm(k->backward, k->forward);
+    const float yn = axis_norm(k->down, k->up);
+    const float xm = dt * k->speed * xn, zm = dt * k->speed * zn, ym = dt * k->speed * yn;
+    pos = v_add(pos, v_mul(right(), xm));
+    pos = v_add(pos, v_mul(dir, zm));
+    pos = v_add(pos, v_mul(up, ym));
+    const float en = axis_norm(k->exp_towards_origin, k->exp_away_origin);
+    pos = v_mul(pos, std::exp(-dt * en));
+    const float xpn = axis_norm(k->pan_left, k->pan_right), ypn = axis_norm(k->pan_up, k->pan_down);
+    const float xp = dt * k->pan_speed * xpn, yp = dt * k->pan_speed * ypn;
+    auto rotate = [&](V3 axis, float angle) {
+        const Q4 q = q_from_axis_angle(axis, angle);
+        dir = q_mul_vec3(q, dir);
+        up = q_mul_vec3(q, up);
+    };
+    rotate(V3{0.0f, 1.0f, 0.0f}, xp);
+    rotate(right(), yp);
+    float mx = 0.0f, my = 0.0f;  // cursor_movement (camera.rs:268-278)
+    if (k->has_prev_cursor && k->has_curr_cursor) {
+        mx = k->curr_cursor[0] - k->prev_cursor[0];
+        my = k->curr_cursor[1] - k->prev_cursor[1];
+    }
+    const float ps = dt * k->pan_speed;
+    if (k->mouse_pressed && do_pan) {
+        rotate(V3{0.0f, 1.0f, 0.0f}, ps * mx);
+        rotate(right(), ps * my);
+    }
+    cam->pos[0] = pos.x; cam->pos[1] = pos.y; cam->pos[2] = pos.z;
+    cam->dir[0] = dir.x; cam->dir[1] = dir.y; cam->dir[2] = dir.z;
+    cam->up[0] = up.x; cam->up[1] = up.y; cam->up[2] = up.z;
+    if (moved) *moved = (xn != 0.0f) | (yn != 0.0f) | (zn != 0.0f) | (xpn != 0.0f) | (ypn != 0.0f);
+    return BH_OK;
+}
+
 int bh_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
                       bh_camera* out) {
     if (!pos || !target) return BH_ERR_INVALID_ARG;

@@ -59,6 +59,52 @@ class Camera:
                               (C.c_float * 3)(*self.up), self.aspect, self.fovy, self.znear, self.zfar)
 
 
+class CameraController:
+    """CameraController (src/camera.rs:115-366): key state, speeds and cursor -> camera motion.
+    `process_key` takes the reference's key names (process_event :186-261); `update_camera` is
+    update_camera (:280-366) through the C ABI (glam f32 arithmetic).  Driving it with a scripted key
+    sequence gives the camera paths of an offline, multi-frame render (tools/render_path.py)."""
+
+    KEYS = {"W": "forward", "S": "backward", "A": "left", "D": "right", "Space": "up", "F": "down",
+            "ArrowUp": "pan_up", "ArrowDown": "pan_down", "ArrowLeft": "pan_left", "ArrowRight": "pan_right",
+            "P": "exp_towards_origin", "O": "exp_away_origin"}
+
+    def __init__(self, speed: float = 5.0, pan_speed: float = 0.5) -> None:  # src/scene.rs:78
+        self.c = _abi.bh_controller()
+        self.c.speed, self.c.pan_speed = speed, pan_speed
+
+    def process_key(self, key: str, pressed: bool) -> bool:
+        if key == "Q":
+            if pressed:
+                self.c.speed = float(np.float32(self.c.speed) / np.float32(1.5))
+            return True
+        if key == "E":
+            if pressed:
+                self.c.speed = float(np.float32(self.c.speed) * np.float32(1.5))
+            return True
+        if key not in self.KEYS:
+            return False
+        setattr(self.c, self.KEYS[key], 1 if pressed else 0)
+        return True
+
+    def process_mouse(self, pressed: bool) -> None:
+        self.c.mouse_pressed = 1 if pressed else 0
+
+    def process_cursor(self, x: float, y: float) -> None:
+        """CursorMoved: prev <- curr, curr <- (x, y) (as f32)."""
+        self.c.prev_cursor[0], self.c.prev_cursor[1] = self.c.curr_cursor[0], self.c.curr_cursor[1]
+        self.c.has_prev_cursor = self.c.has_curr_cursor
+        self.c.curr_cursor[0], self.c.curr_cursor[1] = float(np.float32(x)), float(np.float32(y))
+        self.c.has_curr_cursor = 1
+
+    def update_camera(self, camera: "Camera", dt: float, do_pan: bool = False) -> tuple["Camera", bool]:
+        cc = camera.to_c()
+        moved = C.c_int(0)
+        check(load().bh_controller_update(C.byref(self.c), C.byref(cc), float(np.float32(dt)), int(do_pan),
+                                          C.byref(moved)), "bh_controller_update")
+        return Camera._from_c(cc), bool(moved.value)
+
+
 class CameraUniform:
     """src/uniforms.rs:98-133 — the 112-byte WGSL `Camera` uniform."""
 
@@ -241,7 +287,7 @@ def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_s
                                  bytes_per_pixel, _stream_handle(stream)), "bh_tiles_unpack")
 
 
-__all__ = ["Camera", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+__all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
            "srgb_encode_table", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

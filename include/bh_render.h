@@ -163,6 +163,26 @@ const char* bh_last_error(void);
 /* Defaults of Scene::new (src/scene.rs:68-137). */
 int bh_uniforms_default(bh_uniforms* out);
 int bh_camera_default(uint32_t width, uint32_t height, bh_camera* out);
+/* CameraController (src/camera.rs:115-366), the host camera layer of an animated / offline camera
+ * path: the controller's key state (process_event, :186-261, as booleans), its two speeds
+ * (CameraController::new(5.0, 0.5) at src/scene.rs:78; Q / E scale `speed` by 1/1.5 and 1.5) and
+ * the last two cursor positions (as f32, the conversion of :270-276). */
+typedef struct {
+    uint8_t forward, backward, left, right, up, down;  /* W, S, A, D, Space, F */
+    uint8_t pan_up, pan_down, pan_left, pan_right;     /* arrow keys */
+    uint8_t exp_towards_origin, exp_away_origin;       /* P, O */
+    uint8_t mouse_pressed;                             /* left button */
+    uint8_t has_prev_cursor, has_curr_cursor;          /* Option::Some */
+    uint8_t _pad;
+    float prev_cursor[2], curr_cursor[2];
+    float speed, pan_speed;
+} bh_controller;
+
+/* CameraController::update_camera(camera, delta_time, do_pan) (src/camera.rs:280-366): moves and
+ * rotates *camera by dt seconds of the controller's state, glam f32 arithmetic (Quat::from_axis_angle,
+ * Quat::mul_vec3).  *moved (optional) = the function's return value. */
+int bh_controller_update(const bh_controller* ctrl, bh_camera* camera, float dt, int do_pan, int* moved);
+
 /* CameraUniform::new (src/uniforms.rs:108-122) + ::update (:123-133). */
 int bh_camera_uniform_update(const bh_camera* camera, bh_camera_uniform* out);
 /* Camera aimed at `target` from `pos` (up +Y, fovy pi/2): SURVEY §8d cameras B and C. */
