@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--max-iters", type=int, default=512)
     p.add_argument("--camera", choices=["A", "B", "C"], default="A")
+    p.add_argument("--surfaces", choices=["on", "off"], default="on",
+                   help="off = scene_flags 0 (no disc, no markers: BASELINE config 1's scene)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores in this process's affinity)")
     p.add_argument("--cpu-reps", type=int, default=3)
@@ -96,7 +98,8 @@ def main() -> None:
              "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
 
     sky = bh.synthetic_sky(4096, 2048)
-    scene = bh.Scene(W, H, sky=sky, device=local, max_iters=cap, math=math_mode)
+    flags = bh.BH_SCENE_DEFAULT if args.surfaces == "on" else 0
+    scene = bh.Scene(W, H, sky=sky, device=local, max_iters=cap, math=math_mode, scene_flags=flags)
     if args.camera != "A":
         scene.update(bh.Camera.look_at(*CAMERAS[args.camera], W, H))
     stream = torch.cuda.current_stream(dev)
@@ -187,7 +190,7 @@ def main() -> None:
     if rank == 0:
         pmc = _pmc_entry(W, H, cap, args)
         value = W * H * args.steps / elapsed / 1e6
-        achieved_tf = sum_steps * F_STEP[3] / kern_avg_s / 1e12
+        achieved_tf = sum_steps * F_STEP[flags] / kern_avg_s / 1e12
         alg_bytes = my_px * bpp * 2 + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
         result = {
@@ -204,7 +207,8 @@ def main() -> None:
             "dtype": "f32",
             "data": "synthetic (splitmix64-seeded 4096x2048 RGBA8 sRGB sky; reference default camera)",
             "config": {
-                "workload": f"{W}x{H} frame, cap {cap} RK steps, disc+markers+sky, camera {args.camera}, "
+                "workload": f"{W}x{H} frame, cap {cap} RK steps, "
+                            f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}, "
                             f"{args.fmt} col+blackout, {args.math} math"
                             + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n}, RCCL gather of col to rank 0 "
                                                   "overlapped with the next frame, unpack on rank 0"),
@@ -221,7 +225,7 @@ def main() -> None:
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
                          "traffic": pmc.get("hbm_bytes_per_launch"),
                          "valu_busy": pmc.get("valu_busy_est"),
-                         "note": f"{F_STEP[3]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
+                         "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
                                  "launch time (HIP events on the render stream); FP32 VALU-bound, no "
                                  "MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU issue "
                                  "cycles / SIMD cycles, both from rocprofv3 PMC passes of this configuration "
@@ -263,11 +267,11 @@ def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
 
     threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
     cu, U = scene.camera_uniform.to_bytes(), bytes(scene.uniforms.to_c())
-    oracle.render_rows(cu, U, sky, W, H, cap, 3, 0, 64, threads=threads)  # warm-up
+    oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, 0, 64, threads=threads)  # warm-up
     times = []
     for _ in range(max(1, args.cpu_reps)):
         t0 = time.perf_counter()
-        o_col, _, o_nrk, o_fate = oracle.render_rows(cu, U, sky, W, H, cap, 3, threads=threads)
+        o_col, _, o_nrk, o_fate = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, threads=threads)
         times.append(time.perf_counter() - t0)
     cpu_s = float(np.median(times))
     cpu_baseline = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
