@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
     p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores in this process's affinity)")
     p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--graph", action="store_true",
+                   help="N=1: capture one frame's bh_render (order kernels + march) in a HIP graph and replay it")
     p.add_argument("--verify-gather", action="store_true",
                    help="N>1: rank 0 compares the assembled frame with its own full-frame render (bitwise)")
     return p.parse_args()
@@ -128,9 +130,23 @@ def main() -> None:
 
     frame_no = [0]
 
-    def render(**kw):
+    def render_direct(**kw):
         scene.render(col if pipe is None else pipe.buffer(frame_no[0]), bo, fmt=fmt, stream=stream,
                      schedule=sched, **shard, **kw)
+
+    graph = None
+    if args.graph and n == 1:
+        render_direct()  # allocate the per-geometry buffers before capture
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            scene.render(col, bo, fmt=fmt, stream=torch.cuda.current_stream(dev), schedule=sched, **shard)
+
+    def render(**kw):
+        if graph is not None and not kw:
+            graph.replay()
+        else:
+            render_direct(**kw)
 
     def exchange():
         if pipe is not None:
@@ -214,7 +230,8 @@ def main() -> None:
                                                   "overlapped with the next frame, unpack on rank 0"),
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
                 "schedule": args.schedule, "format": args.fmt,
-                "parallelism": "single GPU" if n == 1 else f"tile-sharded x{n}"
+                "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
+                               else f"tile-sharded x{n}"
                                + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
             },
             "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u>", "launches": args.steps,

@@ -27,7 +27,7 @@ struct bh_ctx {
     // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order
     uint8_t* tile_cost = nullptr;
     uint32_t* order = nullptr;
-    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS words
+    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS + 1 words, zero between frames
     uint64_t order_cap = 0;              // tiles the two buffers hold
     uint64_t order_key = ~0ull;          // (width, height, shard) the costs belong to
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
@@ -664,8 +664,11 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
                     (he = hipMalloc(&c->order, nt * sizeof(uint32_t))) == hipSuccess)
                     c->order_cap = nt;
             }
-            if (he == hipSuccess && !c->order_counters)
-                he = hipMalloc(&c->order_counters, 2 * bh::ORDER_BUCKETS * sizeof(uint32_t));
+            if (he == hipSuccess && !c->order_counters) {
+                he = hipMalloc(&c->order_counters, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t));
+                if (he == hipSuccess)
+                    he = hipMemsetAsync(c->order_counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
+            }
             if (he == hipSuccess) he = hipMemsetAsync(c->tile_cost, 0, nt, s);
             if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order buffers"); }
             c->order_key = key;

@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const T* __restrict__
 // Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), stable
 // enough: slots are visited in centre-out order and each block reserves its bucket ranges with one
 // atomic per bucket, so ties keep (roughly) the centre-out order.  counters: [0..B) counts,
-// [B..2B) cursors, zeroed before the count pass.
+// [B..2B) cursors, [2B] the scatter's block ticket; all zero between frames (zeroed once at
+// allocation, then by the last scatter block of every frame).
 __global__ void __launch_bounds__(256) order_count_kernel(const uint8_t* __restrict__ cost, uint32_t n,
                                                         uint32_t L, uint32_t c, uint32_t* counters) {
     __shared__ uint32_t hist[ORDER_BUCKETS];
@@ -59,6 +60,16 @@ __global__ void __launch_bounds__(256) order_scatter_kernel(const uint8_t* __res
     }
     __syncthreads();
     if (i < n) order[base[b] + k] = t;
+    // the last block to finish resets the counters for the next frame (self-resetting: graph
+    // capture replays this kernel without a memset node).  counters[2B] is the block ticket.
+    if (threadIdx.x == 0) {
+        __threadfence();
+        const uint32_t ticket = atomicAdd(&counters[2 * ORDER_BUCKETS], 1u);
+        if (ticket == gridDim.x - 1u) {
+            __threadfence();
+            for (uint32_t j = 0; j <= 2 * ORDER_BUCKETS; ++j) atomicExch(&counters[j], 0u);
+        }
+    }
 }
 
 }  // namespace bh
@@ -68,8 +79,6 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
                                                                          uint32_t* counters, uint32_t* order,
                                                                          hipStream_t s) {
     if (n == 0) return 0;
-    hipError_t e = hipMemsetAsync(counters, 0, 2 * bh::ORDER_BUCKETS * sizeof(uint32_t), s);
-    if (e != hipSuccess) return (int)e;
     const uint32_t blocks = (n + 255u) / 256u;
     hipLaunchKernelGGL(bh::order_count_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters);
     hipLaunchKernelGGL(bh::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters, order);
