@@ -549,26 +549,42 @@ __device__ __forceinline__ bool same_state(const RayState& st, const Hist& h) {
 // history states live in LDS (ping-pong slots by iteration parity), not VGPRs: holding them in
 // registers takes the kernel from 61 to 73 VGPRs (8 -> 6 waves per SIMD) and measured slower.
 struct HistLds { float4 a[2][2][64]; };  // [slot][ro+tr | rd+outside][lane]
+// XOR-fold of the state compared by same_state: equal states have equal hashes, so a hash match is
+// only a candidate and the full states (in LDS) decide.  The hashes live in 2 VGPRs, so the common
+// case reads no LDS and never waits for it (the serial chain of a lone tail wave is the frame's
+// critical path).
+__device__ __forceinline__ uint32_t state_hash(const RayState& st) {
+    return (__float_as_uint(st.ro.x) ^ __float_as_uint(st.ro.y) ^ __float_as_uint(st.ro.z) ^
+            __float_as_uint(st.rd.x) ^ __float_as_uint(st.rd.y) ^ __float_as_uint(st.rd.z) ^
+            __float_as_uint(st.travelled)) + (st.outside ? 0x9E3779B9u : 0u);
+}
 __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& steps,
                                                  HistLds& H, uint32_t lane) {
+    // h2: hash of the state two iterations back (none yet: a value that forces a full compare
+    // against slot 1, whose travelled is a NaN pattern no arithmetic produces -- no match)
     H.a[1][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, __uint_as_float(0xFFFFFFFFu));
     H.a[1][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+    uint32_t h2 = ~state_hash(st), h1 = 0;
     for (uint32_t p = 0;; p ^= 1u) {
         H.a[p][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.travelled);
         H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+        h1 = state_hash(st);
         const uint32_t fate = march_step(a, f, st);
         if (fate != 0xFFu) { steps = st.n_rk; return fate; }
-        const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
-        const Hist h2{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w) != 0u};
-        if (same_state(st, h2)) {
-            steps = st.n_rk;
-            if ((a.max_iters - st.n_rk) & 1u) {
-                const float4 r0 = H.a[p][0][lane], r1 = H.a[p][1][lane];
-                st.ro = mk(r0.x, r0.y, r0.z); st.rd = mk(r1.x, r1.y, r1.z); st.travelled = r0.w;
+        if (state_hash(st) == h2) {
+            const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
+            const Hist hs{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w) != 0u};
+            if (same_state(st, hs)) {
+                steps = st.n_rk;
+                if ((a.max_iters - st.n_rk) & 1u) {
+                    const float4 r0 = H.a[p][0][lane], r1 = H.a[p][1][lane];
+                    st.ro = mk(r0.x, r0.y, r0.z); st.rd = mk(r1.x, r1.y, r1.z); st.travelled = r0.w;
+                }
+                st.n_rk = a.max_iters;
+                return BH_FATE_CAP;
             }
-            st.n_rk = a.max_iters;
-            return BH_FATE_CAP;
         }
+        h2 = h1;
     }
 }
 
