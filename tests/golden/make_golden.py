@@ -9,7 +9,10 @@ regressions and against each other; they are not reference outputs.
 Each fixture holds its inputs (112-byte camera uniform, 32-byte uniforms, a small RGBA8 sky, frame
 size, RK cap, scene flags) and expected outputs (col RGBA f32, n_rk u16, fate u8).
 
-    python tests/golden/make_golden.py
+bloom_*.npz: the post-processing chain (oracle/bh_bloom_oracle.c, cross-checked against
+oracle/bloom_np.py): inputs col / blackout BGRA8 + levels, expected surface BGRA8.
+
+    python tests/golden/make_golden.py [--only march|bloom]
 """
 from __future__ import annotations
 
@@ -55,10 +58,38 @@ def make(name, spec, sky):
     print(name, np.bincount(fate.ravel(), minlength=4), float(n_rk.mean()))
 
 
+def _bgra(c):
+    e = oracle.srgb_encode(c[..., :3])
+    return np.stack([e[..., 2], e[..., 1], e[..., 0], np.full(e.shape[:2], 255, np.uint8)], -1)
+
+
+def make_bloom(sky):
+    from oracle import bloom_np
+    cu, U = camera_uniform("A", 64, 32), uniforms()
+    col, bo, _, _ = oracle.render_rows(cu.to_bytes(), bytes(U.to_c()), sky, 64, 32, 512, 3)
+    rng = np.random.default_rng(0xB100)
+    rnd = rng.integers(0, 256, size=(30, 50, 4), dtype=np.uint8)
+    rnd[..., 3] = 255
+    sparse = rnd.copy()
+    sparse[..., :3] = np.where(rng.random((30, 50, 1)) < 0.05, sparse[..., :3], 0)
+    cases = {"bloom_camA_64x32_l3": (_bgra(col), _bgra(bo), 3),
+             "bloom_random_50x30_l2": (rnd, sparse, 2),
+             "bloom_random_32x30_l1": (rnd[:, :32].copy(), sparse[:, :32].copy(), 1)}
+    for name, (c, b, lv) in cases.items():
+        out = oracle.bloom(c, b, lv)
+        assert np.array_equal(out, bloom_np.bloom(c, b, lv)), name
+        np.savez_compressed(HERE / f"{name}.npz", col=c, blackout=b, levels=np.array([lv], np.uint32), out=out)
+        print(name, out.shape, float(out[..., :3].mean()))
+
+
 def main():
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     sky = bh.synthetic_sky(SKY_W, SKY_H, SKY_SEED)
-    for name, spec in FIXTURES.items():
-        make(name, spec, sky)
+    if only in (None, "march"):
+        for name, spec in FIXTURES.items():
+            make(name, spec, sky)
+    if only in (None, "bloom"):
+        make_bloom(sky)
 
 
 if __name__ == "__main__":

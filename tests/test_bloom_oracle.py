@@ -54,3 +54,12 @@ def test_bloom_spreads_a_point_and_keeps_col():
     lit = out[..., :3].max(-1) > 0
     ys, xs = np.nonzero(lit)
     assert lit.sum() > 9 and ys.min() < 16 < ys.max() and xs.min() < 32 < xs.max()
+
+
+BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
+
+
+@pytest.mark.parametrize("path", BLOOM_GOLDEN, ids=[p.stem for p in BLOOM_GOLDEN])
+def test_bloom_oracle_reproduces_golden(path):
+    z = np.load(path)
+    assert np.array_equal(oracle.bloom(z["col"], z["blackout"], int(z["levels"][0])), z["out"])

@@ -81,3 +81,16 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
     with pytest.raises(bh.BhError):
         scene.bloom(t, t, t, schedule=7)
     scene.close()
+
+
+BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
+
+
+@pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
+@pytest.mark.parametrize("path", BLOOM_GOLDEN, ids=[p.stem for p in BLOOM_GOLDEN])
+def test_bloom_matches_golden(torch_cuda, sky_small, path, schedule):
+    z = np.load(path)
+    scene = bh.Scene(16, 16, sky=sky_small)
+    got = _gpu_bloom(torch_cuda, scene, z["col"], z["blackout"], int(z["levels"][0]), schedule)
+    assert np.array_equal(got, z["out"])
+    scene.close()
