@@ -630,7 +630,7 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     }
 }
 
-// ---- schedule 0: persistent waves with per-lane refill (default) --------------------------------
+// ---- schedule BH_SCHED_PERSISTENT: persistent waves with per-lane refill (A/B option) ------------
 //
 // Each wave keeps all 64 lanes marching.  Rays are prepared (pixel_ray + s, :362-363, :262-263) in
 // full-width batches of one 8x8 tile into an LDS "ready" queue, and a lane whose ray terminates pops
@@ -759,12 +759,13 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
     }
 }
 
-// ---- schedule 2: two rays per lane (default) ----------------------------------------------------
+// ---- schedule BH_SCHED_PAIR: two rays per lane (A/B option) --------------------------------------
 // One wave64 = two consecutive shard-local 8x8 tiles; each lane marches the pixel at the same (x&7,
 // y&7) position in both (8 px apart for an unsharded frame: coherent step counts) and the loop body
 // interleaves the two rays' iterations: on gfx950 one dependent chain per wave issues only every
 // ~4-5 cycles however many waves share the SIMD, two chains reach the ~2.3-cycle peak
-// (tools/ubench/latency.hip).
+// (tools/ubench/latency.hip).  Measured slower than the tile schedule (113 VGPRs: 4 waves per
+// SIMD instead of 8).
 template <uint32_t FMT>
 __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
     __shared__ float lut[lds_tables<FMT>()];
