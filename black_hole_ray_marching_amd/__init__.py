@@ -9,7 +9,8 @@ from ._abi import (BH_BLOOM_AUTO, BH_BLOOM_LITERAL, BH_FATE_BLACKOUT, BH_FATE_CA
                    BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BH_SCHED_FLAG_STATIC_ORDER, BH_SCHED_PAIR, BH_SCHED_PERSISTENT, BH_SCHED_TILE,
                    BYTES_PER_PIXEL,
                    BhError, load)
-from .scene import (MAX_ITERATIONS, Camera, CameraController, CameraUniform, Scene, Uniforms, shard_tile_count, srgb_encode_table,
+from .scene import (MAX_ITERATIONS, Camera, CameraController, CameraUniform, Scene, Uniforms, load_sky, shard_tile_count,
+                    srgb_encode_table,
                     synthetic_sky, tiles_unpack)
 
 __version__ = "0.1.0"

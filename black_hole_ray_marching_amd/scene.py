@@ -161,6 +161,17 @@ def synthetic_sky(width: int = 4096, height: int = 2048, seed: int = 0x5EED_B1AC
     return out
 
 
+def load_sky(path) -> np.ndarray:
+    """Texture::from_bytes / from_image (src/texture.rs:11-27, src/scene.rs:186-194): decode an image
+    file (the reference ships src/space_4096x2048.jpg) to (H, W, 4) RGBA8 with alpha 255, the bytes
+    bh_create uploads as the Rgba8UnormSrgb sky.  Decoded with Pillow (libjpeg-turbo); the reference
+    uses the jpeg-decoder crate 0.3.1, and JPEG decoders legitimately differ by +-1 LSB, so the
+    texels -- an input to both renderers -- are not part of kernel parity."""
+    from PIL import Image
+    with Image.open(path) as im:
+        return np.ascontiguousarray(np.asarray(im.convert("RGBA"), dtype=np.uint8))
+
+
 def srgb_encode_table() -> np.ndarray:
     """The 257 thresholds of the BGRA8 sRGB encoder (bh_srgb.hpp): code(x) = max k with x >= T[k]."""
     out = np.empty(257, np.float32)
@@ -288,6 +299,6 @@ def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_s
 
 
 __all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
-           "srgb_encode_table", "BH_OUT_BGRA8_SRGB",
+           "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -164,3 +164,16 @@ def test_create_without_device_fails_loudly():
     with pytest.raises(bh.BhError) as ei:
         bh.Scene(16, 16, sky=bh.synthetic_sky(64, 32))
     assert ei.value.status == bh._abi.BH_ERR_NO_DEVICE
+
+
+def test_load_sky_decodes_to_rgba8(tmp_path):
+    """load_sky (Texture::from_image, src/texture.rs:11-27): any image file -> (H, W, 4) RGBA8, alpha 255."""
+    PIL = pytest.importorskip("PIL.Image")
+    sky = bh.synthetic_sky(128, 64)
+    PIL.fromarray(sky[..., :3]).save(tmp_path / "sky.png")
+    got = bh.load_sky(tmp_path / "sky.png")
+    assert got.shape == (64, 128, 4) and np.array_equal(got, sky)
+    PIL.fromarray(sky[..., :3]).save(tmp_path / "sky.jpg", quality=95)
+    j = bh.load_sky(tmp_path / "sky.jpg")
+    assert j.shape == (64, 128, 4) and (j[..., 3] == 255).all()
+    assert np.abs(j[..., :3].astype(int) - sky[..., :3]).mean() < 6  # lossy, but the same picture

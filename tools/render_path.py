@@ -29,6 +29,8 @@ p.add_argument("--max-iters", type=int, default=512)
 p.add_argument("--script", default="W:0-12,ArrowLeft:6-24,P:12-18")
 p.add_argument("--out", default="gpurun_out/path")
 p.add_argument("--no-png", action="store_true")
+p.add_argument("--sky", default=None, help="image file for the sky (e.g. the reference's space_4096x2048.jpg); "
+                                            "default: the synthetic sky")
 args = p.parse_args()
 W, H = args.width, args.height
 keys = []
@@ -38,7 +40,8 @@ for item in filter(None, args.script.split(",")):
     keys.append((k, a, b))
 out_dir = Path(args.out)
 out_dir.mkdir(parents=True, exist_ok=True)
-scene = bh.Scene(W, H, sky=bh.synthetic_sky(), max_iters=args.max_iters, math=bh.BH_MATH_EXACT)
+sky = bh.load_sky(args.sky) if args.sky else bh.synthetic_sky()
+scene = bh.Scene(W, H, sky=sky, max_iters=args.max_iters, math=bh.BH_MATH_EXACT)
 ctrl = bh.CameraController()
 cam = bh.Camera.default(W, H)
 col = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
