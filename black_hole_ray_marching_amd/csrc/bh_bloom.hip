@@ -161,8 +161,11 @@ struct Taps {
 template <class Src>
 __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float v, uint32_t point) {
     F4 s = (point & 1u) ? sample_point(src, u + k.du(0), v + k.dv(0)) : sample(src, u + k.du(0), v + k.dv(0));
-#pragma unroll 1
+#pragma unroll
     for (int i = 1; i < 8; i++) {
+        // the sched barrier keeps one tap in flight at a time: all 8 unrolled taps hoisted together
+        // take 160 VGPRs (3 waves per SIMD); the rolled loop recomputes the offsets every tap
+        __builtin_amdgcn_sched_barrier(0);
         const float tu = u + k.du(i), tv = v + k.dv(i);
         const F4 q = ((point >> i) & 1u) ? sample_point(src, tu, tv) : sample(src, tu, tv);
         const float w = (i & 1) ? 2.0f : 1.0f;  // x * 1.0 == x exactly: one form for both weights
@@ -198,10 +201,26 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
     const Span sx = tap_span(bx, min(bx + 15u, ow - 1u), Rw, k.du_min(), k.du_max(), t.w);
     const Span sy = tap_span(by, min(by + 15u, oh - 1u), Rh, k.dv_min(), k.dv_max(), t.h);
     if (sx.n <= FP && sy.n <= FP) {  // block-uniform
-        for (int32_t i = (int32_t)threadIdx.x; i < sx.n * sy.n; i += 256) {
-            const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-            const F4 d = dec(L, t.px[(size_t)(sy.lo + ly) * t.w + (sx.lo + lx)]);
-            tile[ly * FP + lx] = make_float4(d.r, d.g, d.b, d.a);
+        // all of this thread's texel loads first, then the decodes (the loads' L2 latency overlaps)
+        constexpr int R = (FP * FP + 255) / 256;
+        uint32_t raw[R];
+        const int32_t n = sx.n * sy.n;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                raw[r] = t.px[(size_t)(sy.lo + ly) * t.w + (sx.lo + lx)];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FP + lx] = make_float4(d.r, d.g, d.b, d.a);
+            }
         }
         __syncthreads();
         body(TileSrc<FP>{t, tile, sx.lo, sy.lo});
