@@ -219,7 +219,7 @@ def test_invalid_arguments_fail_loudly(torch_cuda, scene_small):
     scene_small.camera_uniform = old
 
 
-GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("*.npz"))
+GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("cam*.npz"))
 
 
 @pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])

@@ -11,7 +11,7 @@ import oracle
 from oracle import oracle_np
 from tests._cases import camera_uniform, uniforms
 
-GOLDEN = sorted((Path(__file__).parent / "golden").glob("*.npz"))
+GOLDEN = sorted((Path(__file__).parent / "golden").glob("cam*.npz"))
 
 
 def load_fixture(p):
