@@ -25,6 +25,7 @@ struct MarchArgs {
     uint32_t order_centre;     //   many tiles (~ one tile row), starting at block order_centre
     const uint32_t* order;     // optional dispatch order (slot -> shard-local tile), else centre-out
     uint8_t* tile_cost;        // optional output: per shard-local tile, min(255, max n_rk / 2)
+    uint32_t* order_tot;       // with tile_cost: per-bucket tile counts of those costs (buckets < B-1)
     // per-frame invariants, computed on the host with the same correctly rounded f32 ops as the
     // oracle: photon-sphere centre -normalize(ro0) * 1.5 * RS (:294) and (DP * RS) * -1.5 (:126)
     float cps[3];

@@ -27,7 +27,7 @@ struct bh_ctx {
     // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order
     uint8_t* tile_cost = nullptr;
     uint32_t* order = nullptr;
-    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS + 1 words, zero between frames
+    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS + 1 words (bh_tiles.hip order_scatter_kernel)
     uint64_t order_cap = 0;              // tiles the two buffers hold
     uint64_t order_key = ~0ull;          // (width, height, shard) the costs belong to
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
@@ -664,11 +664,11 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
                     (he = hipMalloc(&c->order, nt * sizeof(uint32_t))) == hipSuccess)
                     c->order_cap = nt;
             }
-            if (he == hipSuccess && !c->order_counters) {
+            if (he == hipSuccess && !c->order_counters)
                 he = hipMalloc(&c->order_counters, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t));
-                if (he == hipSuccess)
-                    he = hipMemsetAsync(c->order_counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
-            }
+            // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent
+            if (he == hipSuccess)
+                he = hipMemsetAsync(c->order_counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
             if (he == hipSuccess) he = hipMemsetAsync(c->tile_cost, 0, nt, s);
             if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order buffers"); }
             c->order_key = key;
@@ -678,11 +678,17 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
         if (oe != 0) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail((hipError_t)oe, "order kernels"); }
         a.order = c->order;
         a.tile_cost = c->tile_cost;
+        a.order_tot = c->order_counters;
     }
     int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
                                      : bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s);
     if (prev != c->device) (void)hipSetDevice(prev);
-    if (e != 0) return hip_fail((hipError_t)e, "march kernel launch");
+    if (e != 0) {
+        // the costs and their histogram are written together by the march kernel; without it they
+        // may disagree, so the next frame starts the temporal order afresh
+        c->order_key = ~0ull;
+        return hip_fail((hipError_t)e, "march kernel launch");
+    }
     return BH_OK;
 }
 

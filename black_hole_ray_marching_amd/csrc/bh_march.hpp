@@ -625,8 +625,15 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
     if (a.tile_cost) {
-        const uint32_t m = wave_max_u32(steps);
-        if (lane == 0u) a.tile_cost[t] = (uint8_t)min(m >> 1, 255u);
+        // the next frame's cost and its bucket histogram (a no-return atomic: the wave does not wait);
+        // the last bucket is the remainder and is not counted
+        const uint32_t m = min(wave_max_u32(steps) >> 1, 255u);
+        if (lane == 0u) {
+            a.tile_cost[t] = (uint8_t)m;
+            const uint32_t b = cost_bucket(m);
+            if (b < ORDER_BUCKETS - 1u)
+                __hip_atomic_fetch_add(&a.order_tot[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 

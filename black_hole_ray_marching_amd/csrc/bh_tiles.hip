@@ -24,25 +24,17 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const T* __restrict__
     out[(size_t)py * width + px] = packed[g * 64u + lane];
 }
 
-// Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), stable
-// enough: slots are visited in centre-out order and each block reserves its bucket ranges with one
-// atomic per bucket, so ties keep (roughly) the centre-out order.  counters: [0..B) counts,
-// [B..2B) cursors, [2B] the scatter's block ticket; all zero between frames (zeroed once at
-// allocation, then by the last scatter block of every frame).
-__global__ void __launch_bounds__(256) order_count_kernel(const uint8_t* __restrict__ cost, uint32_t n,
-                                                        uint32_t L, uint32_t c, uint32_t* counters) {
-    __shared__ uint32_t hist[ORDER_BUCKETS];
-    if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&hist[cost_bucket(cost[centre_out(i, n, L, c)])], 1u);
-    __syncthreads();
-    if (threadIdx.x < ORDER_BUCKETS && hist[threadIdx.x]) atomicAdd(&counters[threadIdx.x], hist[threadIdx.x]);
-}
+// Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), one
+// kernel: the bucket histogram was accumulated by the march kernel that wrote the costs
+// (MarchArgs::order_tot), so each block only reserves its bucket ranges (one returning atomic per
+// bucket, issued in parallel) and scatters.  Slots are visited in centre-out order, so ties keep
+// (roughly) the centre-out order.  counters: [0..B-1) the histogram (the last bucket is the
+// remainder), [B..2B) cursors, [2B] the block ticket; the last block to finish zeroes them all, so
+// they are zero again before the next march kernel accumulates (graph replay needs no memset node).
 __global__ void __launch_bounds__(256) order_scatter_kernel(const uint8_t* __restrict__ cost, uint32_t n,
                                                           uint32_t L, uint32_t c, uint32_t* counters,
                                                           uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[ORDER_BUCKETS], base[ORDER_BUCKETS];
+    __shared__ uint32_t hist[ORDER_BUCKETS], base[ORDER_BUCKETS], ticket;
     if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -55,20 +47,20 @@ __global__ void __launch_bounds__(256) order_scatter_kernel(const uint8_t* __res
     __syncthreads();
     if (threadIdx.x < ORDER_BUCKETS && hist[threadIdx.x]) {
         uint32_t off = 0;
-        for (uint32_t j = 0; j < threadIdx.x; ++j) off += counters[j];
+#pragma unroll
+        for (uint32_t j = 0; j < ORDER_BUCKETS - 1u; ++j) off += j < threadIdx.x ? counters[j] : 0u;
         base[threadIdx.x] = off + atomicAdd(&counters[ORDER_BUCKETS + threadIdx.x], hist[threadIdx.x]);
     }
     __syncthreads();
     if (i < n) order[base[b] + k] = t;
-    // the last block to finish resets the counters for the next frame (self-resetting: graph
-    // capture replays this kernel without a memset node).  counters[2B] is the block ticket.
     if (threadIdx.x == 0) {
         __threadfence();
-        const uint32_t ticket = atomicAdd(&counters[2 * ORDER_BUCKETS], 1u);
-        if (ticket == gridDim.x - 1u) {
-            __threadfence();
-            for (uint32_t j = 0; j <= 2 * ORDER_BUCKETS; ++j) atomicExch(&counters[j], 0u);
-        }
+        ticket = atomicAdd(&counters[2 * ORDER_BUCKETS], 1u);
+    }
+    __syncthreads();
+    if (ticket == gridDim.x - 1u && threadIdx.x <= 2u * ORDER_BUCKETS) {
+        __threadfence();
+        atomicExch(&counters[threadIdx.x], 0u);
     }
 }
 
@@ -80,7 +72,6 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
                                                                          hipStream_t s) {
     if (n == 0) return 0;
     const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(bh::order_count_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters);
     hipLaunchKernelGGL(bh::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters, order);
     return (int)hipGetLastError();
 }
