@@ -10,8 +10,8 @@ blackout targets as north_star asks.
 
 N=1: one GPU renders the whole frame.  N>1 (torch.distributed, one process per GPU, RCCL): weak
 scaling, the frame grows with N (~8.4 Mpix per GPU, aspect 2:1: 8192x4096 at N=4), each rank renders
-its (tx + 3*ty) % N share of 8x8 tiles, the tile-packed `col` shares are gathered to rank 0 in one
-collective and unpacked there; each timed step includes render, gather and unpack.
+its (tx + 3*ty) % N share of 8x8 tiles, the tile-packed `col` shares (RGB planes: alpha is always 1
+and not shipped) are gathered to rank 0 in one collective and unpacked there; each timed step includes render, gather and unpack.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
@@ -114,17 +114,19 @@ def main() -> None:
         pipe = None
     else:
         # weak scaling: each rank renders its (tx + 3ty) % n tiles into a packed buffer; frame i's
-        # gather to rank 0 (col only: rank 0 can recompute blackout_col) overlaps frame i+1's render
+        # gather to rank 0 (col only: rank 0 can recompute blackout_col) overlaps frame i+1's render.
+        # The shards are BH_LAYOUT_TILES_RGB (alpha, always 1, is not shipped: 3/4 of the bytes into
+        # rank 0's xGMI links); rank 0's unpack restores it.
         stride = multigpu.packed_stride(W, H, n)
         my_px = bh.shard_tile_count(W, H, rank, n) * 64
-        bo = torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev)
+        bo = torch.empty((stride, 3, 64), dtype=ch_dtype, device=dev)
         frame = torch.empty((H, W, 4), dtype=ch_dtype, device=dev) if rank == 0 else None
-        shard = dict(layout=bh.BH_LAYOUT_TILES, shard_index=rank, shard_count=n)
+        shard = dict(layout=bh.BH_LAYOUT_TILES_RGB, shard_index=rank, shard_count=n)
 
         def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
-            bh.tiles_unpack(gathered, frame, W, H, n, stride, bpp, stream=torch.cuda.current_stream(dev))
+            bh.tiles_unpack_rgb(gathered, frame, W, H, n, stride, fmt, stream=torch.cuda.current_stream(dev))
 
-        pipe = multigpu.GatherPipeline(lambda: torch.empty((stride * 64, 4), dtype=ch_dtype, device=dev),
+        pipe = multigpu.GatherPipeline(lambda: torch.empty((stride, 3, 64), dtype=ch_dtype, device=dev),
                                        rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
         col = pipe.buffer(0)
 
@@ -196,8 +198,9 @@ def main() -> None:
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
     # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
-    nrk_buf = torch.zeros(col.shape[:-1], dtype=torch.int16, device=dev)
-    steps_buf = torch.zeros(col.shape[:-1], dtype=torch.int16, device=dev)
+    px_shape = (H, W) if n == 1 else (stride * 64,)  # the layout's pixel index space
+    nrk_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
+    steps_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
     render(dbg_n_rk=nrk_buf, dbg_steps=steps_buf)
     torch.cuda.synchronize(dev)
     sum_nrk = int(nrk_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
@@ -207,7 +210,7 @@ def main() -> None:
         pmc = _pmc_entry(W, H, cap, args)
         value = W * H * args.steps / elapsed / 1e6
         achieved_tf = sum_steps * F_STEP[flags] / kern_avg_s / 1e12
-        alg_bytes = my_px * bpp * 2 + sky.nbytes
+        alg_bytes = my_px * (bpp if n == 1 else bpp * 3 // 4) * 2 + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
         result = {
             "metric": METRIC,
@@ -226,7 +229,7 @@ def main() -> None:
                 "workload": f"{W}x{H} frame, cap {cap} RK steps, "
                             f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}, "
                             f"{args.fmt} col+blackout, {args.math} math"
-                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n}, RCCL gather of col to rank 0 "
+                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n}, RCCL gather of col (RGB planes) to rank 0 "
                                                   "overlapped with the next frame, unpack on rank 0"),
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
                 "schedule": args.schedule, "format": args.fmt,

@@ -19,7 +19,7 @@ BH_BLOOM_AUTO, BH_BLOOM_LITERAL = 0, 1
 BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
-BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES = 0, 1
+BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB = 0, 1, 2
 BH_SCHED_TILE, BH_SCHED_PAIR, BH_SCHED_PERSISTENT = 0, 1, 2
 BH_SCHED_FLAG_STATIC_ORDER = 0x100
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
@@ -82,6 +82,8 @@ SIGNATURES = {
     "bh_shard_tile_count": (C.c_int64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
+    "bh_tiles_unpack_rgb": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_uint64, C.c_uint32, C.c_void_p]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
     "bh_controller_update": (C.c_int, [C.POINTER(bh_controller), C.POINTER(bh_camera), C.c_float, C.c_int,
                                        C.POINTER(C.c_int)]),

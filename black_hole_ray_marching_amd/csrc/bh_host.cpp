@@ -603,7 +603,7 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (!c || !cam || !U || !d || !d->out_col) return BH_ERR_INVALID_ARG;
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
-    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES) return BH_ERR_INVALID_ARG;
+    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGB) return BH_ERR_INVALID_ARG;
     if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER))) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
@@ -701,6 +701,19 @@ int bh_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t heig
             return BH_ERR_INVALID_ARG;
     int e = bh_launch_tiles_unpack(packed, out, width, height, shard_count, shard_stride_tiles, bpp,
                                    reinterpret_cast<hipStream_t>(stream));
+    if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
+    return BH_OK;
+}
+
+int bh_tiles_unpack_rgb(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
+                        uint64_t shard_stride_tiles, uint32_t format, void* stream) {
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
+    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < shard_count; ++k)
+        if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
+            return BH_ERR_INVALID_ARG;
+    int e = bh_launch_tiles_unpack_rgb(packed, out, width, height, shard_count, shard_stride_tiles, format,
+                                       reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
     return BH_OK;
 }

@@ -489,14 +489,36 @@ __device__ __forceinline__ void load_tables(const MarchArgs& a, float* tab) {
     }
 }
 
+// BH_LAYOUT_TILES_RGB store: pixel idx = tile * 64 + lane goes to three channel planes of its tile
+// (alpha, always 1, is dropped; the unpack restores it).  Each plane store of a wave is one
+// contiguous 64-element run.
+template <uint32_t FMT>
+__device__ __forceinline__ void store_px_planar(void* base, size_t idx, v3 c, const float* enc) {
+    const size_t o = (idx >> 6) * 192u + (idx & 63u);
+    if constexpr (FMT == BH_OUT_RGBA32F) {
+        float* p = reinterpret_cast<float*>(base) + o;
+        p[0] = c.x; p[64] = c.y; p[128] = c.z;
+    } else if constexpr (FMT == BH_OUT_RGBA16F) {
+        __half* p = reinterpret_cast<__half*>(base) + o;
+        p[0] = __float2half_rn(c.x); p[64] = __float2half_rn(c.y); p[128] = __float2half_rn(c.z);
+    } else {
+        const uint32_t w = srgb_bgra8(c.x, c.y, c.z, enc);
+        uint8_t* p = reinterpret_cast<uint8_t*>(base) + o;
+        p[0] = (uint8_t)w; p[64] = (uint8_t)(w >> 8); p[128] = (uint8_t)(w >> 16);
+    }
+}
+
 // fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
 template <uint32_t FMT>
 __device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab, size_t idx, v3 col, uint32_t n_rk,
                                             uint32_t fate, uint32_t steps) {
-    store_px<FMT>(a.out_col, idx, col, tab + 256);
-    if (a.out_blackout) {
-        const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
-        store_px<FMT>(a.out_blackout, idx, bo, tab + 256);
+    const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
+    if (a.layout == BH_LAYOUT_TILES_RGB) {
+        store_px_planar<FMT>(a.out_col, idx, col, tab + 256);
+        if (a.out_blackout) store_px_planar<FMT>(a.out_blackout, idx, bo, tab + 256);
+    } else {
+        store_px<FMT>(a.out_col, idx, col, tab + 256);
+        if (a.out_blackout) store_px<FMT>(a.out_blackout, idx, bo, tab + 256);
     }
     if (a.dbg_n_rk) a.dbg_n_rk[idx] = (uint16_t)n_rk;
     if (a.dbg_fate) a.dbg_fate[idx] = (uint8_t)fate;
@@ -509,7 +531,7 @@ __device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab
 }
 
 __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
-    return (a.layout == BH_LAYOUT_TILES) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
+    return (a.layout != BH_LAYOUT_ROWMAJOR) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
 }
 
 // Iterations after which a still-marching wave raises its issue priority (the frame's tail: measured

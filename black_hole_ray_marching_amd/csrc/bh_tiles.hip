@@ -4,6 +4,23 @@
 
 namespace bh {
 
+// Packed tile g (shard-major, each shard padded to stride_tiles) -> its pixel for this lane; false
+// for padding tiles and pixels outside the frame.
+__device__ __forceinline__ bool unpack_pixel(uint64_t g, uint32_t width, uint32_t height, uint32_t tiles_x,
+                                             uint32_t shard_count, uint64_t stride_tiles, uint32_t* px,
+                                             uint32_t* py) {
+    const uint32_t shard = (uint32_t)(g / stride_tiles);
+    const uint32_t t = (uint32_t)(g - (uint64_t)shard * stride_tiles);
+    const uint32_t tiles_y = (height + 7u) / 8u;
+    if (t >= shard_tile_count(tiles_x, tiles_y, shard, shard_count)) return false;  // padding tiles
+    uint32_t tx, ty;
+    shard_tile_coords(t, tiles_x, shard, shard_count, &tx, &ty);
+    const uint32_t lane = threadIdx.x & 63u;
+    *px = tx * 8u + (lane & 7u);
+    *py = ty * 8u + (lane >> 3);
+    return *px < width && *py < height;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) tiles_unpack_kernel(const T* __restrict__ packed, T* __restrict__ out,
                                                            uint32_t width, uint32_t height, uint32_t tiles_x,
@@ -11,17 +28,31 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const T* __restrict__
                                                            uint64_t total_tiles) {
     // one wave = one packed tile; consecutive waves walk shard 0's tiles, then shard 1's, ...
     const uint64_t g = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (g >= total_tiles) return;
-    const uint32_t shard = (uint32_t)(g / stride_tiles);
-    const uint32_t t = (uint32_t)(g - (uint64_t)shard * stride_tiles);
-    const uint32_t tiles_y = (height + 7u) / 8u;
-    if (t >= shard_tile_count(tiles_x, tiles_y, shard, shard_count)) return;  // padding tiles
-    uint32_t tx, ty;
-    shard_tile_coords(t, tiles_x, shard, shard_count, &tx, &ty);
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
-    if (px >= width || py >= height) return;
-    out[(size_t)py * width + px] = packed[g * 64u + lane];
+    uint32_t px, py;
+    if (g >= total_tiles || !unpack_pixel(g, width, height, tiles_x, shard_count, stride_tiles, &px, &py)) return;
+    out[(size_t)py * width + px] = packed[g * 64u + (threadIdx.x & 63u)];
+}
+
+// BH_LAYOUT_TILES_RGB: three 64-element channel planes per tile -> RGBA/BGRA texels, alpha restored.
+template <uint32_t FMT>
+__global__ void __launch_bounds__(256) tiles_unpack_rgb_kernel(const void* __restrict__ packed, void* __restrict__ out,
+                                                               uint32_t width, uint32_t height, uint32_t tiles_x,
+                                                               uint32_t shard_count, uint64_t stride_tiles,
+                                                               uint64_t total_tiles) {
+    const uint64_t g = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint32_t px, py;
+    if (g >= total_tiles || !unpack_pixel(g, width, height, tiles_x, shard_count, stride_tiles, &px, &py)) return;
+    const size_t o = g * 192u + (threadIdx.x & 63u), q = (size_t)py * width + px;
+    if constexpr (FMT == BH_OUT_RGBA32F) {
+        const float* p = reinterpret_cast<const float*>(packed) + o;
+        reinterpret_cast<float4*>(out)[q] = make_float4(p[0], p[64], p[128], 1.0f);
+    } else if constexpr (FMT == BH_OUT_RGBA16F) {
+        const uint16_t* p = reinterpret_cast<const uint16_t*>(packed) + o;
+        reinterpret_cast<uint2*>(out)[q] = make_uint2(p[0] | ((uint32_t)p[64] << 16), p[128] | (0x3C00u << 16));
+    } else {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(packed) + o;
+        reinterpret_cast<uint32_t*>(out)[q] = p[0] | ((uint32_t)p[64] << 8) | ((uint32_t)p[128] << 16) | 0xFF000000u;
+    }
 }
 
 // Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), one
@@ -89,6 +120,25 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(cons
         case 16: hipLaunchKernelGGL(bh::tiles_unpack_kernel<uint4>, grid, block, 0, s, (const uint4*)packed, (uint4*)out, width, height, tiles_x, shard_count, stride_tiles, total); break;
         case 8: hipLaunchKernelGGL(bh::tiles_unpack_kernel<uint2>, grid, block, 0, s, (const uint2*)packed, (uint2*)out, width, height, tiles_x, shard_count, stride_tiles, total); break;
         case 4: hipLaunchKernelGGL(bh::tiles_unpack_kernel<uint32_t>, grid, block, 0, s, (const uint32_t*)packed, (uint32_t*)out, width, height, tiles_x, shard_count, stride_tiles, total); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,
+                                                                              uint32_t height, uint32_t shard_count,
+                                                                              uint64_t stride_tiles, uint32_t format,
+                                                                              hipStream_t s) {
+    const uint32_t tiles_x = (width + 7u) / 8u;
+    const uint64_t total = stride_tiles * shard_count;
+    const uint64_t blocks = (total + 3u) / 4u;
+    if (blocks == 0) return 0;
+    if (blocks > 0x7fffffffull) return (int)hipErrorInvalidValue;
+    dim3 grid((uint32_t)blocks), block(256);
+    switch (format) {
+        case BH_OUT_RGBA32F: hipLaunchKernelGGL(bh::tiles_unpack_rgb_kernel<BH_OUT_RGBA32F>, grid, block, 0, s, packed, out, width, height, tiles_x, shard_count, stride_tiles, total); break;
+        case BH_OUT_RGBA16F: hipLaunchKernelGGL(bh::tiles_unpack_rgb_kernel<BH_OUT_RGBA16F>, grid, block, 0, s, packed, out, width, height, tiles_x, shard_count, stride_tiles, total); break;
+        case BH_OUT_BGRA8_SRGB: hipLaunchKernelGGL(bh::tiles_unpack_rgb_kernel<BH_OUT_BGRA8_SRGB>, grid, block, 0, s, packed, out, width, height, tiles_x, shard_count, stride_tiles, total); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();

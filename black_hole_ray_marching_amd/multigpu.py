@@ -3,9 +3,9 @@
 The frame is cut into 8x8 tiles; tile (tx, ty) belongs to rank (tx + 3*ty) % world (SURVEY.md
 §8e: the diagonal interleave spreads the expensive photon-sphere region over all ranks; contiguous
 bands would leave the centre band's owner with ~1.3x the average work).  Each rank renders its
-tiles with BH_LAYOUT_TILES into one contiguous buffer, the buffers are gathered to rank 0 in a
-single collective (no reduction exists in this path), and rank 0 scatters them to a row-major frame
-with the bh_tiles_unpack kernel.
+tiles with BH_LAYOUT_TILES (or BH_LAYOUT_TILES_RGB, alpha dropped) into one contiguous buffer, the
+buffers are gathered to rank 0 in a single collective (no reduction exists in this path), and rank
+0 scatters them to a row-major frame with the bh_tiles_unpack(_rgb) kernel.
 
 The reference renders one frame on one GPU (src/state.rs:255-307); this module is the multi-GPU
 extension named by north_star.  The pure-Python tile math mirrors bh_common.hpp so that host logic
@@ -59,6 +59,16 @@ def unpack_tiles_numpy(packed: np.ndarray, width: int, height: int, S: int, stri
             ok = (px < width) & (py < height)
             out[py[ok], px[ok]] = packed[(k * stride + t) * 64 + lane[ok]]
     return out
+
+
+def planar_to_packed(planar: np.ndarray, alpha) -> np.ndarray:
+    """BH_LAYOUT_TILES_RGB buffer (n_tiles, 3, 64) -> BH_LAYOUT_TILES pixels (n_tiles * 64, 4), the
+    constant `alpha` (1.0 or 255, in the format's own type) restored as the 4th channel."""
+    n = planar.shape[0]
+    px = np.empty((n, 64, 4), dtype=planar.dtype)
+    px[..., :3] = planar.transpose(0, 2, 1)
+    px[..., 3] = alpha
+    return px.reshape(n * 64, 4)
 
 
 def gather_packed(packed, rank: int, world: int, gathered=None, group=None):

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
-from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
+from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
                    BH_OUT_RGBA32F, BH_OUT_BGRA8_SRGB, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
 
 MAX_ITERATIONS = 1000  # src/black_hole_maybe.wgsl:85
@@ -194,6 +194,17 @@ def _ptr(t) -> int | None:
     return t.data_ptr()
 
 
+def _check_size(t, need: int, name: str) -> None:
+    """Host-side bounds check of a caller buffer (tensor-like objects; raw pointers are trusted)."""
+    if t is None or isinstance(t, int) or not hasattr(t, "element_size"):
+        return
+    have = t.numel() * t.element_size()
+    if have < need:
+        raise BhError(_abi.BH_ERR_INVALID_ARG, f"render: {name} holds {have} bytes, the frame needs {need}")
+    if hasattr(t, "is_contiguous") and not t.is_contiguous():
+        raise BhError(_abi.BH_ERR_INVALID_ARG, f"render: {name} must be contiguous")
+
+
 class Scene:
     """src/scene.rs `Scene`: owns the sky texture (on `device`), camera, uniforms; renders frames."""
 
@@ -261,6 +272,17 @@ class Scene:
         d.math = self.math if math is None else math
         d.layout, d.shard_index, d.shard_count = layout, shard_index, shard_count
         d.schedule = schedule
+        if layout == BH_LAYOUT_ROWMAJOR:
+            px = d.width * d.height
+        else:
+            px = shard_tile_count(d.width, d.height, shard_index, shard_count) * 64
+        bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+        col_bytes = px * bpp * 3 // 4 if layout == BH_LAYOUT_TILES_RGB else px * bpp
+        _check_size(output, col_bytes, "output")
+        _check_size(blackout_output, col_bytes, "blackout_output")
+        _check_size(dbg_n_rk, px * 2, "dbg_n_rk")
+        _check_size(dbg_fate, px, "dbg_fate")
+        _check_size(dbg_steps, px * 2, "dbg_steps")
         d.out_col, d.out_blackout = _ptr(output), _ptr(blackout_output)
         d.dbg_n_rk, d.dbg_fate, d.dbg_steps = _ptr(dbg_n_rk), _ptr(dbg_fate), _ptr(dbg_steps)
         check(self.lib.bh_render(self._ctx, C.byref(self.camera_uniform.c), C.byref(self.uniforms.to_c()),
@@ -298,7 +320,15 @@ def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_s
                                  bytes_per_pixel, _stream_handle(stream)), "bh_tiles_unpack")
 
 
+def tiles_unpack_rgb(packed, out, width: int, height: int, shard_count: int, shard_stride_tiles: int,
+                     fmt: int, stream=None) -> None:
+    """bh_tiles_unpack_rgb: gathered BH_LAYOUT_TILES_RGB shards of format `fmt` -> row-major frame."""
+    check(load().bh_tiles_unpack_rgb(_ptr(packed), _ptr(out), width, height, shard_count, shard_stride_tiles,
+                                     fmt, _stream_handle(stream)), "bh_tiles_unpack_rgb")
+
+
 __all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+           "tiles_unpack_rgb",
            "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
-           "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]
+           "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_LAYOUT_TILES_RGB", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -110,9 +110,13 @@ typedef enum {
 /* Output layout. */
 typedef enum {
     BH_LAYOUT_ROWMAJOR = 0, /* out[y * width + x]; requires shard_count == 1 */
-    BH_LAYOUT_TILES = 1     /* the shard's 8x8 tiles packed in shard order, 64 pixels per tile,
+    BH_LAYOUT_TILES = 1,    /* the shard's 8x8 tiles packed in shard order, 64 pixels per tile,
                                pixel (x & 7) + 8 * (y & 7) inside a tile; pixels outside the frame
                                are left untouched */
+    BH_LAYOUT_TILES_RGB = 2 /* BH_LAYOUT_TILES without alpha (both targets' alpha is always 1,
+                               src/black_hole_maybe.wgsl:369): each tile is three planes of 64
+                               channel values in the format's memory order less alpha (R, G, B for
+                               RGBA16F/RGBA32F; B, G, R for BGRA8), 3/4 of the bytes to gather */
 } bh_layout;
 
 /* Work schedule of the march kernel (same results, different speed). */
@@ -224,6 +228,12 @@ int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_inde
 int bh_tiles_unpack(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
                     uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t bytes_per_pixel,
                     void* hip_stream);
+
+/* As bh_tiles_unpack for BH_LAYOUT_TILES_RGB shards of `format` (bh_out_format): restores the
+ * constant alpha (1.0 / 255) of the row-major frame. */
+int bh_tiles_unpack_rgb(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
+                        uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
+                        void* hip_stream);
 
 /* The BGRA8 sRGB encoder's threshold table: out[k] (k = 1..255) = the smallest float x with
  * encode(x) >= k, out[0] = 0, out[256] = +inf; encode(x) = the largest k with x >= out[k]. */

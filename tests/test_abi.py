@@ -138,6 +138,22 @@ def test_unpack_reference_roundtrip():
     assert np.array_equal(frame[..., 0], xx) and np.array_equal(frame[..., 1], yy)
 
 
+def test_planar_tiles_restore_the_packed_pixels():
+    """BH_LAYOUT_TILES_RGB is BH_LAYOUT_TILES with each tile's pixels split into R, G, B planes and
+    alpha dropped; planar_to_packed (the numpy statement of bh_tiles_unpack_rgb's per-tile step)
+    inverts it when alpha is the constant."""
+    rng = np.random.default_rng(3)
+    n = 7
+    px = rng.integers(0, 256, (n * 64, 4), dtype=np.uint8)
+    px[:, 3] = 255
+    planes = px.reshape(n, 64, 4)[..., :3].transpose(0, 2, 1).copy()
+    assert planes.shape == (n, 3, 64) and planes.nbytes == px.nbytes * 3 // 4
+    assert np.array_equal(multigpu.planar_to_packed(planes, 255), px)
+    f = rng.standard_normal((n * 64, 4)).astype(np.float16)
+    f[:, 3] = 1.0
+    assert np.array_equal(multigpu.planar_to_packed(f.reshape(n, 64, 4)[..., :3].transpose(0, 2, 1), 1.0), f)
+
+
 def test_weak_scaling_frames():
     assert multigpu.weak_scaling_frame(1) == (4096, 2048)
     assert multigpu.weak_scaling_frame(4) == (8192, 4096)  # BASELINE config 4 frame

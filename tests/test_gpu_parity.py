@@ -171,6 +171,45 @@ def test_tiles_shards_unpack(torch_cuda, scene_small, S, schedule):
     assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
 
 
+@pytest.mark.parametrize("fmt", [bh.BH_OUT_RGBA32F, bh.BH_OUT_RGBA16F, bh.BH_OUT_BGRA8_SRGB])
+@pytest.mark.parametrize("S", [1, 3, 8])
+def test_tiles_rgb_shards_unpack(torch_cuda, scene_small, S, fmt):
+    """BH_LAYOUT_TILES_RGB (the multi-GPU transport, alpha dropped): each shard's planes equal the
+    BH_LAYOUT_TILES pixels less alpha, for col and blackout, and bh_tiles_unpack_rgb of the gathered
+    shards reproduces the row-major frame word for word (alpha restored)."""
+    from black_hole_ray_marching_amd.multigpu import planar_to_packed
+    torch = torch_cuda
+    W, H = 100, 52
+    dt = {bh.BH_OUT_RGBA32F: torch.float32, bh.BH_OUT_RGBA16F: torch.float16, bh.BH_OUT_BGRA8_SRGB: torch.uint8}[fmt]
+    alpha = 255 if fmt == bh.BH_OUT_BGRA8_SRGB else 1.0
+    scene = scene_small
+    scene.camera_uniform = camera_uniform("C", W, H)
+    scene.uniforms, scene.max_iters, scene.scene_flags = uniforms(), 512, 3
+    ref = torch.zeros((H, W, 4), dtype=dt, device="cuda")
+    scene.render(ref, None, fmt=fmt, width=W, height=H)
+    stride = max(bh.shard_tile_count(W, H, k, S) for k in range(S))
+    planes = torch.zeros((S * stride, 3, 64), dtype=dt, device="cuda")
+    for k in range(S):
+        n = bh.shard_tile_count(W, H, k, S)
+        px_c = torch.zeros((n * 64, 4), dtype=dt, device="cuda")
+        px_b = torch.zeros_like(px_c)
+        pl_b = torch.zeros((n, 3, 64), dtype=dt, device="cuda")
+        kw = dict(fmt=fmt, shard_index=k, shard_count=S, width=W, height=H)
+        scene.render(planes[k * stride:k * stride + n], pl_b, layout=bh.BH_LAYOUT_TILES_RGB, **kw)
+        scene.render(px_c, px_b, layout=bh.BH_LAYOUT_TILES, **kw)
+        torch.cuda.synchronize()
+        for pl, px in ((planes[k * stride:k * stride + n], px_c), (pl_b, px_b)):
+            # pixels outside the frame are untouched in both layouts (zeros), alpha included
+            got = planar_to_packed(pl.cpu().numpy(), alpha)
+            want = px.cpu().numpy().copy()
+            want[..., 3] = alpha
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    out = torch.zeros((H, W, 4), dtype=dt, device="cuda")
+    bh.tiles_unpack_rgb(planes, out, W, H, S, stride, fmt)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
+
+
 def test_headline_rows_bitexact_and_fast(torch_cuda):
     """4096x2048, cap 512, camera A, full sky: sampled rows through the full-size launch."""
     torch = torch_cuda
