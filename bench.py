@@ -245,6 +245,7 @@ def main() -> None:
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
                          "traffic": pmc.get("hbm_bytes_per_launch"),
                          "valu_busy": pmc.get("valu_busy_est"),
+                         "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                          "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
                                  "launch time (HIP events on the render stream); FP32 VALU-bound, no "
                                  "MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU issue "
@@ -276,6 +277,16 @@ def _pmc_entry(W, H, cap, args):
         return {}
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
     """cpu_baseline: the C oracle on the host cores over the same full frame, `cpu_reps` times
     (bounded: ~1 s wall, ~15 core-seconds on the GPU box); parity: the GPU frame (fp32 output of the
@@ -294,9 +305,20 @@ def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
         o_col, _, o_nrk, o_fate = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, threads=threads)
         times.append(time.perf_counter() - t0)
     cpu_s = float(np.median(times))
+    sum_nrk = int(o_nrk.astype(np.int64).sum())
+    # single-thread leg (1 thread and all cores): every 8th row of the same frame
+    t0 = time.perf_counter()
+    _, _, s_nrk, _ = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, 0, H, threads=1, row_step=8)
+    one_s = time.perf_counter() - t0
     cpu_baseline = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
                     "sample": f"the full {W}x{H} cap-{cap} frame, x{len(times)} (median {cpu_s:.2f} s): C oracle "
-                              f"(oracle/bh_oracle.c, gcc -O2 -ffp-contract=off), OpenMP {threads} threads"}
+                              f"(oracle/bh_oracle.c, gcc -O2 -ffp-contract=off), OpenMP {threads} threads",
+                    "n_rk_per_s": round(sum_nrk / cpu_s, 1),
+                    "single_thread": {"value": round(s_nrk.size / one_s / 1e6, 4), "unit": "Mpix/s",
+                                      "n_rk_per_s": round(int(s_nrk.astype(np.int64).sum()) / one_s, 1),
+                                      "sample": f"every 8th row of the frame ({s_nrk.size} px, {one_s:.2f} s), 1 thread"},
+                    "host": {"cpu": _cpu_model(), "nproc": os.cpu_count(),
+                             "affinity": len(os.sched_getaffinity(0))}}
     c32 = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     nrk = torch.empty((H, W), dtype=torch.int16, device=dev)
     fate = torch.empty((H, W), dtype=torch.uint8, device=dev)

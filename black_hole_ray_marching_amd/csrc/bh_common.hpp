@@ -66,21 +66,56 @@ __host__ __device__ inline uint64_t shard_tile_count(uint32_t tiles_x, uint32_t 
     return n;
 }
 
-// Shard-local tile index t -> global tile coordinates.  Walks at most one row period (P <= S rows).
+// The rows of one period of shard k, walked without divisions (these run once per wave in the
+// march kernel and once per tile in the unpack; the division-per-row form cost ~1000 VALU
+// instructions per tile at S = 8).  Row r of a period starts at column st = (k - 3r) mod S and
+// owns q0 + (st < r0) tiles, with tiles_x = q0*S + r0.
+struct ShardRows {
+    uint32_t k, S, q0, r0, m;  // m = 3r mod S of the current row
+    __host__ __device__ ShardRows(uint32_t tiles_x, uint32_t k_, uint32_t S_) : k(k_), S(S_), m(0u) {
+        q0 = tiles_x / S; r0 = tiles_x - q0 * S;
+    }
+    __host__ __device__ uint32_t start() const { return k >= m ? k - m : k + S - m; }
+    __host__ __device__ uint32_t count() const { return q0 + (start() < r0 ? 1u : 0u); }
+    __host__ __device__ void next() { m += 3u; while (m >= S) m -= S; }
+};
+
+// Shard-local tile index t -> global tile coordinates.
 __host__ __device__ inline void shard_tile_coords(uint32_t t, uint32_t tiles_x, uint32_t k, uint32_t S,
                                                   uint32_t* tx, uint32_t* ty) {
     if (S == 1u) { *ty = t / tiles_x; *tx = t - *ty * tiles_x; return; }
     const uint32_t P = shard_period(S);
     uint32_t per = 0;
-    for (uint32_t r = 0; r < P; ++r) per += shard_row_count(tiles_x, r, k, S);
-    uint32_t period = t / per, rem = t - period * per, row = period * P;
-    for (uint32_t r = 0; r < P; ++r) {
-        uint32_t c = shard_row_count(tiles_x, r, k, S);
-        if (rem < c) { row += r; break; }
+    ShardRows R(tiles_x, k, S);
+    for (uint32_t r = 0; r < P; ++r, R.next()) per += R.count();
+    const uint32_t period = t / per;
+    uint32_t rem = t - period * per, row = 0;
+    ShardRows Q(tiles_x, k, S);
+    for (; row + 1u < P; ++row, Q.next()) {
+        const uint32_t c = Q.count();
+        if (rem < c) break;
         rem -= c;
     }
-    *ty = row;
-    *tx = shard_row_start(row, k, S) + rem * S;
+    *ty = period * P + row;
+    *tx = Q.start() + rem * S;
+}
+
+// Inverse of shard_tile_coords: global tile (tx, ty) -> its shard and its shard-local index.
+__host__ __device__ inline uint32_t shard_tile_index(uint32_t tx, uint32_t ty, uint32_t tiles_x, uint32_t S,
+                                                     uint32_t* shard) {
+    const uint32_t k = (tx + 3u * (ty % S)) % S;
+    *shard = k;
+    if (S == 1u) return ty * tiles_x + tx;
+    const uint32_t P = shard_period(S);
+    const uint32_t rp = ty % P;
+    uint32_t per = 0, pre = 0;
+    ShardRows R(tiles_x, k, S);
+    for (uint32_t r = 0; r < P; ++r, R.next()) {
+        const uint32_t c = R.count();
+        per += c;
+        pre += r < rp ? c : 0u;
+    }
+    return (ty / P) * per + pre + tx / S;  // tx = row start + j*S with the row start < S
 }
 
 // Centre-out dispatch order (a bijection of [0, n)): the shard-local tile range is cut into blocks

@@ -43,6 +43,18 @@ def shard_tiles(width: int, height: int, k: int, S: int) -> np.ndarray:
     return np.array(out, dtype=np.int64).reshape(-1, 2)
 
 
+def shard_tile_index(tx: int, ty: int, width: int, height: int, S: int) -> tuple[int, int]:
+    """Inverse of shard_tiles (bh_common.hpp shard_tile_index): tile (tx, ty) -> (shard, local index)."""
+    tiles_x = (width + TILE - 1) // TILE
+    k = (tx + 3 * ty) % S
+    if S == 1:
+        return k, ty * tiles_x + tx
+    P = shard_period(S)
+    per = sum(shard_row_count(tiles_x, r, k, S) for r in range(P))
+    pre = sum(shard_row_count(tiles_x, r, k, S) for r in range(ty % P))
+    return k, (ty // P) * per + pre + tx // S
+
+
 def packed_stride(width: int, height: int, S: int) -> int:
     """Tiles per rank in the gather buffer (the largest shard; smaller shards are padded)."""
     return max(shard_tile_count(width, height, k, S) for k in range(S))

@@ -138,6 +138,14 @@ def test_unpack_reference_roundtrip():
     assert np.array_equal(frame[..., 0], xx) and np.array_equal(frame[..., 1], yy)
 
 
+@pytest.mark.parametrize("W,H,S", [(100, 52, 1), (100, 52, 3), (44, 30, 5), (200, 120, 8), (64, 64, 6)])
+def test_shard_tile_index_inverts_the_shard_order(W, H, S):
+    """The unpack kernels address the packed buffer from the output tile (shard_tile_index)."""
+    for k in range(S):
+        for t, (tx, ty) in enumerate(multigpu.shard_tiles(W, H, k, S)):
+            assert multigpu.shard_tile_index(int(tx), int(ty), W, H, S) == (k, t)
+
+
 def test_planar_tiles_restore_the_packed_pixels():
     """BH_LAYOUT_TILES_RGB is BH_LAYOUT_TILES with each tile's pixels split into R, G, B planes and
     alpha dropped; planar_to_packed (the numpy statement of bh_tiles_unpack_rgb's per-tile step)
