@@ -238,7 +238,9 @@ def main() -> None:
                                else f"tile-sharded x{n}"
                                + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
             },
-            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u>", "launches": args.steps,
+            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
+                               + (", 3u>" if args.schedule.startswith("tile") and flags == 3
+                                  else (", 4294967295u>" if args.schedule.startswith("tile") else ">")), "launches": args.steps,
                        "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
                        "max_ms": round(float(kern_ms.max()), 5), "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
                        "mean_n_rk": round(sum_nrk / my_px, 4), "frames_per_s": round(1.0 / kern_avg_s, 2)},

@@ -205,7 +205,9 @@ struct FOps {
         return muls(p, s * (iq2 * iq2 * iq));
     }
     __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs(p, s, dot(p, p), 0.0f); }
-    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
+    __device__ __forceinline__ void sq_args(float, float) {}
+    __device__ __forceinline__ void sq_arg(float) {}
+    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags, float&, float&) {
         const float rho = __builtin_amdgcn_sqrtf(p.x * p.x + p.z * p.z);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y) - 0.02f);
         // min of the four sphere SDFs == sqrt(min of squared distances) - 0.5 (sqrt is monotone)
@@ -241,9 +243,24 @@ struct XOps {
     __device__ __forceinline__ static float absmin3(float m, float x, float y, float z) {
         return fminf(m, fminf(fabsf(x), fminf(fabsf(y), fabsf(z))));
     }
-    __device__ __forceinline__ float sqrt(float x, bool used = true) {
-        if constexpr (CR) { bad |= used & crm::sqrt_bad(x); return crm::sqrt_core(x); }
+    // Square roots.  The core is exact for x >= SQRT_MIN (and 0, inf, NaN); below that the caller
+    // must raise `bad`.  Which check covers which root (one v_cmp per check, so they are pooled):
+    //  * r = |ro| and the pow25 roots of rd_derivative: x < 2^-96 makes q*q underflow to 0, so the
+    //    denominator Q = (q*q)*sqrt(q) is 0 (or NaN) and div_d_bad(Q) raises `bad` already.  A lane
+    //    that leaves the step before k1 (surface / blackout) only used r in r < 1 / r > 1, which
+    //    every candidate root of x < 2^-96 decides correctly (all are < 1);
+    //  * rho (disc) and the marker distance: one shared check on the minimum of their arguments
+    //    (sq_args; a flag-disabled term can only cause a spare re-run); the photon-sphere distance
+    //    (sq_arg, evaluated after the step's early exits).
+    __device__ __forceinline__ float sqrt(float x) {
+        if constexpr (CR) return crm::sqrt_core(x);
         else return __builtin_sqrtf(x);
+    }
+    __device__ __forceinline__ void sq_args(float a, float b) {
+        if constexpr (CR) bad |= crm::sqrt_bad(fminf(a, b));
+    }
+    __device__ __forceinline__ void sq_arg(float a) {
+        if constexpr (CR) bad |= crm::sqrt_bad(a);
     }
     __device__ __forceinline__ v3 div6(v3 x) {
         if constexpr (CR) {
@@ -283,15 +300,18 @@ struct XOps {
     }
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
-    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags) {
-        const float rho = sqrt(p.x * p.x + p.z * p.z, (flags & BH_SCENE_DISC) != 0u);
+    // sdf(p) with the arguments of its two roots (for sq_args)
+    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags, float& rho2, float& qm) {
+        rho2 = p.x * p.x + p.z * p.z;
+        const float rho = sqrt(rho2);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
         const float xx = p.x * p.x, yy = p.y * p.y;
         const float dz = -10.0f - p.z, zz = dz * dz;
         const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
         const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
         const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
-        const float m = sqrt(fminf(q1, fminf(q2, fminf(q3, q4))), (flags & BH_SCENE_MARKERS) != 0u) - 0.5f;
+        qm = fminf(q1, fminf(q2, fminf(q3, q4)));
+        const float m = sqrt(qm) - 0.5f;
         // fminf(disc, inf) == disc and fminf(inf, m) == m bit for bit: same result as selecting
         return fminf((flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
                      (flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
@@ -299,34 +319,51 @@ struct XOps {
 };
 #endif
 
-// One iteration of the loop body (:266-328) on `st`.  Returns BH_FATE_* if the ray terminates in
-// this iteration (state then unchanged except `outside`; n_rk counts completed RK updates), or
-// 0xFF if it continues.
+// One iteration of the loop body (:266-328) from `in` into `out`.  Returns BH_FATE_* if the ray
+// terminates in this iteration (n_rk counts completed RK updates), or 0xFF if it continues.
 //
-// BRANCHY = true (single-ray schedules): a lane whose ray terminates before the RK update returns at
-// once and the update is committed unconditionally (saves the selects; the RK block is skipped when
-// every active lane terminates).  BRANCHY = false keeps one basic block for the pair schedule.
-template <bool BRANCHY, class Ops>
-__device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, RayState& st, Ops& X) {
-    const v3 ro = st.ro, rd = st.rd;
+// BRANCHY = true (single-ray schedules): a lane whose ray terminates before the RK update (surface /
+// blackout, fate >= BH_FATE_SURFACE) returns at once WITHOUT writing `out`: its final state is `in`
+// (only n_rk is read for those fates).  Every other lane gets the whole updated state in `out`.
+// `in` is never written, so the caller ping-pongs two states and no register copies are needed
+// (the IEEE re-run of march_step_io reads `in` again); the RK block is skipped when every active
+// lane terminates.  BRANCHY = false keeps one basic block for the pair schedule: `out` is always
+// written (selects).  `in` and `out` may alias only when BRANCHY = false.
+// Scene flags: a kernel instantiated for one flag set (SF) drops the per-step flag selects.
+constexpr uint32_t SF_DYN = 0xFFFFFFFFu;
+
+__device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
+
+template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN>
+__device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
+                                            Ops& X) {
+    const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
+    const v3 ro = in.ro, rd = in.rd;
+    const float travelled = in.travelled, s = in.s;
+    const uint32_t n_rk = in.n_rk;
+    const bool outside = in.outside;
     const float r2 = dot(ro, ro);
     const float r = X.sqrt(r2);                                        // :271
     // :272-283
     // bitwise (not short-circuit) logic keeps the iteration one basic block
     const bool bo_on = a.blackout_eh != 0u;
     const bool out_now = r > 1.0f;
-    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | ((!out_now) & st.outside));
-    st.outside = st.outside | out_now;                                 // only read when bo_on
-    const float ds = X.sdf(ro, a.rs, a.scene_flags);                   // :285
+    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | ((!out_now) & outside));
+    float rho2, qm;
+    const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
+    X.sq_args(rho2, qm);
     uint32_t pre = (ds < MIN_DIST) ? (uint32_t)BH_FATE_SURFACE : 0xFFu;   // :286-288
     pre = blackout ? (uint32_t)BH_FATE_BLACKOUT : pre;
     if constexpr (BRANCHY) {
         if (pre != 0xFFu) return pre;
     }
-    const float dps = X.length(sub(f.cps, ro)) - 0.075f;               // :294
+    // :294 after the exits (measured: 1.5 % faster than before them, A/B r01)
+    const v3 dc = sub(f.cps, ro);
+    const float qps = dot(dc, dc);
+    const float dps = X.sqrt(qps) - 0.075f;
+    X.sq_arg(qps);
     const float dist = fminf(ds, dps);                                 // :299
     const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
-    const float s = st.s;
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
     const v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r, true));
@@ -349,23 +386,25 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     }
 #endif
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
-    const float ntr = st.travelled + dt;                               // :324
+    const float ntr = travelled + dt;                                  // :324
+    out.s = s;
+    out.outside = outside | out_now;                                   // only read when bo_on
     if constexpr (BRANCHY) {
-        st.ro = nro;
-        st.rd = nrd;
-        st.travelled = ntr;
-        st.n_rk += 1u;
-        uint32_t fate = (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;
+        out.ro = nro;
+        out.rd = nrd;
+        out.travelled = ntr;
+        out.n_rk = n_rk + 1u;
+        uint32_t fate = (n_rk + 1u >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;
         return (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;
     }
     const bool go = pre == 0xFFu;
-    st.ro = sel(go, nro, ro);
-    st.rd = sel(go, nrd, rd);
-    st.travelled = go ? ntr : st.travelled;
-    st.n_rk += go ? 1u : 0u;
+    out.ro = sel(go, nro, ro);
+    out.rd = sel(go, nrd, rd);
+    out.travelled = go ? ntr : travelled;
+    out.n_rk = n_rk + (go ? 1u : 0u);
     // flat selects (a nested ?: becomes exec-mask branches)
-    uint32_t fate = (st.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
-    fate = (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;              // :325-327
+    uint32_t fate = (out.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
+    fate = (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;               // :325-327
     return go ? fate : pre;
 }
 
@@ -373,15 +412,17 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
 __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 #endif
 
-// One iteration for one ray (tile / persistent schedules).
-__device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
+// One iteration for one ray from `in` into `out` (step_bf<true> contract: `out` is not written for
+// fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
+template <uint32_t SF = SF_DYN>
+__device__ __forceinline__ uint32_t march_step_io(const MarchArgs& a, const Frame& f, const RayState& in,
+                                                  RayState& out) {
 #if BH_FAST
     FOps X;
-    return step_bf<true>(a, f, st, X);
+    return step_bf<true, FOps, SF>(a, f, in, out, X);
 #else
-    RayState t = st;
     XOps<true> X;
-    uint32_t fate = step_bf<true>(a, f, t, X);
+    uint32_t fate = step_bf<true, XOps<true>, SF>(a, f, in, out, X);
     const uint64_t badm = __ballot(X.bad);
     if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
 #ifdef BH_DIAG_SLOW
@@ -391,33 +432,42 @@ __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& 
         }
 #endif
         if (X.bad) {
-            t = st;
             XOps<false> Y;
-            fate = step_bf<true>(a, f, t, Y);
+            fate = step_bf<true, XOps<false>, SF>(a, f, in, out, Y);
         }
     }
-    st = t;
     return fate;
 #endif
+}
+
+// One iteration for one ray in place (persistent schedule, the tile schedule's cycle watch).
+template <uint32_t SF = SF_DYN>
+__device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
+    // t = st / st = t rather than a select on the fate: the copies fill the tail waves' dependency
+    // stalls (a select form measured 9 % slower at cap 1000, A/B r01)
+    RayState t = st;  // lanes that leave before the RK update keep `st` (n_rk is what they need)
+    const uint32_t fate = march_step_io<SF>(a, f, st, t);
+    st = t;
+    return fate;
 }
 
 // One iteration for two independent rays of the same lane (pair schedule).  Dead rays (alive_k
 // false) are computed on their frozen state and discarded, so the two iterations stay one block.
 __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, RayState& s0, RayState& s1,
                                             bool& alive0, bool& alive1, uint32_t& fate0, uint32_t& fate1) {
-    RayState t0 = s0, t1 = s1;
+    RayState t0, t1;
 #if BH_FAST
     FOps X0, X1;
-    uint32_t f0 = step_bf<false>(a, f, t0, X0);
-    uint32_t f1 = step_bf<false>(a, f, t1, X1);
+    uint32_t f0 = step_bf<false>(a, f, s0, t0, X0);
+    uint32_t f1 = step_bf<false>(a, f, s1, t1, X1);
 #else
     XOps<true> X0, X1;
-    uint32_t f0 = step_bf<false>(a, f, t0, X0);
-    uint32_t f1 = step_bf<false>(a, f, t1, X1);
+    uint32_t f0 = step_bf<false>(a, f, s0, t0, X0);
+    uint32_t f1 = step_bf<false>(a, f, s1, t1, X1);
     const bool bad0 = X0.bad & alive0, bad1 = X1.bad & alive1;
     if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
-        if (bad0) { t0 = s0; XOps<false> Y; f0 = step_bf<false>(a, f, t0, Y); }
-        if (bad1) { t1 = s1; XOps<false> Y; f1 = step_bf<false>(a, f, t1, Y); }
+        if (bad0) { XOps<false> Y; f0 = step_bf<false>(a, f, s0, t0, Y); }
+        if (bad1) { XOps<false> Y; f1 = step_bf<false>(a, f, s1, t1, Y); }
     }
 #endif
     // selects, not branches
@@ -580,6 +630,9 @@ __device__ __forceinline__ uint32_t state_hash(const RayState& st) {
             __float_as_uint(st.rd.x) ^ __float_as_uint(st.rd.y) ^ __float_as_uint(st.rd.z) ^
             __float_as_uint(st.travelled)) + (st.outside ? 0x9E3779B9u : 0u);
 }
+// March `st` to termination with the fast-forward; `steps` = RK updates actually executed.
+// (The tail waves are latency-bound: a ping-pong / uniform-trip form of this loop measured slower.)
+template <uint32_t SF>
 __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& steps,
                                                  HistLds& H, uint32_t lane) {
     // h2: hash of the state two iterations back (none yet: a value that forces a full compare
@@ -591,7 +644,7 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
         H.a[p][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.travelled);
         H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
         h1 = state_hash(st);
-        const uint32_t fate = march_step(a, f, st);
+        const uint32_t fate = march_step<SF>(a, f, st);
         if (fate != 0xFFu) { steps = st.n_rk; return fate; }
         if (state_hash(st) == h2) {
             const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
@@ -610,7 +663,7 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
     }
 }
 
-template <uint32_t FMT>
+template <uint32_t FMT, uint32_t SF>
 __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     __shared__ float lut[lds_tables<FMT>()];
     load_tables<FMT>(a, lut);
@@ -633,8 +686,28 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     st.outside = false;
     uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
-        for (uint32_t it = 0; it < PRIO_ITERS; ++it)
-            if ((fate = march_step(a, f, st)) != 0xFFu) break;
+        // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
+        // writes its input, so no per-step register copies); `in_b` records which one holds the
+        // lane's final state: the output of its last iteration, or its input for the fates decided
+        // before the RK update.  The trip condition is wave-uniform and each lane's iteration is
+        // predicated: with a divergent loop exit the state would be live out of the loop at a
+        // different iteration per lane, which costs a register copy of every state value per
+        // iteration.  (390 -> 370 VALU per step; with the flag template and the guard pooling
+        // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
+        RayState sb = st;
+        bool in_b = false, alive = true;
+        static_assert(PRIO_ITERS % 2u == 0u, "ping-pong pairs");
+        for (uint32_t it = 0; it < PRIO_ITERS && __ballot(alive) != 0ull; it += 2u) {
+            if (alive) {
+                fate = march_step_io<SF>(a, f, st, sb);
+                if (fate != 0xFFu) { alive = false; in_b = !fate_before_rk(fate); }
+            }
+            if (alive) {
+                fate = march_step_io<SF>(a, f, sb, st);
+                if (fate != 0xFFu) { alive = false; in_b = fate_before_rk(fate); }
+            }
+        }
+        if (in_b) st = sb;
         steps = st.n_rk;
         if (fate == 0xFFu) {
             // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
@@ -642,7 +715,7 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
             // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
             __builtin_amdgcn_s_setprio(2);
             __shared__ HistLds hist[4];  // 16 KiB per workgroup: 8 workgroups per CU still fit
-            fate = march_cycles(a, f, st, steps, hist[threadIdx.x >> 6], lane);
+            fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
         }
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
