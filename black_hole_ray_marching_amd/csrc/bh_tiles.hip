@@ -75,33 +75,70 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
 
 // Counting sort of the dispatch order by the previous frame's per-tile cost (cost_bucket), one
 // kernel: the bucket histogram was accumulated by the march kernel that wrote the costs
-// (MarchArgs::order_tot), so each block only reserves its bucket ranges (one returning atomic per
-// bucket, issued in parallel) and scatters.  Slots are visited in centre-out order, so ties keep
-// (roughly) the centre-out order.  counters: [0..B-1) the histogram (the last bucket is the
-// remainder), [B..2B) cursors, [2B] the block ticket; the last block to finish zeroes them all, so
-// they are zero again before the next march kernel accumulates (graph replay needs no memset node).
-__global__ void __launch_bounds__(256) order_scatter_kernel(const uint8_t* __restrict__ cost, uint32_t n,
-                                                          uint32_t L, uint32_t c, uint32_t* counters,
-                                                          uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[ORDER_BUCKETS], base[ORDER_BUCKETS], ticket;
-    if (threadIdx.x < ORDER_BUCKETS) hist[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t t = 0, b = 0, k = 0;
-    if (i < n) {
-        t = centre_out(i, n, L, c);
-        b = cost_bucket(cost[t]);
-        k = atomicAdd(&hist[b], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < ORDER_BUCKETS && hist[threadIdx.x]) {
-        uint32_t off = 0;
+// (MarchArgs::order_tot).  A block of ORDER_THREADS threads takes ORDER_PER_BLOCK consecutive
+// dispatch slots (each wave a contiguous run of ORDER_PER_WAVE, visited in centre-out order); ranks
+// inside a wave come from per-bucket ballots (no LDS atomics), the block's per-wave counts are
+// prefix-summed in LDS, and the block reserves its range of every bucket with one returning global
+// atomic per bucket.  Ties therefore keep the centre-out order inside a block.  counters: [0..B-1)
+// the histogram (the last bucket is the remainder), [B..2B) cursors, [2B] the block ticket; the last
+// block to finish zeroes them all, so they are zero again before the next march kernel accumulates
+// (graph replay needs no memset node).  (One tile per thread with an LDS atomic per tile and 512
+// blocks' global atomics on the same 6 words took 22.8 us per frame; this form ~4 us.)
+constexpr uint32_t ORDER_THREADS = 1024;
+constexpr uint32_t ORDER_WAVES = ORDER_THREADS / 64u;
+constexpr uint32_t ORDER_PER_LANE = 4;
+constexpr uint32_t ORDER_PER_WAVE = 64u * ORDER_PER_LANE;
+constexpr uint32_t ORDER_PER_BLOCK = ORDER_THREADS * ORDER_PER_LANE;
+
+__global__ void __launch_bounds__(ORDER_THREADS) order_scatter_kernel(const uint8_t* __restrict__ cost, uint32_t n,
+                                                                      uint32_t L, uint32_t c, uint32_t* counters,
+                                                                      uint32_t* __restrict__ order) {
+    __shared__ uint32_t woff[ORDER_WAVES][ORDER_BUCKETS];  // per-wave counts, then offsets in the block
+    __shared__ uint32_t base[ORDER_BUCKETS], ticket;
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint32_t s0 = blockIdx.x * ORDER_PER_BLOCK + w * ORDER_PER_WAVE + lane;
+    uint32_t t[ORDER_PER_LANE], b[ORDER_PER_LANE], r[ORDER_PER_LANE];
+    uint32_t cnt[ORDER_BUCKETS];
 #pragma unroll
-        for (uint32_t j = 0; j < ORDER_BUCKETS - 1u; ++j) off += j < threadIdx.x ? counters[j] : 0u;
-        base[threadIdx.x] = off + atomicAdd(&counters[ORDER_BUCKETS + threadIdx.x], hist[threadIdx.x]);
+    for (uint32_t q = 0; q < ORDER_BUCKETS; ++q) cnt[q] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < ORDER_PER_LANE; ++j) {
+        const uint32_t slot = s0 + 64u * j;
+        t[j] = slot < n ? centre_out(slot, n, L, c) : 0u;
+        b[j] = slot < n ? cost_bucket(cost[t[j]]) : ORDER_BUCKETS;
+        r[j] = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < ORDER_BUCKETS; ++q) {
+            const uint64_t m = __ballot(b[j] == q);
+            if (b[j] == q)
+                r[j] = cnt[q] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            cnt[q] += (uint32_t)__popcll(m);
+        }
+    }
+    if (lane < ORDER_BUCKETS) {
+        uint32_t v = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < ORDER_BUCKETS; ++q) v = lane == q ? cnt[q] : v;
+        woff[w][lane] = v;
     }
     __syncthreads();
-    if (i < n) order[base[b] + k] = t;
+    if (threadIdx.x < ORDER_BUCKETS) {
+        const uint32_t q = threadIdx.x;
+        uint32_t tot = 0;
+        for (uint32_t v = 0; v < ORDER_WAVES; ++v) {  // exclusive prefix over the block's waves
+            const uint32_t x = woff[v][q];
+            woff[v][q] = tot;
+            tot += x;
+        }
+        uint32_t off = 0;  // start of bucket q in the order: the histogram's earlier buckets
+#pragma unroll
+        for (uint32_t j = 0; j < ORDER_BUCKETS - 1u; ++j) off += j < q ? counters[j] : 0u;
+        base[q] = tot ? off + atomicAdd(&counters[ORDER_BUCKETS + q], tot) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < ORDER_PER_LANE; ++j)
+        if (b[j] < ORDER_BUCKETS) order[base[b[j]] + woff[w][b[j]] + r[j]] = t[j];
     if (threadIdx.x == 0) {
         __threadfence();
         ticket = atomicAdd(&counters[2 * ORDER_BUCKETS], 1u);
@@ -120,8 +157,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
                                                                          uint32_t* counters, uint32_t* order,
                                                                          hipStream_t s) {
     if (n == 0) return 0;
-    const uint32_t blocks = (n + 255u) / 256u;
-    hipLaunchKernelGGL(bh::order_scatter_kernel, dim3(blocks), dim3(256), 0, s, cost, n, L, c, counters, order);
+    const uint32_t blocks = (n + bh::ORDER_PER_BLOCK - 1u) / bh::ORDER_PER_BLOCK;
+    hipLaunchKernelGGL(bh::order_scatter_kernel, dim3(blocks), dim3(bh::ORDER_THREADS), 0, s, cost, n, L, c, counters,
+                       order);
     return (int)hipGetLastError();
 }
 

@@ -310,6 +310,33 @@ def test_temporal_order_never_changes_results(torch_cuda, sky_small):
     scene.close()
 
 
+@pytest.mark.parametrize("W,H", [(1024, 1024), (1496, 1000)])
+def test_temporal_order_is_a_permutation_across_blocks(torch_cuda, sky_small, W, H):
+    """The order kernel sorts ORDER_PER_BLOCK (4096) slots per block and reserves bucket ranges
+    with global atomics: at several blocks (and a partial last block), frames rendered in the
+    learned order cover every tile exactly once (NaN-filled targets) and equal the static order."""
+    torch = torch_cuda
+    cap = 64
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
+    ref = None
+    for i, cam in enumerate(["B", "A", "A", "E", "A"]):
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        col = torch.full((H, W, 4), float("nan"), device="cuda")
+        scene.render(col, None, schedule=bh.BH_SCHED_TILE)
+        torch.cuda.synchronize()
+        if cam != "A":
+            continue
+        got = col.cpu().numpy().view(np.uint32)
+        if ref is None:
+            st = torch.full((H, W, 4), float("nan"), device="cuda")
+            scene.render(st, None, schedule=bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER)
+            torch.cuda.synchronize()
+            ref = st.cpu().numpy().view(np.uint32)
+            assert not np.isnan(st.cpu().numpy()).any()
+        assert np.array_equal(got, ref), f"frame {i}"
+    scene.close()
+
+
 @pytest.mark.parametrize("cam", ["A", "B"])
 def test_cycle_fast_forward_is_exact(torch_cuda, cam):
     """The tile schedule advances rays caught in an exact period-1/2 cycle straight to the cap
