@@ -178,7 +178,7 @@ struct RayState {
     float travelled;
     float s;
     uint32_t n_rk;
-    bool outside;
+    uint32_t outside;  // 0 / 1: the WGSL's `outside` (:270); u32, so the blackout test stays compare + select
 };
 
 // ---- one RK iteration, branch-free ---------------------------------------------------------------
@@ -335,27 +335,28 @@ constexpr uint32_t SF_DYN = 0xFFFFFFFFu;
 __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
 
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN>
-__device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
-                                            Ops& X) {
+__device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
+                                        uint32_t& fate) {
     const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
     const v3 ro = in.ro, rd = in.rd;
     const float travelled = in.travelled, s = in.s;
     const uint32_t n_rk = in.n_rk;
-    const bool outside = in.outside;
     const float r2 = dot(ro, ro);
     const float r = X.sqrt(r2);                                        // :271
-    // :272-283
-    // bitwise (not short-circuit) logic keeps the iteration one basic block
+    // :272-283: blackout if (r < 1 and rd.ro < 0), or if !(r > 1) and the ray was outside before;
+    // r > 1 sets `outside`.  Bitwise (not short-circuit) logic: lane masks, no branches.
     const bool bo_on = a.blackout_eh != 0u;
-    const bool out_now = r > 1.0f;
-    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | ((!out_now) & outside));
+    const bool not_out = !(r > 1.0f);                                  // NaN r: "else" branch, as the WGSL
+    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | (not_out & (in.outside != 0u)));
     float rho2, qm;
     const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
     X.sq_args(rho2, qm);
-    uint32_t pre = (ds < MIN_DIST) ? (uint32_t)BH_FATE_SURFACE : 0xFFu;   // :286-288
-    pre = blackout ? (uint32_t)BH_FATE_BLACKOUT : pre;
+    const bool surface = ds < MIN_DIST;                                // :286-288
     if constexpr (BRANCHY) {
-        if (pre != 0xFFu) return pre;
+        if (blackout | surface) {
+            fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+            return true;
+        }
     }
     // :294 after the exits (measured: 1.5 % faster than before them, A/B r01)
     const v3 dc = sub(f.cps, ro);
@@ -388,24 +389,28 @@ __device__ __forceinline__ uint32_t step_bf(const MarchArgs& a, const Frame& f, 
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
     const float ntr = travelled + dt;                                  // :324
     out.s = s;
-    out.outside = outside | out_now;                                   // only read when bo_on
+    out.outside = not_out ? in.outside : 1u;                           // only read when bo_on
+    const bool escape = ntr > a.max_dist;                              // :325-327
+    const bool capped = n_rk + 1u >= a.max_iters;                      // loop end (:266)
     if constexpr (BRANCHY) {
         out.ro = nro;
         out.rd = nrd;
         out.travelled = ntr;
         out.n_rk = n_rk + 1u;
-        uint32_t fate = (n_rk + 1u >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;
-        return (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;
+        fate = escape ? (uint32_t)BH_FATE_ESCAPE : (uint32_t)BH_FATE_CAP;
+        return escape | capped;
     }
-    const bool go = pre == 0xFFu;
+    const bool pre = blackout | surface;
+    const bool go = !pre;
     out.ro = sel(go, nro, ro);
     out.rd = sel(go, nrd, rd);
     out.travelled = go ? ntr : travelled;
     out.n_rk = n_rk + (go ? 1u : 0u);
     // flat selects (a nested ?: becomes exec-mask branches)
-    uint32_t fate = (out.n_rk >= a.max_iters) ? (uint32_t)BH_FATE_CAP : 0xFFu;  // loop end (:266)
-    fate = (ntr > a.max_dist) ? (uint32_t)BH_FATE_ESCAPE : fate;               // :325-327
-    return go ? fate : pre;
+    const uint32_t pre_fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+    const uint32_t post_fate = escape ? (uint32_t)BH_FATE_ESCAPE : (uint32_t)BH_FATE_CAP;
+    fate = go ? post_fate : pre_fate;
+    return pre | escape | capped;
 }
 
 #ifdef BH_DIAG_SLOW
@@ -415,14 +420,14 @@ __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 // One iteration for one ray from `in` into `out` (step_bf<true> contract: `out` is not written for
 // fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
 template <uint32_t SF = SF_DYN>
-__device__ __forceinline__ uint32_t march_step_io(const MarchArgs& a, const Frame& f, const RayState& in,
-                                                  RayState& out) {
+__device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
+                                              uint32_t& fate) {
 #if BH_FAST
     FOps X;
-    return step_bf<true, FOps, SF>(a, f, in, out, X);
+    return step_bf<true, FOps, SF>(a, f, in, out, X, fate);
 #else
     XOps<true> X;
-    uint32_t fate = step_bf<true, XOps<true>, SF>(a, f, in, out, X);
+    bool done = step_bf<true, XOps<true>, SF>(a, f, in, out, X, fate);
     const uint64_t badm = __ballot(X.bad);
     if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
 #ifdef BH_DIAG_SLOW
@@ -433,22 +438,24 @@ __device__ __forceinline__ uint32_t march_step_io(const MarchArgs& a, const Fram
 #endif
         if (X.bad) {
             XOps<false> Y;
-            fate = step_bf<true, XOps<false>, SF>(a, f, in, out, Y);
+            done = step_bf<true, XOps<false>, SF>(a, f, in, out, Y, fate);
         }
     }
-    return fate;
+    return done;
 #endif
 }
 
-// One iteration for one ray in place (persistent schedule, the tile schedule's cycle watch).
+// One iteration for one ray in place (persistent schedule, the tile schedule's cycle watch):
+// BH_FATE_* if the ray terminates, else 0xFF.
 template <uint32_t SF = SF_DYN>
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
     // t = st / st = t rather than a select on the fate: the copies fill the tail waves' dependency
     // stalls (a select form measured 9 % slower at cap 1000, A/B r01)
     RayState t = st;  // lanes that leave before the RK update keep `st` (n_rk is what they need)
-    const uint32_t fate = march_step_io<SF>(a, f, st, t);
+    uint32_t fate;
+    const bool done = march_step_io<SF>(a, f, st, t, fate);
     st = t;
-    return fate;
+    return done ? fate : 0xFFu;
 }
 
 // One iteration for two independent rays of the same lane (pair schedule).  Dead rays (alive_k
@@ -458,16 +465,18 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
     RayState t0, t1;
 #if BH_FAST
     FOps X0, X1;
-    uint32_t f0 = step_bf<false>(a, f, s0, t0, X0);
-    uint32_t f1 = step_bf<false>(a, f, s1, t1, X1);
+    uint32_t f0, f1;
+    const bool d0 = step_bf<false>(a, f, s0, t0, X0, f0);
+    const bool d1 = step_bf<false>(a, f, s1, t1, X1, f1);
 #else
     XOps<true> X0, X1;
-    uint32_t f0 = step_bf<false>(a, f, s0, t0, X0);
-    uint32_t f1 = step_bf<false>(a, f, s1, t1, X1);
+    uint32_t f0, f1;
+    bool d0 = step_bf<false>(a, f, s0, t0, X0, f0);
+    bool d1 = step_bf<false>(a, f, s1, t1, X1, f1);
     const bool bad0 = X0.bad & alive0, bad1 = X1.bad & alive1;
     if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
-        if (bad0) { XOps<false> Y; f0 = step_bf<false>(a, f, s0, t0, Y); }
-        if (bad1) { XOps<false> Y; f1 = step_bf<false>(a, f, s1, t1, Y); }
+        if (bad0) { XOps<false> Y; d0 = step_bf<false>(a, f, s0, t0, Y, f0); }
+        if (bad1) { XOps<false> Y; d1 = step_bf<false>(a, f, s1, t1, Y, f1); }
     }
 #endif
     // selects, not branches
@@ -477,7 +486,7 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
     s1.ro = sel(alive1, t1.ro, s1.ro); s1.rd = sel(alive1, t1.rd, s1.rd);
     s1.travelled = alive1 ? t1.travelled : s1.travelled; s1.n_rk = alive1 ? t1.n_rk : s1.n_rk;
     s1.outside = alive1 ? t1.outside : s1.outside;
-    const bool e0 = alive0 & (f0 != 0xFFu), e1 = alive1 & (f1 != 0xFFu);
+    const bool e0 = alive0 & d0, e1 = alive1 & d1;
     fate0 = e0 ? f0 : fate0;
     fate1 = e1 ? f1 : fate1;
     alive0 = alive0 & !e0;
@@ -607,7 +616,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // termination test can fire (both states of the cycle already passed them), so the ray ends with
 // fate CAP, n_rk = max_iters and the cycle state of matching parity: the loop's own result,
 // without running it.  Checked from PRIO_ITERS on (the cycles found start at median iteration 30).
-struct Hist { v3 ro, rd; float tr; bool outside; };
+struct Hist { v3 ro, rd; float tr; uint32_t outside; };
 
 __device__ __forceinline__ bool same_bits(float x, float y) { return __float_as_uint(x) == __float_as_uint(y); }
 __device__ __forceinline__ bool same_state(const RayState& st, const Hist& h) {
@@ -628,7 +637,7 @@ struct HistLds { float4 a[2][2][64]; };  // [slot][ro+tr | rd+outside][lane]
 __device__ __forceinline__ uint32_t state_hash(const RayState& st) {
     return (__float_as_uint(st.ro.x) ^ __float_as_uint(st.ro.y) ^ __float_as_uint(st.ro.z) ^
             __float_as_uint(st.rd.x) ^ __float_as_uint(st.rd.y) ^ __float_as_uint(st.rd.z) ^
-            __float_as_uint(st.travelled)) + (st.outside ? 0x9E3779B9u : 0u);
+            __float_as_uint(st.travelled)) + st.outside * 0x9E3779B9u;
 }
 // March `st` to termination with the fast-forward; `steps` = RK updates actually executed.
 // (The tail waves are latency-bound: a ping-pong / uniform-trip form of this loop measured slower.)
@@ -638,17 +647,17 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
     // h2: hash of the state two iterations back (none yet: a value that forces a full compare
     // against slot 1, whose travelled is a NaN pattern no arithmetic produces -- no match)
     H.a[1][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, __uint_as_float(0xFFFFFFFFu));
-    H.a[1][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+    H.a[1][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float(st.outside));
     uint32_t h2 = ~state_hash(st), h1 = 0;
     for (uint32_t p = 0;; p ^= 1u) {
         H.a[p][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.travelled);
-        H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float((uint32_t)st.outside));
+        H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float(st.outside));
         h1 = state_hash(st);
         const uint32_t fate = march_step<SF>(a, f, st);
         if (fate != 0xFFu) { steps = st.n_rk; return fate; }
         if (state_hash(st) == h2) {
             const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
-            const Hist hs{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w) != 0u};
+            const Hist hs{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w)};
             if (same_state(st, hs)) {
                 steps = st.n_rk;
                 if ((a.max_iters - st.n_rk) & 1u) {
@@ -683,7 +692,7 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
     st.s = ray_s(f, st.rd);
     st.travelled = 0.0f;
     st.n_rk = 0;
-    st.outside = false;
+    st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
         // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
@@ -699,17 +708,15 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
         static_assert(PRIO_ITERS % 2u == 0u, "ping-pong pairs");
         for (uint32_t it = 0; it < PRIO_ITERS && __ballot(alive) != 0ull; it += 2u) {
             if (alive) {
-                fate = march_step_io<SF>(a, f, st, sb);
-                if (fate != 0xFFu) { alive = false; in_b = !fate_before_rk(fate); }
+                if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; in_b = !fate_before_rk(fate); }
             }
             if (alive) {
-                fate = march_step_io<SF>(a, f, sb, st);
-                if (fate != 0xFFu) { alive = false; in_b = fate_before_rk(fate); }
+                if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; in_b = fate_before_rk(fate); }
             }
         }
         if (in_b) st = sb;
         steps = st.n_rk;
-        if (fate == 0xFFu) {
+        if (alive) {
             // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
             // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
             // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
@@ -773,7 +780,7 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
     uint32_t n_ready = 0, n_done = 0;                  // queue fill levels (wave-uniform)
 
     RayState st;
-    st.ro = f.ro0; st.rd = f.ro0; st.s = 0.0f; st.travelled = 0.0f; st.n_rk = 0; st.outside = false;
+    st.ro = f.ro0; st.rd = f.ro0; st.s = 0.0f; st.travelled = 0.0f; st.n_rk = 0; st.outside = 0u;
     uint32_t idx = 0;
     bool alive = false;
 
@@ -817,7 +824,7 @@ __global__ void __launch_bounds__(256) march_persistent_kernel(MarchArgs a, uint
                         st.rd = mk(Q.r_x[e], Q.r_y[e], Q.r_z[e]);
                         st.s = Q.r_s[e];
                         idx = Q.r_idx[e];
-                        st.travelled = 0.0f; st.n_rk = 0; st.outside = false;
+                        st.travelled = 0.0f; st.n_rk = 0; st.outside = 0u;
                         alive = true;
                     }
                 }
@@ -895,7 +902,7 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
     bool alive1 = t1 < a.n_tiles && px1 < a.width && py1 < a.height;
     const bool valid0 = alive0, valid1 = alive1;
     RayState s0, s1;
-    s0.ro = f.ro0; s0.travelled = 0.0f; s0.n_rk = 0; s0.outside = false;
+    s0.ro = f.ro0; s0.travelled = 0.0f; s0.n_rk = 0; s0.outside = 0u;
     s1 = s0;
     s0.rd = sel(valid0, pixel_ray(a, px0, py0), f.ro0);
     s1.rd = sel(valid1, pixel_ray(a, px1, py1), f.ro0);
