@@ -4,8 +4,9 @@
 // v_div_fixup) and measures ~50 cycles per wave-instruction stream on MI355X; its IEEE sqrt ~54
 // (tools/ubench/valu_rates.hip).  The march loop needs 18 divisions and 7 square roots per RK step,
 // so these dominate the exact (bit-parity) kernel.  The forms below drop the scaling/fix-up steps,
-// which only act on operands near the ends of the exponent range, and share one refined reciprocal
-// between the three divisions of rd_derivative.  Each form is the SAME arithmetic as hipcc's
+// which only act on operands near the ends of the exponent range, share one correctly rounded
+// reciprocal between the three divisions of rd_derivative, and are as short as exhaustive checks
+// on the device allow (tools/ubench/cr_forms.hip).  Each form is the SAME arithmetic as hipcc's
 // correctly-rounded expansion inside its safe domain, and each caller accumulates a "bad" flag for
 // operands outside that domain; the march loop then redoes that RK step with plain IEEE ops
 // (bh_march.hpp, march_step).  tests/test_gpu_crmath.py checks every form against IEEE results on
@@ -18,34 +19,41 @@ namespace bh {
 namespace crm {
 
 // ---- square root ------------------------------------------------------------------------------
-// v_sqrt_f32 is within 1 ulp for inputs >= 2^-96; one residual test on each neighbour picks the
-// correctly rounded value (LLVM's lowering of an IEEE fsqrt without its small-input scaling).
-// Exact for x >= 2^-96 (incl. +inf), x == +-0, and NaN/negative -> NaN.
+// One Newton step on the hardware reciprocal square root: y = v_rsq(x), s = x*y, and the residual
+// x - s*s (exact in an FMA) corrects s by y/2:  sqrt(x) = fma(x - s*s, y/2, s).  1 transcendental + 4
+// VALU ops (the previous form, v_sqrt + a residual test of both neighbours, took 1 + 8).  Equal to
+// the IEEE sqrt for EVERY float x in [2^-102, FLT_MAX] (exhaustive, tools/ubench/cr_forms.hip on
+// MI355X; profiles/r01_cr_forms.log); wrong for 0 (0*inf), +inf (inf*0) and x < 2^-102, so the guard
+// is the range [SQRT_MIN, FLT_MAX] (NaN fails it too).
 constexpr float SQRT_MIN = 0x1p-96f;
+constexpr float SQRT_MAX = 0x1.fffffep127f;
 
 __device__ __forceinline__ float sqrt_core(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
-    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
-    const float rm = __builtin_fmaf(-sm, s, x);
-    const float rp = __builtin_fmaf(-sp, s, x);
-    float r = (rm <= 0.0f) ? sm : s;
-    r = (rp > 0.0f) ? sp : r;
-    return r;
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
+    const float h = 0.5f * y;
+    const float r = __builtin_fmaf(-s, s, x);
+    return __builtin_fmaf(r, h, s);
 }
-// unsafe iff 0 <= x < 2^-96 (x == 0 is exact too, but rare; it just takes the IEEE path)
-__device__ __forceinline__ bool sqrt_bad(float x) { return x < SQRT_MIN; }
+// unsafe iff x is outside [2^-96, FLT_MAX] (0, +inf and NaN included)
+__device__ __forceinline__ bool sqrt_bad(float x) { return !(x >= SQRT_MIN && x <= SQRT_MAX); }
+// the same for two values (one v_min + one v_max + two compares)
+__device__ __forceinline__ bool sqrt_bad2(float a, float b) {
+    return !(fminf(a, b) >= SQRT_MIN) | !(fmaxf(a, b) <= SQRT_MAX);
+}
 
 // ---- division by a shared denominator ---------------------------------------------------------
-// Markstein sequence of hipcc's IEEE division with the div_scale / div_fmas scaling left out:
-//   r0 = rcp(d); r = r0 + r0*(1 - d*r0); y = n*r; y += r*(n - d*y); q = y + r*(n - d*y)
-// Correctly rounded when d and n/d are normal and far from the exponent limits and |n| is not tiny
-// (the residual n - d*y must not underflow).  The caller guarantees:
+// r = v_rcp(d) refined once, r += r*(1 - d*r), is the correctly rounded reciprocal RN(1/d) for every
+// normal d whose reciprocal is normal (exhaustive on MI355X, tools/ubench/cr_forms.hip op R).  Then
+// y = n*r and ONE residual correction  q = y + r*(n - d*y)  is RN(n/d) (Markstein's theorem; checked
+// exhaustively over all 2^46 pairs of significands n, d in [1, 2) against the two-correction
+// sequence of hipcc's IEEE division, op D; every op is exactly scale-covariant in the guarded normal
+// range, op X, so the square covers the domain).  Domain (the caller guarantees it):
 //   DIV_D_MIN <= d <= DIV_D_MAX  (checked per denominator, div_d_bad)
 //   n == 0 or DIV_N_MIN <= |n| <= 2^64
-// The residuals are formed negated, e' = d*y - n = -(n - d*y) (exact in an FMA, RN is symmetric),
-// and added back as fma(-e', r, y): identical for n != 0, and for n = +-0 every sum then keeps the
-// IEEE sign of the zero quotient (-0 + -0 = -0) without a copysign.
+// The residual is formed negated, e = d*y - n = -(n - d*y) (exact in an FMA, RN is symmetric), and
+// added back as fma(-e, r, y): identical for n != 0, and for n = +-0 the sum keeps the IEEE sign of
+// the zero quotient (-0 + -0 = -0) without a copysign.
 constexpr float DIV_D_MIN = 0x1p-40f;
 constexpr float DIV_D_MAX = 0x1p+60f;
 constexpr float DIV_N_MIN = 0x1p-60f;
@@ -60,10 +68,8 @@ __device__ __forceinline__ Rcp rcp_refined(float d) {
 }
 __device__ __forceinline__ float div_core(float n, const Rcp& R) {
     const float y = n * R.r;
-    const float e1 = __builtin_fmaf(R.d, y, -n);
-    const float y1 = __builtin_fmaf(-e1, R.r, y);
-    const float e2 = __builtin_fmaf(R.d, y1, -n);
-    return __builtin_fmaf(-e2, R.r, y1);
+    const float e = __builtin_fmaf(R.d, y, -n);
+    return __builtin_fmaf(-e, R.r, y);
 }
 __device__ __forceinline__ bool div_d_bad(float d) { return !(d >= DIV_D_MIN && d <= DIV_D_MAX); }
 

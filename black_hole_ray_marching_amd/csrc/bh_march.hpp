@@ -243,21 +243,21 @@ struct XOps {
     __device__ __forceinline__ static float absmin3(float m, float x, float y, float z) {
         return fminf(m, fminf(fabsf(x), fminf(fabsf(y), fabsf(z))));
     }
-    // Square roots.  The core is exact for x >= SQRT_MIN (and 0, inf, NaN); below that the caller
-    // must raise `bad`.  Which check covers which root (one v_cmp per check, so they are pooled):
-    //  * r = |ro| and the pow25 roots of rd_derivative: x < 2^-96 makes q*q underflow to 0, so the
-    //    denominator Q = (q*q)*sqrt(q) is 0 (or NaN) and div_d_bad(Q) raises `bad` already.  A lane
-    //    that leaves the step before k1 (surface / blackout) only used r in r < 1 / r > 1, which
-    //    every candidate root of x < 2^-96 decides correctly (all are < 1);
-    //  * rho (disc) and the marker distance: one shared check on the minimum of their arguments
-    //    (sq_args; a flag-disabled term can only cause a spare re-run); the photon-sphere distance
-    //    (sq_arg, evaluated after the step's early exits).
+    // Square roots.  The core is exact for x in [SQRT_MIN, FLT_MAX]; outside that the caller must
+    // raise `bad`.  Which check covers which root (one v_cmp per bound, so they are pooled):
+    //  * r = |ro| and the pow25 roots of rd_derivative: x < 2^-96 makes q*q underflow to 0 and
+    //    x = inf makes it inf, so the denominator Q = (q*q)*sqrt(q) is 0, inf or NaN and
+    //    div_d_bad(Q) raises `bad` already.  The step's exit tests (before k1) compare r^2, not r
+    //    (step_bf), so a lane that leaves early never reads r;
+    //  * rho (disc) and the marker distance: one shared range check on the min and max of their
+    //    arguments (sq_args; a flag-disabled term can only cause a spare re-run); the photon-sphere
+    //    distance (sq_arg, evaluated after the step's early exits).
     __device__ __forceinline__ float sqrt(float x) {
         if constexpr (CR) return crm::sqrt_core(x);
         else return __builtin_sqrtf(x);
     }
     __device__ __forceinline__ void sq_args(float a, float b) {
-        if constexpr (CR) bad |= crm::sqrt_bad(fminf(a, b));
+        if constexpr (CR) bad |= crm::sqrt_bad2(a, b);
     }
     __device__ __forceinline__ void sq_arg(float a) {
         if constexpr (CR) bad |= crm::sqrt_bad(a);
@@ -332,6 +332,9 @@ struct XOps {
 // Scene flags: a kernel instantiated for one flag set (SF) drops the per-step flag selects.
 constexpr uint32_t SF_DYN = 0xFFFFFFFFu;
 
+// r > 1 for r = RN(sqrt(r2)) exactly when r2 > 1 + 2^-23 (step_bf)
+constexpr float R2_GT1 = 0x1.000002p0f;
+
 __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
 
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN>
@@ -345,9 +348,14 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const float r = X.sqrt(r2);                                        // :271
     // :272-283: blackout if (r < 1 and rd.ro < 0), or if !(r > 1) and the ray was outside before;
     // r > 1 sets `outside`.  Bitwise (not short-circuit) logic: lane masks, no branches.
+    // The tests read r^2: for r = RN(sqrt(r2)),  r < 1  <=>  r2 < 1  and  r > 1  <=>  r2 > 1 + 2^-23
+    // (RN(sqrt) is monotone; sqrt(1 + 2^-23) < 1 + 2^-24, the midpoint above 1, and
+    // sqrt(next float) > it; NaN fails every compare either way; tests/test_oracle.py checks every
+    // float in [1/4, 4]).  So the exits do not wait for the root, and lanes that leave here need no
+    // guard on it.
     const bool bo_on = a.blackout_eh != 0u;
-    const bool not_out = !(r > 1.0f);                                  // NaN r: "else" branch, as the WGSL
-    const bool blackout = bo_on & (((r < 1.0f) & (dot(rd, ro) < 0.0f)) | (not_out & (in.outside != 0u)));
+    const bool not_out = !(r2 > R2_GT1);                               // NaN: "else" branch, as the WGSL
+    const bool blackout = bo_on & (((r2 < 1.0f) & (dot(rd, ro) < 0.0f)) | (not_out & (in.outside != 0u)));
     float rho2, qm;
     const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
     X.sq_args(rho2, qm);

@@ -34,6 +34,9 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 4: srgb_encode over every 32-bit pattern in [base, base + count) against a binary search of T
 // op 6: srgb_encode_lut (table form) against srgb_encode over every 32-bit pattern in [base, base + count)
 // op 5: div12 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
+// op 7: div_core over EVERY pair of significands (n, d) in [1, 2)^2 with d's 23 fraction bits in
+//       [base, base + count / 2^23): all 2^23 numerators per denominator (the full 2^46 square is
+//       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
 __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, uint64_t count,
                                                       unsigned long long* cnt, uint32_t* ex, const float* T,
                                                       const uint8_t* B) {
@@ -42,7 +45,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
         if (op == 0) {
             const uint32_t bits = (uint32_t)(base + i);
             const float x = __uint_as_float(bits);
-            if (crm::sqrt_bad(x) && x != 0.0f) continue;
+            if (crm::sqrt_bad(x)) continue;
             const float got = crm::sqrt_core(x), want = __builtin_sqrtf(x);
             if (__float_as_uint(got) != __float_as_uint(want) && !(got != got && want != want))
                 record(cnt, ex, bits, 0, __float_as_uint(got), __float_as_uint(want));
@@ -78,6 +81,12 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             }
             const uint32_t got = srgb_encode(x, T);
             if (got != (uint32_t)lo) record(cnt, ex, bits, 0, got, (uint32_t)lo);
+        } else if (op == 7) {
+            const uint32_t dm = (uint32_t)(base + (i >> 23)) & 0x7FFFFFu, nm = (uint32_t)i & 0x7FFFFFu;
+            const float d = __uint_as_float(0x3F800000u | dm), n = __uint_as_float(0x3F800000u | nm);
+            const float got = crm::div_core(n, crm::rcp_refined(d)), want = n / d;
+            if (__float_as_uint(got) != __float_as_uint(want))
+                record(cnt, ex, __float_as_uint(n), __float_as_uint(d), __float_as_uint(got), __float_as_uint(want));
         } else if (op == 2 || op == 3) {
             const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
             float d = fabsf(rnd_float(h1, -40, 59));
@@ -103,7 +112,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 6 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 7 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;

@@ -244,7 +244,9 @@ int bh_srgb_encode_table(float* out257);
  * patterns [base, base+count); op 2: n/d on `count` random pairs seeded by base; op 3: n/d near exact
  * quotients; op 4: the BGRA8 sRGB encoder over float bit patterns [base, base+count) against a
  * binary search of bh_srgb_encode_table; op 5: x/12 as the bloom chain computes it, over bit
- * patterns [base, base+count); op 6: the bloom chain's table-form sRGB encoder against op 4's).  *out_mismatches = number of differing results;
+ * patterns [base, base+count); op 6: the bloom chain's table-form sRGB encoder against op 4's; op 7:
+ * n/d over all 2^23 numerator significands for the denominator significands (fraction bits)
+ * [base, base + count/2^23)).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

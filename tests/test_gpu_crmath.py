@@ -2,7 +2,9 @@
 (black_hole_ray_marching_amd/csrc/bh_crmath.hpp) against hipcc's IEEE operations, on device.
 
 Exhaustive where the domain is 1-D (sqrt over every non-negative float bit pattern; x/6 over all
-2^32 patterns), randomised for n/d (2^31 random pairs + 2^30 near-exact quotients)."""
+2^32 patterns); for n/d, every numerator significand against blocks of denominator significands
+(the whole 2^46 square is tools/ubench/cr_forms.hip, log in profiles/r01_cr_forms.log), plus 2^31
+random pairs over the guarded exponent range and 2^30 near-exact quotients."""
 import ctypes as C
 
 import pytest
@@ -29,7 +31,7 @@ def run(lib, op, base, count):
 
 
 def test_sqrt_core_exhaustive(lib):
-    # every non-negative pattern from +0 up to +inf (the guard sends 0 < x < 2^-96 to IEEE sqrt)
+    # every non-negative pattern from +0 up to +inf (the guard sends x < 2^-96 and +inf to IEEE sqrt)
     m, ex = run(lib, 0, 0, 0x7F800001)
     assert m == 0, ex
 
@@ -41,6 +43,14 @@ def test_div6_exhaustive(lib):
 
 def test_div_core_random(lib):
     m, ex = run(lib, 2, 12345, 1 << 31)
+    assert m == 0, ex
+
+
+@pytest.mark.parametrize("d0", [0, 0x3A5F00, 0x7FFFC0])
+def test_div_core_significand_blocks(lib, d0):
+    # 64 denominator significands (incl. 1.0, and the all-ones fraction at 0x7FFFFF) x all 2^23
+    # numerator significands
+    m, ex = run(lib, 7, d0, 64 << 23)
     assert m == 0, ex
 
 

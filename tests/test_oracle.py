@@ -172,3 +172,19 @@ def test_srgb_encode_table_matches_definition_exhaustively():
         prev = np.nextafter(T[k], np.float32(0))
         assert lib.bho_srgb_encode(float(T[k])) == k and lib.bho_srgb_encode(float(prev)) == k - 1, k
     assert oracle.srgb_table_mismatches(T) == 0
+
+
+def test_exit_tests_on_r_squared_equal_tests_on_r():
+    # The kernel's blackout/outside tests (bh_march.hpp step_bf) read r2 = dot(ro, ro) instead of
+    # r = RN(sqrt(r2)) (src/black_hole_maybe.wgsl:271-283 compares r with 1):
+    #   r < 1 <=> r2 < 1   and   r > 1 <=> r2 > 1 + 2^-23.
+    # RN(sqrt) is monotone, so checking every float in [1/4, 4] (both sides of both thresholds)
+    # proves it for all r2; numpy's float32 sqrt is the correctly rounded IEEE sqrt.
+    lo, hi = np.float32(0.25).view(np.uint32), np.float32(4.0).view(np.uint32)
+    r2 = np.arange(lo, hi + 1, dtype=np.uint32).view(np.float32)
+    r = np.sqrt(r2)
+    assert r.dtype == np.float32
+    assert np.array_equal(r < 1.0, r2 < np.float32(1.0))
+    assert np.array_equal(r > 1.0, r2 > np.float32(1.0 + 2.0 ** -23))
+    for x in (np.float32(0.0), np.float32(np.inf), np.float32(np.nan)):
+        assert (np.sqrt(x) < 1.0) == (x < 1.0) and (np.sqrt(x) > 1.0) == (x > np.float32(1.0 + 2.0 ** -23))
