@@ -52,6 +52,30 @@ __device__ __forceinline__ v3 normalize(v3 a) { return divs(a, len(a)); }
 // normative pow forms (oracle/bh_oracle.c header): three correctly rounded f32 ops each
 __device__ __forceinline__ float pow25(float q) { return (q * q) * __builtin_sqrtf(q); }
 __device__ __forceinline__ float pow15(float c) { return c * __builtin_sqrtf(c); }
+
+// The per-ray set-up and shading ops on the cheap correctly rounded cores of bh_crmath.hpp (the same
+// bits as the IEEE forms above, proofs at each).
+//
+// normalize(v) = v / sqrt(dot(v, v)): exact when q = dot(v, v) is in [2^-80, 2^120] (inside the sqrt
+// core's domain, and then the length is in the division core's [2^-40, 2^60], which also bounds
+// every |v_i| <= 2^60) and every component is 0 or >= 2^-60 in magnitude.  Otherwise the lanes
+// concerned take the IEEE form (a wave-uniform branch; never seen on real frames).
+__device__ __forceinline__ v3 normalize_x(v3 v) {
+    const float q = dot(v, v);
+    const float l = crm::sqrt_core(q);
+    const crm::Rcp R = crm::rcp_refined(l);
+    const v3 n = mk(crm::div_core(v.x, R), crm::div_core(v.y, R), crm::div_core(v.z, R));
+    const bool bad = !(q >= 0x1p-80f && q <= 0x1p120f) |
+                     (crm::kmin3(crm::key(v.x), crm::key(v.y), crm::key(v.z)) < crm::KEY_MIN);
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0ull, 0)) {
+        if (bad) return normalize(v);
+    }
+    return n;
+}
+// c * sqrt(c) for a bilinear sky sample c: c is +0 or in [2^-60, 1] (texels decode to 0 or
+// >= 3.0e-4, the bilinear weights are 0 or >= 2^-24: two weight products keep c >= 1.8e-18), so
+// the sqrt core is exact for every c > 0 and c = +0 gives +0 as c * sqrt(c) does.
+__device__ __forceinline__ float pow15_x(float c) { return c > 0.0f ? c * crm::sqrt_core(c) : c; }
 #endif
 
 constexpr float MIN_DIST = 0.001f;        // :80
@@ -158,13 +182,24 @@ __device__ __forceinline__ Frame make_frame(const MarchArgs& a) {
 
 // vs_main + rasteriser interpolation + fs_main :362 for pixel (px, py): the world-space corner rays of
 // the screen triangle (3,1),(-1,1),(-1,-3) interpolated at the pixel centre, normalised.
+// Exact mode: the two divisions use the division core (numerators in [0.5, 2^32], denominators 2W,
+// 2H in [2, 2^33]: always inside its domain) and the normalisation normalize_x.
 __device__ __forceinline__ v3 pixel_ray(const MarchArgs& a, uint32_t px, uint32_t py) {
+#if BH_FAST
     const float l0 = ((float)px + 0.5f) / (2.0f * (float)a.width);
     const float l2 = ((float)py + 0.5f) / (2.0f * (float)a.height);
+#else
+    const float l0 = crm::div_core((float)px + 0.5f, crm::rcp_refined(2.0f * (float)a.width));
+    const float l2 = crm::div_core((float)py + 0.5f, crm::rcp_refined(2.0f * (float)a.height));
+#endif
     const float l1 = (1.0f - l0) - l2;
     const v3 d = add(add(smul(l0, mk(a.c0[0], a.c0[1], a.c0[2])), smul(l1, mk(a.c1[0], a.c1[1], a.c1[2]))),
                      smul(l2, mk(a.c2[0], a.c2[1], a.c2[2])));
+#if BH_FAST
     return normalize(d);
+#else
+    return normalize_x(d);
+#endif
 }
 
 // s = ((DP*RS)*-1.5) * h2 with h2 = |ro0 x rd0|^2 (:262-263), hoisted out of rd_derivative.
@@ -305,12 +340,18 @@ struct XOps {
         rho2 = p.x * p.x + p.z * p.z;
         const float rho = sqrt(rho2);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
+        // The four sphere arguments are q1,2 = (xx + (+-10 - y)^2) + zz and q3,4 = ((+-10 - x)^2 + yy)
+        // + zz.  Of each pair only the sphere on the point's side can be the minimum, and its
+        // argument is computed from t = RN(10 - |y|) (resp. |x|): RN(-10 - y) = -RN(10 + y) and
+        // |10 - y| <= 10 + y for y >= 0 (mirrored for y < 0), and every later op (square, sums) is
+        // monotone in |t|, so the rounded q of the near sphere is <= the far one's and equals
+        // (xx + t*t) + zz bit for bit.  min(q1..q4) == min(qy, qx): 11 ops instead of 20
+        // (tests/test_oracle.py::test_marker_pair_reduction checks the identity).
         const float xx = p.x * p.x, yy = p.y * p.y;
         const float dz = -10.0f - p.z, zz = dz * dz;
-        const float a1 = 10.0f - p.y, a2 = -10.0f - p.y, b3 = 10.0f - p.x, b4 = -10.0f - p.x;
-        const float q1 = (xx + a1 * a1) + zz, q2 = (xx + a2 * a2) + zz;
-        const float q3 = (b3 * b3 + yy) + zz, q4 = (b4 * b4 + yy) + zz;
-        qm = fminf(q1, fminf(q2, fminf(q3, q4)));
+        const float ty = 10.0f - fabsf(p.y), tx = 10.0f - fabsf(p.x);
+        const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
+        qm = fminf(qy, qx);
         const float m = sqrt(qm) - 0.5f;
         // fminf(disc, inf) == disc and fminf(inf, m) == m bit for bit: same result as selecting
         return fminf((flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
@@ -355,7 +396,11 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // guard on it.
     const bool bo_on = a.blackout_eh != 0u;
     const bool not_out = !(r2 > R2_GT1);                               // NaN: "else" branch, as the WGSL
-    const bool blackout = bo_on & (((r2 < 1.0f) & (dot(rd, ro) < 0.0f)) | (not_out & (in.outside != 0u)));
+    // rd.ro < 0 only matters for lanes inside r < 1 (the black hole's interior: rare), so the dot
+    // product is evaluated behind a wave-uniform test (-4 VALU per step; 1 % on the headline, A/B r01)
+    bool ingoing = false;
+    if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = dot(rd, ro) < 0.0f;
+    const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
     float rho2, qm;
     const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
     X.sq_args(rho2, qm);
@@ -436,7 +481,7 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
 #else
     XOps<true> X;
     bool done = step_bf<true, XOps<true>, SF>(a, f, in, out, X, fate);
-    const uint64_t badm = __ballot(X.bad);
+    const uint64_t badm = __builtin_amdgcn_ballot_w64(X.bad);
     if (__builtin_expect(badm != 0ull, 0)) {   // wave-uniform: rare IEEE re-run
 #ifdef BH_DIAG_SLOW
         if ((threadIdx.x & 63u) == 0u) {
@@ -482,7 +527,7 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
     bool d0 = step_bf<false>(a, f, s0, t0, X0, f0);
     bool d1 = step_bf<false>(a, f, s1, t1, X1, f1);
     const bool bad0 = X0.bad & alive0, bad1 = X1.bad & alive1;
-    if (__builtin_expect(__ballot(bad0 || bad1) != 0ull, 0)) {   // rare IEEE re-runs
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad0 | bad1) != 0ull, 0)) {   // rare IEEE re-runs
         if (bad0) { XOps<false> Y; d0 = step_bf<false>(a, f, s0, t0, Y, f0); }
         if (bad1) { XOps<false> Y; d1 = step_bf<false>(a, f, s1, t1, Y, f1); }
     }
@@ -505,21 +550,25 @@ __device__ __forceinline__ void march_step2(const MarchArgs& a, const Frame& f, 
 __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32_t fate, v3 rd) {
     if (fate == BH_FATE_BLACKOUT) return mk(0.0f, 0.0f, 0.0f);
     if (fate == BH_FATE_SURFACE) return mk(1.0f, 1.0f, 1.0f);
-    const v3 n = normalize(rd);                             // :330
 #if BH_FAST
+    const v3 n = normalize(rd);                             // :330
     const float az = atan2f(n.z, n.x);                      // :332
-#else
-    const float az = (float)atan2((double)n.z, (double)n.x);
-#endif
     const float x = (az + ONE_PI) / TWO_PI;                 // :334
+#else
+    const v3 n = normalize_x(rd);
+    const float az = (float)atan2((double)n.z, (double)n.x);
+    // az + pi is +0 or in [2^-22, 7] (az is an f32 in [-RN(pi), RN(pi)]): inside the division core's
+    // domain
+    const float x = crm::div_core(az + ONE_PI, crm::Rcp{TWO_PI, 1.0f / TWO_PI});  // RN(1/2pi) folded
+#endif
     const float y = (n.y + 1.0f) * 0.5f;                    // :336
     v3 col = sample_sky(a, lut, x, 1.0f - y);               // :341
 #if BH_FAST
     col.y = col.y * __builtin_sqrtf(col.y);                 // :342
     col.z = col.z * __builtin_sqrtf(col.z);                 // :343
 #else
-    col.y = pow15(col.y);
-    col.z = pow15(col.z);
+    col.y = pow15_x(col.y);
+    col.z = pow15_x(col.z);
 #endif
     return col;
 }
@@ -714,7 +763,7 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
         RayState sb = st;
         bool in_b = false, alive = true;
         static_assert(PRIO_ITERS % 2u == 0u, "ping-pong pairs");
-        for (uint32_t it = 0; it < PRIO_ITERS && __ballot(alive) != 0ull; it += 2u) {
+        for (uint32_t it = 0; it < PRIO_ITERS && __builtin_amdgcn_ballot_w64(alive) != 0ull; it += 2u) {
             if (alive) {
                 if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; in_b = !fate_before_rk(fate); }
             }

@@ -188,3 +188,34 @@ def test_exit_tests_on_r_squared_equal_tests_on_r():
     assert np.array_equal(r > 1.0, r2 > np.float32(1.0 + 2.0 ** -23))
     for x in (np.float32(0.0), np.float32(np.inf), np.float32(np.nan)):
         assert (np.sqrt(x) < 1.0) == (x < 1.0) and (np.sqrt(x) > 1.0) == (x > np.float32(1.0 + 2.0 ** -23))
+
+
+def test_marker_pair_reduction():
+    # bh_march.hpp XOps::sdf evaluates the marker term (src/black_hole_maybe.wgsl:107-117) as
+    # sqrt(min(qy, qx)) - 0.5 with qy = (x*x + t*t) + zz, t = RN(10 - |y|), qx = (u*u + y*y) + zz,
+    # u = RN(10 - |x|): only the sphere on the point's side of each pair can be nearest.  Checked
+    # bit for bit against the oracle's four-sphere min on random and adversarial points.
+    from oracle import oracle_np as onp
+    rng = np.random.default_rng(7)
+    f32 = np.float32
+    parts = [rng.normal(0, s, (200_000, 3)) for s in (1.0, 10.0, 30.0, 1e3)]
+    pts = np.concatenate(parts).astype(f32)
+    special = np.array([0.0, -0.0, 10.0, -10.0, 1e-30, -1e-30, 9.999999, -10.000001, 1e19, -1e19,
+                        np.inf, -np.inf, np.nan], dtype=f32)
+    grid = np.stack(np.meshgrid(special, special, special, indexing="ij"), -1).reshape(-1, 3)
+    near = (f32(10.0) + rng.integers(-3, 4, (100_000, 3)).astype(f32) * np.spacing(f32(10.0))).astype(f32)
+    near *= rng.choice(np.array([-1, 1], dtype=f32), near.shape)
+    pts = np.concatenate([pts, grid, near]).astype(f32)
+    px, py, pz = pts[:, 0], pts[:, 1], pts[:, 2]
+    with np.errstate(all="ignore"):
+        ref = onp._sdf(px, py, pz, f32(1.0), onp.SCENE_MARKERS)
+        xx, yy = px * px, py * py
+        dz = f32(-10.0) - pz
+        zz = dz * dz
+        t, u = f32(10.0) - np.abs(py), f32(10.0) - np.abs(px)
+        qm = np.fmin((xx + t * t) + zz, (u * u + yy) + zz)
+        got = np.sqrt(qm) - f32(0.5)
+    assert got.dtype == np.float32 and ref.dtype == np.float32
+    both_nan = np.isnan(got) & np.isnan(ref)
+    assert np.array_equal(got.view(np.uint32)[~both_nan], ref.view(np.uint32)[~both_nan])
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
