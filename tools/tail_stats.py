@@ -45,3 +45,7 @@ edges = [0, 16, 32, 64, 128, 256, 512, 768, 1000, 100000]
 h, _ = np.histogram(tmax, bins=edges)
 print("tiles by slowest ray's executed steps:", dict(zip([f"{a}-{b}" for a, b in zip(edges, edges[1:])], h.tolist())))
 print("top tile max steps:", np.sort(tmax.ravel())[-10:])
+ws = tmax.sum()
+print(f"wave-steps {ws} (mean {tmax.mean():.2f} per tile); beyond {48} iterations: {np.maximum(tmax - 48, 0).sum()} "
+      f"({np.maximum(tmax - 48, 0).sum() / ws:.1%}) in {(tmax > 48).sum()} tiles; lane-steps / (64 x wave-steps) = "
+      f"{s.sum() / (64 * ws):.3f}")
