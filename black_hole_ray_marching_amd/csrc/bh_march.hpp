@@ -231,15 +231,18 @@ struct FOps {
     bool bad = false;  // no guard in fast mode
     __device__ __forceinline__ float sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }  // raw v_sqrt_f32
     __device__ __forceinline__ float length(v3 p) { return __builtin_amdgcn_sqrtf(dot(p, p)); }
+    template <int K>
     __device__ __forceinline__ v3 div6(v3 x) { return muls(x, 1.0f / 6.0f); }
     __device__ __forceinline__ v3 add2(v3 a, v3 b) {  // a + 2b
         return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
     }
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float, bool = false) {
+    template <int K>
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
         const float iq = rsq(q), iq2 = iq * iq;
         return muls(p, s * (iq2 * iq2 * iq));
     }
-    __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs(p, s, dot(p, p), 0.0f); }
+    template <int K>
+    __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs<K>(p, s, dot(p, p), 0.0f); }
     __device__ __forceinline__ void sq_args(float, float) {}
     __device__ __forceinline__ void sq_arg(float) {}
     __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags, float&, float&) {
@@ -272,11 +275,21 @@ struct XOps {
     // min |n| (one v_min3_f32 with |.| modifiers per three values) and a zero just takes the IEEE
     // path; the x/6 check is waived when dt == 0.  (min |n| everywhere: measured 7 % slower, frozen
     // rays fell back at every step.)
-    uint32_t kmin = 0xFFFFFFFFu;
-    float amin = __builtin_inff();   // k2..k4 numerators
-    float amin6 = __builtin_inff();  // x/6 numerators
+    // Each accumulator is one running chain started by its first value (an explicit +inf start is
+    // not folded away, since fminf(inf, NaN) is not NaN), so consecutive values pair up into
+    // v_min3_f32: -5 VALU per step, 0.6 % (A/B r01).  (Pooling the denominators' range checks into
+    // one min/max over the squared lengths r^2, |ro - cps|^2 and the k-point dot products -- a range
+    // of q that implies Q's -- is 5 VALU fewer again but measured 12 % slower at cap 64 and 512 with
+    // the same IEEE re-run count: the compiler then interleaves k3's and k4's rsq/rcp chains; the
+    // max-ilp and iterative-ilp scheduling strategies did not recover it.)
+    uint32_t kmin;  // k1 numerators (keys)
+    float amin;     // k2..k4 numerators
+    float amin6;    // x/6 numerators
     __device__ __forceinline__ static float absmin3(float m, float x, float y, float z) {
-        return fminf(m, fminf(fabsf(x), fminf(fabsf(y), fabsf(z))));
+        return fminf(fminf(fminf(m, fabsf(x)), fabsf(y)), fabsf(z));
+    }
+    __device__ __forceinline__ static float absmin3(float x, float y, float z) {
+        return fminf(fminf(fabsf(x), fabsf(y)), fabsf(z));
     }
     // Square roots.  The core is exact for x in [SQRT_MIN, FLT_MAX]; outside that the caller must
     // raise `bad`.  Which check covers which root (one v_cmp per bound, so they are pooled):
@@ -297,9 +310,10 @@ struct XOps {
     __device__ __forceinline__ void sq_arg(float a) {
         if constexpr (CR) bad |= crm::sqrt_bad(a);
     }
+    template <int K>  // K = 0 for the first call of a step, 1 for the second
     __device__ __forceinline__ v3 div6(v3 x) {
         if constexpr (CR) {
-            amin6 = absmin3(amin6, x.x, x.y, x.z);
+            amin6 = (K == 0) ? absmin3(x.x, x.y, x.z) : absmin3(amin6, x.x, x.y, x.z);
             return mk(crm::div6(x.x), crm::div6(x.y), crm::div6(x.z));
         } else {
             return mk(x.x / 6.0f, x.y / 6.0f, x.z / 6.0f);
@@ -316,12 +330,15 @@ struct XOps {
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
     // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq, bool zeros = false) {
+    // K = 1..4: the RK stage (k1's numerators may be zeros, see above)
+    template <int K>
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq) {
         const float Q = (q * q) * sq;
         const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
         if constexpr (CR) {
             bad |= crm::div_d_bad(Q);
-            if (zeros) kmin = min(kmin, crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz)));
+            if constexpr (K == 1) kmin = crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz));
+            else if constexpr (K == 2) amin = absmin3(nx, ny, nz);
             else amin = absmin3(amin, nx, ny, nz);
             const crm::Rcp R = crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
@@ -329,9 +346,10 @@ struct XOps {
             return mk(nx / Q, ny / Q, nz / Q);
         }
     }
+    template <int K>
     __device__ __forceinline__ v3 accel(v3 p, float s) {
         const float q = dot(p, p);
-        return accel_qs(p, s, q, sqrt(q));
+        return accel_qs<K>(p, s, q, sqrt(q));
     }
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
@@ -423,15 +441,15 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
-    const v3 rd_k1 = smul(dt, X.accel_qs(ro, s, r2, r, true));
+    const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r));
     const v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
-    const v3 rd_k2 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k1)), s));
+    const v3 rd_k2 = smul(dt, X.template accel<2>(add(ro, smul(0.5f, ro_k1)), s));
     const v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
-    const v3 rd_k3 = smul(dt, X.accel(add(ro, smul(0.5f, ro_k2)), s));
+    const v3 rd_k3 = smul(dt, X.template accel<3>(add(ro, smul(0.5f, ro_k2)), s));
     const v3 ro_k4 = smul(dt, add(rd, rd_k3));
-    const v3 rd_k4 = smul(dt, X.accel(add(ro, ro_k3), s));
-    const v3 dro = X.div6(add(X.add2(X.add2(ro_k1, ro_k2), ro_k3), ro_k4));
-    const v3 drd = X.div6(add(X.add2(X.add2(rd_k1, rd_k2), rd_k3), rd_k4));
+    const v3 rd_k4 = smul(dt, X.template accel<4>(add(ro, ro_k3), s));
+    const v3 dro = X.template div6<0>(add(X.add2(X.add2(ro_k1, ro_k2), ro_k3), ro_k4));
+    const v3 drd = X.template div6<1>(add(X.add2(X.add2(rd_k1, rd_k2), rd_k3), rd_k4));
 #if !BH_FAST
     if constexpr (Ops::kCR) {
         // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
@@ -765,13 +783,19 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
         // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
         RayState sb = st;
         bool in_b = false, alive = true;
-        static_assert(PRIO_ITERS % 2u == 0u, "ping-pong pairs");
-        for (uint32_t it = 0; it < PRIO_ITERS && __builtin_amdgcn_ballot_w64(alive) != 0ull; it += 2u) {
-            if (alive) {
-                if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; in_b = !fate_before_rk(fate); }
-            }
-            if (alive) {
-                if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; in_b = fate_before_rk(fate); }
+        // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
+        // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
+        constexpr uint32_t TRIP_PAIRS = 3;
+        static_assert(PRIO_ITERS % (2u * TRIP_PAIRS) == 0u, "whole trips");
+        for (uint32_t it = 0; it < PRIO_ITERS && __builtin_amdgcn_ballot_w64(alive) != 0ull; it += 2u * TRIP_PAIRS) {
+#pragma unroll
+            for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
+                if (alive) {
+                    if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; in_b = !fate_before_rk(fate); }
+                }
+                if (alive) {
+                    if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; in_b = fate_before_rk(fate); }
+                }
             }
         }
         if (in_b) st = sb;
