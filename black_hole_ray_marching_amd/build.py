@@ -27,8 +27,11 @@ HIPCC = os.environ.get("HIPCC", shutil.which("hipcc") or "/opt/rocm/bin/hipcc")
 COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
 # per-translation-unit floating-point contracts (DESIGN.md "Math modes")
 TU_FLAGS = {
-    # packed FP32 has no throughput advantage on gfx950 (tools/ubench/valu_rates.hip): no SLP packing
-    "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
+    # packed FP32 has no throughput advantage on gfx950 (tools/ubench/valu_rates.hip): no SLP packing.
+    # No machine scheduling (pre- or post-RA): the step's source order issues faster than the
+    # scheduler's interleavings (0.687 -> 0.644 ms headline, A/B r01).
+    "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
+                           "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
     "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
     "bh_tiles.hip": [],
     "bh_bloom.hip": ["-ffp-contract=off"],
