@@ -43,6 +43,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=300)
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
     p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
+    p.add_argument("--variant", choices=["auto", "issue", "latency"], default="auto",
+                   help="exact math: build of the march kernels (auto: per frame, include/bh_render.h)")
     p.add_argument("--fmt", choices=["rgba16f", "rgba32f", "bgra8"], default="rgba16f")
     p.add_argument("--width", type=int, default=0)
     p.add_argument("--height", type=int, default=0)
@@ -99,6 +101,7 @@ def main() -> None:
     math_mode = bh.BH_MATH_EXACT if args.math == "exact" else bh.BH_MATH_FAST
     sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
              "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
+    sched |= {"auto": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[args.variant]
 
     sky = bh.synthetic_sky(4096, 2048)
     flags = bh.BH_SCENE_DEFAULT if args.surfaces == "on" else 0

@@ -6,7 +6,7 @@ include/bh_render.h); this package is the host-side mirror of the reference's Sc
 """
 from ._abi import (BH_BLOOM_AUTO, BH_BLOOM_LITERAL, BH_FATE_BLACKOUT, BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_LAYOUT_ROWMAJOR,
                    BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_BGRA8_SRGB, BH_OUT_RGBA16F,
-                   BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BH_SCHED_FLAG_STATIC_ORDER, BH_SCHED_PAIR, BH_SCHED_PERSISTENT, BH_SCHED_TILE,
+                   BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BH_SCHED_FLAG_STATIC_ORDER, BH_SCHED_FLAG_ISSUE_ORDER, BH_SCHED_FLAG_LATENCY, BH_SCHED_PAIR, BH_SCHED_PERSISTENT, BH_SCHED_TILE,
                    BYTES_PER_PIXEL,
                    BhError, load)
 from .scene import (MAX_ITERATIONS, Camera, CameraController, CameraUniform, Scene, Uniforms, load_sky, shard_tile_count,

@@ -22,6 +22,8 @@ BH_SCENE_DEFAULT = 3
 BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB = 0, 1, 2
 BH_SCHED_TILE, BH_SCHED_PAIR, BH_SCHED_PERSISTENT = 0, 1, 2
 BH_SCHED_FLAG_STATIC_ORDER = 0x100
+BH_SCHED_FLAG_ISSUE_ORDER = 0x200   # exact math: force the source-order build of the kernels
+BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled build
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 

@@ -32,6 +32,8 @@ TU_FLAGS = {
     # scheduler's interleavings (0.687 -> 0.644 ms headline, A/B r01).
     "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
                            "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
+    # the same kernels WITH machine scheduling: shorter per-step latency for tail-bound frames
+    "bh_march_exact_lat.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
     "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
     "bh_tiles.hip": [],
     "bh_bloom.hip": ["-ffp-contract=off"],
@@ -60,7 +62,8 @@ def build_product(force: bool = False) -> Path:
     for src, flags in TU_FLAGS.items():
         s = CSRC / src
         o = OBJ / (s.stem + ".o")
-        if force or _stale(o, [s, *headers, Path(__file__)]):
+        deps = [s, *headers, Path(__file__)] + ([CSRC / "bh_march_exact.hip"] if src == "bh_march_exact_lat.hip" else [])
+        if force or _stale(o, deps):
             _run([HIPCC, *COMMON, *flags, "-c", str(s), "-o", str(o)])
         objs.append(o)
     if force or _stale(LIB, objs):

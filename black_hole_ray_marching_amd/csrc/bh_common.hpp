@@ -152,6 +152,9 @@ __host__ __device__ inline uint32_t cost_bucket(uint32_t c) {
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
                                                                          uint32_t* counters, uint32_t grid,
                                                                          hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact_lat(const bh::MarchArgs& a, uint32_t schedule,
+                                                                             uint32_t* counters, uint32_t grid,
+                                                                             hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_fast(const bh::MarchArgs& a, uint32_t schedule,
                                                                         uint32_t* counters, uint32_t grid,
                                                                         hipStream_t s);

@@ -24,6 +24,7 @@ struct bh_ctx {
     uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
+    uint32_t cus = 0;                        // compute units of the device
     // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order
     uint8_t* tile_cost = nullptr;
     uint32_t* order = nullptr;
@@ -416,6 +417,7 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
         if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess || cus <= 0) {
             st = hip_fail(e, "hipDeviceGetAttribute(CU count)");
         } else {
+            c->cus = (uint32_t)cus;
             c->grid_exact = (uint32_t)(cus * bh_march_blocks_per_cu_exact());
             c->grid_fast = (uint32_t)(cus * bh_march_blocks_per_cu_fast());
         }
@@ -598,13 +600,25 @@ int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_inde
     return (int64_t)bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, shard_index, shard_count);
 }
 
+// Which build of the exact kernels runs a frame (BH_SCHED_FLAG_ISSUE_ORDER / _LATENCY force one).  The
+// source-order build issues the bulk of the steps faster (headline 0.644 vs 0.687 ms), the machine-
+// scheduled one runs a lone wave's serial step chain faster (cap 1000: 0.82 vs 0.95 ms; 1920x1080:
+// 0.216 vs 0.253 ms).  A frame is throughput-bound when every CU has many tiles to issue while the
+// few capped waves march (>= 256 tiles per CU) and the cap keeps those waves' chains shorter than the
+// bulk (max_iters <= 512): A/B r01, DESIGN.md §5 item 8.
+static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles, uint32_t cus) {
+    if (d->schedule & BH_SCHED_FLAG_ISSUE_ORDER) return true;
+    if (d->schedule & BH_SCHED_FLAG_LATENCY) return false;
+    return d->max_iters <= 512u && (uint64_t)n_tiles >= 256ull * (cus ? cus : 256u);
+}
+
 int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, const bh_render_desc* d,
               void* stream) {
     if (!c || !cam || !U || !d || !d->out_col) return BH_ERR_INVALID_ARG;
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
     if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGB) return BH_ERR_INVALID_ARG;
-    if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER))) return BH_ERR_INVALID_ARG;
+    if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER | BH_SCHED_FLAG_ISSUE_ORDER | BH_SCHED_FLAG_LATENCY))) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
@@ -680,8 +694,10 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
         a.tile_cost = c->tile_cost;
         a.order_tot = c->order_counters;
     }
-    int e = d->math == BH_MATH_EXACT ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
-                                     : bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s);
+    int e = d->math != BH_MATH_EXACT ? bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s)
+            : march_variant_issue_order(d, a.n_tiles, c->cus)
+                ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
+                : bh_launch_march_exact_lat(a, sched, c->counters, c->grid_exact, s);
     if (prev != c->device) (void)hipSetDevice(prev);
     if (e != 0) {
         // the costs and their histogram are written together by the march kernel; without it they

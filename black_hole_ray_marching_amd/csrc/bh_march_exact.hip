@@ -1,7 +1,19 @@
 // Exact (parity) instantiation of the march kernel.  Built with -ffp-contract=off and the default
 // correctly-rounded f32 division/sqrt: same op sequence as oracle/bh_oracle.c (bit-exact parity).
+//
+// Two builds of this file (same source, same arithmetic, different instruction schedules; build.py):
+//   bh_march_exact.hip      namespace exact      no machine scheduling: the step in source order, the
+//                                                faster issue stream for throughput-bound frames;
+//   bh_march_exact_lat.hip  namespace exact_lat  LLVM's machine schedulers: interleaved chains, the
+//                                                shorter latency per step of a lone tail wave.
+// bh_render picks one per frame (bh_host.cpp, march_variant).
 #define BH_FAST 0
+#ifndef BH_NS
 #define BH_NS exact
+#define BH_EXACT_LAUNCH bh_launch_march_exact
+#define BH_EXACT_BLOCKS bh_march_blocks_per_cu_exact
+#define BH_EXACT_AUX 1
+#endif
 #include "bh_march.hpp"
 
 namespace {
@@ -10,22 +22,22 @@ int launch(const bh::MarchArgs& a, uint32_t schedule, uint32_t* counters, uint32
     if (schedule == BH_SCHED_TILE) {
         const uint32_t blocks = (a.n_tiles + 3u) / 4u;
         if (a.scene_flags == BH_SCENE_DEFAULT)  // the reference's scene: flags folded at compile time
-            hipLaunchKernelGGL((bh::exact::march_tile_kernel<FMT, BH_SCENE_DEFAULT>), dim3(blocks), dim3(256), 0, s, a);
+            hipLaunchKernelGGL((bh::BH_NS::march_tile_kernel<FMT, BH_SCENE_DEFAULT>), dim3(blocks), dim3(256), 0, s, a);
         else
-            hipLaunchKernelGGL((bh::exact::march_tile_kernel<FMT, bh::exact::SF_DYN>), dim3(blocks), dim3(256), 0, s, a);
+            hipLaunchKernelGGL((bh::BH_NS::march_tile_kernel<FMT, bh::BH_NS::SF_DYN>), dim3(blocks), dim3(256), 0, s, a);
     } else if (schedule == BH_SCHED_PAIR) {
         const uint32_t pairs = (a.n_tiles + 1u) / 2u;
-        hipLaunchKernelGGL(bh::exact::march_pair_kernel<FMT>, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(bh::BH_NS::march_pair_kernel<FMT>, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
     } else {
-        hipError_t e = hipMemsetAsync(counters, 0, bh::exact::NQ * bh::exact::CTR_STRIDE * sizeof(uint32_t), s);
+        hipError_t e = hipMemsetAsync(counters, 0, bh::BH_NS::NQ * bh::BH_NS::CTR_STRIDE * sizeof(uint32_t), s);
         if (e != hipSuccess) return (int)e;
-        hipLaunchKernelGGL(bh::exact::march_persistent_kernel<FMT>, dim3(grid), dim3(256), 0, s, a, counters);
+        hipLaunchKernelGGL(bh::BH_NS::march_persistent_kernel<FMT>, dim3(grid), dim3(256), 0, s, a, counters);
     }
     return (int)hipGetLastError();
 }
 }  // namespace
 
-extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const bh::MarchArgs& a, uint32_t schedule,
+extern "C" __attribute__((visibility("hidden"))) int BH_EXACT_LAUNCH(const bh::MarchArgs& a, uint32_t schedule,
                                                                              uint32_t* counters, uint32_t grid,
                                                                              hipStream_t s) {
     switch (a.format) {
@@ -36,20 +48,20 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_march_exact(const
 }
 
 // Resident 256-thread blocks per CU of the persistent kernel (sizes its grid: every block resident).
-extern "C" __attribute__((visibility("hidden"))) int bh_march_blocks_per_cu_exact(void) {
+extern "C" __attribute__((visibility("hidden"))) int BH_EXACT_BLOCKS(void) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::exact::march_persistent_kernel<BH_OUT_BGRA8_SRGB>, 256, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bh::BH_NS::march_persistent_kernel<BH_OUT_BGRA8_SRGB>, 256, 0) != hipSuccess) return 1;
     return n > 0 ? n : 1;
 }
 
-#ifdef BH_DIAG_SLOW
+#if defined(BH_DIAG_SLOW) && defined(BH_EXACT_AUX)
 // diagnostics build only: read and reset the fallback counters
 extern "C" int bh_diag_slow_counts(uint32_t* lane_steps, uint32_t* wave_steps) {
     uint32_t z = 0;
-    if (hipMemcpyFromSymbol(lane_steps, HIP_SYMBOL(bh::exact::g_diag_slow_lane_steps), 4) != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(wave_steps, HIP_SYMBOL(bh::exact::g_diag_slow_wave_steps), 4) != hipSuccess) return -1;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::exact::g_diag_slow_lane_steps), &z, 4);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::exact::g_diag_slow_wave_steps), &z, 4);
+    if (hipMemcpyFromSymbol(lane_steps, HIP_SYMBOL(bh::BH_NS::g_diag_slow_lane_steps), 4) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(wave_steps, HIP_SYMBOL(bh::BH_NS::g_diag_slow_wave_steps), 4) != hipSuccess) return -1;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_slow_lane_steps), &z, 4);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_slow_wave_steps), &z, 4);
     return 0;
 }
 #endif

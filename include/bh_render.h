@@ -129,6 +129,12 @@ typedef enum {
 } bh_schedule;
 /* OR into `schedule` to use the static centre-out order only (no per-tile cost feedback). */
 #define BH_SCHED_FLAG_STATIC_ORDER 0x100u
+/* Exact math: which build of the march kernels runs (same bits either way).  By default bh_render
+ * picks per frame: the source-order build when the frame is throughput-bound (>= 256 tiles per CU
+ * and max_iters <= 512), else the machine-scheduled build, whose lone tail waves step faster.
+ * These flags force one (BH_SCHED_FLAG_ISSUE_ORDER wins if both are set). */
+#define BH_SCHED_FLAG_ISSUE_ORDER 0x200u
+#define BH_SCHED_FLAG_LATENCY 0x400u
 
 /* Per-pixel fate codes written to dbg_fate. */
 #define BH_FATE_CAP      0u  /* loop ran out (max_iters); still shades sky with its current rd */

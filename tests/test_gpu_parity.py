@@ -101,7 +101,13 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+# every schedule, and both builds of the exact kernels (source order / machine-scheduled; the small
+# test frames pick the latter by default)
+SCHEDULES = [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_ISSUE_ORDER,
+             bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_LATENCY, bh.BH_SCHED_PERSISTENT | bh.BH_SCHED_FLAG_ISSUE_ORDER]
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("cam,W,H,cap,flags,over", CASES)
 def test_exact_bitexact(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over, schedule):
     cu, U = camera_uniform(cam, W, H), uniforms(**over)
@@ -146,7 +152,7 @@ def test_blackout_target_none(torch_cuda, scene_small, sky_small):
     assert np.array_equal(g[0].view(np.uint32), o[0].view(np.uint32))
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("S", [1, 2, 3, 5, 8])
 def test_tiles_shards_unpack(torch_cuda, scene_small, S, schedule):
     torch = torch_cuda
@@ -261,7 +267,7 @@ def test_invalid_arguments_fail_loudly(torch_cuda, scene_small):
 GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("cam*.npz"))
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
 def test_exact_matches_golden_fixtures(torch_cuda, path, schedule):
     torch = torch_cuda
@@ -381,7 +387,7 @@ def _bgra8_expected(col_f32):
     return out
 
 
-@pytest.mark.parametrize("schedule", [bh.BH_SCHED_PAIR, bh.BH_SCHED_TILE, bh.BH_SCHED_PERSISTENT])
+@pytest.mark.parametrize("schedule", SCHEDULES)
 @pytest.mark.parametrize("cam", ["A", "D"])
 def test_bgra8_srgb_output_is_encoded_exact_result(torch_cuda, sky_small, cam, schedule):
     """BH_OUT_BGRA8_SRGB (the reference's Bgra8UnormSrgb targets): every byte equals the normative
