@@ -36,7 +36,8 @@ TU_FLAGS = {
     "bh_march_exact_lat.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
     "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
     "bh_tiles.hip": [],
-    "bh_bloom.hip": ["-ffp-contract=off"],
+    # post-RA scheduling off: fused bloom chain 0.556 -> 0.548 ms (A/B r01; pre-RA off too: 0.561)
+    "bh_bloom.hip": ["-ffp-contract=off", "-mllvm", "-enable-post-misched=0"],
     "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
 }
