@@ -34,7 +34,9 @@ TU_FLAGS = {
                            "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
     # the same kernels WITH machine scheduling: shorter per-step latency for tail-bound frames
     "bh_march_exact_lat.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
-    "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt"],
+    # the fast (tolerance) kernels: no machine scheduling either (0.468 -> 0.440 ms headline, A/B r01)
+    "bh_march_fast.hip": ["-ffp-contract=fast", "-fno-hip-fp32-correctly-rounded-divide-sqrt",
+                          "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
     "bh_tiles.hip": [],
     # post-RA scheduling off: fused bloom chain 0.556 -> 0.548 ms (A/B r01; pre-RA off too: 0.561)
     "bh_bloom.hip": ["-ffp-contract=off", "-mllvm", "-enable-post-misched=0"],
