@@ -86,6 +86,8 @@ SIGNATURES = {
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
     "bh_tiles_unpack_rgb": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                       C.c_uint64, C.c_uint32, C.c_void_p]),
+    "bh_tiles_unpack_rgb_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
     "bh_controller_update": (C.c_int, [C.POINTER(bh_controller), C.POINTER(bh_camera), C.c_float, C.c_int,
                                        C.POINTER(C.c_int)]),

@@ -166,7 +166,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
                                                                          hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,
                                                                               uint32_t height, uint32_t shard_count,
-                                                                              uint64_t stride_tiles, uint32_t format,
+                                                                              uint64_t stride_tiles, uint32_t format, uint32_t rows_in_flight,
                                                                               hipStream_t s);
 // base codes of the table form of the sRGB encoder (bh_srgb.hpp), built from its 257 thresholds
 extern "C" __attribute__((visibility("hidden"))) void bh_srgb_bucket_table(const float* T257, uint8_t* B);

@@ -721,17 +721,22 @@ int bh_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t heig
     return BH_OK;
 }
 
-int bh_tiles_unpack_rgb(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
-                        uint64_t shard_stride_tiles, uint32_t format, void* stream) {
+int bh_tiles_unpack_rgb_rows(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
+                             uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight, void* stream) {
     if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
     if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
             return BH_ERR_INVALID_ARG;
     int e = bh_launch_tiles_unpack_rgb(packed, out, width, height, shard_count, shard_stride_tiles, format,
-                                       reinterpret_cast<hipStream_t>(stream));
+                                       rows_in_flight, reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
     return BH_OK;
+}
+
+int bh_tiles_unpack_rgb(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
+                        uint64_t shard_stride_tiles, uint32_t format, void* stream) {
+    return bh_tiles_unpack_rgb_rows(packed, out, width, height, shard_count, shard_stride_tiles, format, 0u, stream);
 }
 
 }  // extern "C"

@@ -33,7 +33,10 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
     __shared__ uint32_t lds[UNPACK_SPAN * TW];
     __shared__ uint64_t gsrc[UNPACK_SPAN];  // packed tile of each output tile of the span
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-    const uint32_t tx0 = blockIdx.x * UNPACK_SPAN, ty = blockIdx.y;
+    const uint32_t tx0 = blockIdx.x * UNPACK_SPAN;
+    const uint32_t tiles_y = (u.height + 7u) / 8u;
+    for (uint32_t ty = blockIdx.y; ty < tiles_y; ty += gridDim.y) {  // grid-stride over tile rows
+    __syncthreads();  // the previous row's LDS reads are done
     if (threadIdx.x < UNPACK_SPAN && tx0 + threadIdx.x < u.tiles_x) {
         uint32_t k;
         const uint32_t t = shard_tile_index(tx0 + threadIdx.x, ty, u.tiles_x, u.shard_count, &k);
@@ -49,7 +52,7 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
     }
     __syncthreads();
     const uint32_t x = threadIdx.x, px = tx0 * 8u + x;
-    if (px >= u.width) return;
+    if (px >= u.width) continue;  // no barrier below: lanes past the frame just skip the stores
     const uint32_t* tile = lds + (x >> 3) * TW;
     for (uint32_t r = 0; r < 8u; ++r) {
         const uint32_t py = ty * 8u + r;
@@ -70,6 +73,7 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
             v = c[e] | ((uint32_t)c[64 + e] << 8) | ((uint32_t)c[128 + e] << 16) | 0xFF000000u;
         }
         reinterpret_cast<P*>(out)[(size_t)py * u.width + px] = v;
+    }
     }
 }
 
@@ -164,18 +168,21 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
 }
 
 static void unpack_launch_shape(uint32_t width, uint32_t height, uint32_t shard_count, uint64_t stride_tiles,
-                                bh::UnpackGrid* u, dim3* grid) {
+                                uint32_t rows_in_flight, bh::UnpackGrid* u, dim3* grid) {
     u->width = width; u->height = height; u->tiles_x = (width + 7u) / 8u; u->shard_count = shard_count;
     u->stride_tiles = stride_tiles;
-    *grid = dim3((u->tiles_x + bh::UNPACK_SPAN - 1u) / bh::UNPACK_SPAN, (height + 7u) / 8u);
+    const uint32_t tiles_y = (height + 7u) / 8u;
+    // rows_in_flight tile rows per grid pass (0: all), the kernel grid-strides over the rest
+    *grid = dim3((u->tiles_x + bh::UNPACK_SPAN - 1u) / bh::UNPACK_SPAN,
+                 rows_in_flight && rows_in_flight < tiles_y ? rows_in_flight : tiles_y);
 }
 
 template <bool PLANAR>
 static int unpack_launch(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
-                         uint64_t stride_tiles, uint32_t bpp, hipStream_t s) {
+                         uint64_t stride_tiles, uint32_t bpp, uint32_t rows_in_flight, hipStream_t s) {
     bh::UnpackGrid u;
     dim3 grid, block(256);
-    unpack_launch_shape(width, height, shard_count, stride_tiles, &u, &grid);
+    unpack_launch_shape(width, height, shard_count, stride_tiles, rows_in_flight, &u, &grid);
     const uint32_t* p = static_cast<const uint32_t*>(packed);
     switch (bpp) {
         case 16: hipLaunchKernelGGL((bh::tiles_unpack_kernel<16, PLANAR>), grid, block, 0, s, p, out, u); break;
@@ -189,13 +196,13 @@ static int unpack_launch(const void* packed, void* out, uint32_t width, uint32_t
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
                                       uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp,
                                       hipStream_t s) {
-    return unpack_launch<false>(packed, out, width, height, shard_count, stride_tiles, bpp, s);
+    return unpack_launch<false>(packed, out, width, height, shard_count, stride_tiles, bpp, 0u, s);
 }
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,
                                                                               uint32_t height, uint32_t shard_count,
                                                                               uint64_t stride_tiles, uint32_t format,
-                                                                              hipStream_t s) {
+                                                                              uint32_t rows_in_flight, hipStream_t s) {
     const uint32_t bpp = format == BH_OUT_RGBA32F ? 16u : format == BH_OUT_RGBA16F ? 8u : format == BH_OUT_BGRA8_SRGB ? 4u : 0u;
-    return unpack_launch<true>(packed, out, width, height, shard_count, stride_tiles, bpp, s);
+    return unpack_launch<true>(packed, out, width, height, shard_count, stride_tiles, bpp, rows_in_flight, s);
 }

@@ -321,10 +321,16 @@ def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_s
 
 
 def tiles_unpack_rgb(packed, out, width: int, height: int, shard_count: int, shard_stride_tiles: int,
-                     fmt: int, stream=None) -> None:
-    """bh_tiles_unpack_rgb: gathered BH_LAYOUT_TILES_RGB shards of format `fmt` -> row-major frame."""
-    check(load().bh_tiles_unpack_rgb(_ptr(packed), _ptr(out), width, height, shard_count, shard_stride_tiles,
-                                     fmt, _stream_handle(stream)), "bh_tiles_unpack_rgb")
+                     fmt: int, stream=None, rows_in_flight: int = 0) -> None:
+    """bh_tiles_unpack_rgb(_rows): gathered BH_LAYOUT_TILES_RGB shards of format `fmt` -> row-major
+    frame; rows_in_flight > 0 throttles it for overlap with a render (include/bh_render.h)."""
+    if rows_in_flight:
+        check(load().bh_tiles_unpack_rgb_rows(_ptr(packed), _ptr(out), width, height, shard_count,
+                                              shard_stride_tiles, fmt, rows_in_flight, _stream_handle(stream)),
+              "bh_tiles_unpack_rgb_rows")
+    else:
+        check(load().bh_tiles_unpack_rgb(_ptr(packed), _ptr(out), width, height, shard_count, shard_stride_tiles,
+                                         fmt, _stream_handle(stream)), "bh_tiles_unpack_rgb")
 
 
 __all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",

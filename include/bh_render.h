@@ -241,6 +241,15 @@ int bh_tiles_unpack_rgb(const void* packed, void* out_rowmajor, uint32_t width, 
                         uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
                         void* hip_stream);
 
+/* As bh_tiles_unpack_rgb with at most `rows_in_flight` 8-pixel tile rows of the frame in flight at
+ * once (0 = all; the kernel grid-strides over the rest).  For an unpack that overlaps a render on
+ * the same GPU (rank 0 of the multi-GPU pipeline): a small value (16) keeps it from displacing the
+ * render's waves -- slower alone, but rank 0's render + unpack frame measured 0.78 -> 0.73 ms at
+ * the N=8 frame. */
+int bh_tiles_unpack_rgb_rows(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
+                             uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
+                             uint32_t rows_in_flight, void* hip_stream);
+
 /* The BGRA8 sRGB encoder's threshold table: out[k] (k = 1..255) = the smallest float x with
  * encode(x) >= k, out[0] = 0, out[256] = +inf; encode(x) = the largest k with x >= out[k]. */
 int bh_srgb_encode_table(float* out257);

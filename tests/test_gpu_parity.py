@@ -210,10 +210,13 @@ def test_tiles_rgb_shards_unpack(torch_cuda, scene_small, S, fmt):
             want = px.cpu().numpy().copy()
             want[..., 3] = alpha
             assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
-    out = torch.zeros((H, W, 4), dtype=dt, device="cuda")
-    bh.tiles_unpack_rgb(planes, out, W, H, S, stride, fmt)
-    torch.cuda.synchronize()
-    assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8))
+    # all tile rows at once, and throttled to 2 rows in flight (bh_tiles_unpack_rgb_rows: the
+    # kernel grid-strides over the 7 tile rows)
+    for rows in (0, 2):
+        out = torch.zeros((H, W, 4), dtype=dt, device="cuda")
+        bh.tiles_unpack_rgb(planes, out, W, H, S, stride, fmt, rows_in_flight=rows)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.uint8), ref.view(torch.uint8)), f"rows_in_flight={rows}"
 
 
 def test_headline_rows_bitexact_and_fast(torch_cuda):

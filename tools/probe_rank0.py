@@ -23,14 +23,22 @@ def main():
     bo = torch.empty_like(col)
     gathered = torch.zeros((n * stride, 3, 64), dtype=torch.float16, device=dev)
     frame = torch.empty((H, W, 4), dtype=torch.float16, device=dev)
-    rs, ss = torch.cuda.current_stream(), torch.cuda.Stream()
+    # BH_RENDER_PRIO=1: the render stream at high priority (the unpack stream stays at the default)
+    import os
+    hi = os.environ.get("BH_RENDER_PRIO") == "1"
+    rs = torch.cuda.Stream(priority=-1) if hi else torch.cuda.current_stream()
+    ss = torch.cuda.Stream()
+    # BH_UNPACK_ROWS=k: the unpack's tile rows in flight (bh_tiles_unpack_rgb_rows; 0 = all)
+    rows = int(os.environ.get("BH_UNPACK_ROWS", "0"))
+    # BH_VARIANT=issue|latency: force a build of the exact kernels (default: bh_render's choice)
+    sched = {"": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[os.environ.get("BH_VARIANT", "")]
 
     def render():
         scene.render(col, bo, fmt=bh.BH_OUT_RGBA16F, layout=bh.BH_LAYOUT_TILES_RGB, shard_index=0, shard_count=n,
-                     stream=rs)
+                     stream=rs, schedule=sched)
 
     def unpack():
-        bh.tiles_unpack_rgb(gathered, frame, W, H, n, stride, bh.BH_OUT_RGBA16F, stream=ss)
+        bh.tiles_unpack_rgb(gathered, frame, W, H, n, stride, bh.BH_OUT_RGBA16F, stream=ss, rows_in_flight=rows)
 
     def run(k, with_unpack, unpack_only=False):
         torch.cuda.synchronize()
@@ -46,7 +54,7 @@ def main():
 
     for _ in range(2):
         run(5, True)
-    out = {"n": n, "frame": f"{W}x{H}", "tiles": nt,
+    out = {"n": n, "frame": f"{W}x{H}", "tiles": nt, "render_prio_high": hi, "variant": os.environ.get("BH_VARIANT", "auto"), "unpack_rows_in_flight": rows,
            "render_ms": round(run(50, False), 4), "render_plus_unpack_ms": round(run(50, True), 4),
            "unpack_only_ms": round(run(50, True, True), 4)}
     print(json.dumps(out))
