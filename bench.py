@@ -4,22 +4,33 @@
 restatement, oracle/bh_oracle.c).
 
 A "step" is one frame: one pass of the hot path (Scene::render -> the HIP march kernel) over the
-synthetic 4096x2048 frame, the sky already resident in HBM.  Default arithmetic: BH_MATH_EXACT, the
-bit-exact path (the only one that can meet |delta| < 1e-4, DESIGN.md "Math modes"); RGBA16F col +
-blackout targets as north_star asks.
+synthetic frame, the sky already resident in HBM.  Default arithmetic: BH_MATH_EXACT, the bit-exact
+path (the only one that can meet |delta| < 1e-4); RGBA16F col + blackout targets as
+north_star asks.
 
-N=1: one GPU renders the whole frame.  N>1 (torch.distributed, one process per GPU, RCCL): weak
-scaling, the frame grows with N (~8.4 Mpix per GPU, aspect 2:1: 8192x4096 at N=4), each rank renders
-its (tx + 3*ty) % N share of 8x8 tiles, the tile-packed `col` shares (RGB planes: alpha is always 1
-and not shipped) are gathered to rank 0 in one collective and unpacked there; each timed step includes render, gather and unpack.
+Workloads (--workload):
+  strong   (default) north_star's fixed 4096x2048 frame, split over the N GPUs (strong scaling; at
+           N=1 this is the headline, BASELINE configs[2]);
+  config4  BASELINE configs[3]: the fixed 8192x4096 frame split over the N GPUs (8 in the config);
+  weak     ~8.4 Mpix per GPU at aspect 2:1 (the frame grows with N).
+N>1: one process per GPU (torch.distributed, RCCL).  Each rank renders its (tx + 3*ty) % N share of
+8x8 tiles in BH_LAYOUT_TILES_RGBM (RGB planes + the blackout mask word: 6.125 B per RGBA16F pixel),
+the shards are gathered to rank 0 (one collective per frame, overlapped with the next frame's
+render), and rank 0 unpacks BOTH targets, col and blackout_col, row-major.  Every timed step
+includes render, gather and unpack.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload strong|config4|weak]
+
+Without torchrun, `--gpus N` (N > 1) starts its own N ranks (child processes, before anything
+touches a GPU) and exits non-zero unless all N ranks finish; the ranks never fall back to fewer GPUs.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -34,16 +45,19 @@ F_STEP = {3: 209, 0: 159}  # flop-equivalents per completed RK step (surfaces on
 PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
-
-# tile rows in flight of rank 0's unpack (bh_tiles_unpack_rgb_rows)
+# tile rows in flight of rank 0's unpack (bh_tiles_unpack_rgbm rows_in_flight)
 UNPACK_ROWS_IN_FLIGHT = 16
 
-def parse():
+WORKLOADS = {"strong": (4096, 2048), "config4": (8192, 4096)}
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)   # SURVEY §8d timing protocol: 100 timed frames
-    # SURVEY §8d asks for 10 warm-up frames; 300 (0.25 s) let the clocks settle: +1 % measured
+    # SURVEY §8d asks for 10 warm-up frames; 300 (0.25 s) let the clocks settle
     p.add_argument("--warmup", type=int, default=300)
+    p.add_argument("--workload", choices=["strong", "config4", "weak"], default="strong")
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
     p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
     p.add_argument("--variant", choices=["auto", "issue", "latency"], default="auto",
@@ -56,237 +70,62 @@ def parse():
     p.add_argument("--surfaces", choices=["on", "off"], default="on",
                    help="off = scene_flags 0 (no disc, no markers: BASELINE config 1's scene)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores in this process's affinity)")
+    p.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--graph", action="store_true",
-                   help="N=1: capture one frame's bh_render (order kernels + march) in a HIP graph and replay it")
+                   help="N=1: capture one frame's bh_render (order kernel + march) in a HIP graph and replay it")
     p.add_argument("--verify-gather", action="store_true",
-                   help="N>1: rank 0 compares the assembled frame with its own full-frame render (bitwise)")
-    return p.parse_args()
+                   help="N>1: rank 0 compares both assembled targets with its own full-frame render (bitwise)")
+    p.add_argument("--frames-per-launch", type=int, default=0,
+                   help="frames rendered by one bh_render_frames launch (1..8; 0 = auto, DESIGN.md §5 item 9)")
+    p.add_argument("--plumbing", action="store_true",
+                   help="no GPU: the N-rank launch, gather pipeline and RGBM unpack on CPU (gloo) with "
+                        "synthetic shards (tests only; prints no measurement)")
+    return p.parse_args(argv)
 
 
 CAMERAS = {"B": ((0.0, 3.0, -20.0), (0.0, 0.0, 0.0)), "C": ((0.0, 6.0, -12.0), (0.0, 0.0, 0.0))}
 
 
-def main() -> None:
-    args = parse()
-    import torch
-    import torch.distributed as dist
+# ---- rank launcher (no torchrun) --------------------------------------------------------------------
 
-    import black_hole_ray_marching_amd as bh
-    from black_hole_ray_marching_amd import multigpu
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    n = max(world, 1)
-    # BH_BENCH_REHEARSAL=1 (development only, never set by the driver): all ranks share cuda:0 and
-    # the gloo backend, to exercise the N>1 path (sharding, pipelined gather, unpack) on a 1-GPU box
-    rehearsal = os.environ.get("BH_BENCH_REHEARSAL") == "1"
-    if rehearsal:
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if n > 1:
-        if rehearsal:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-
-    W, H = (args.width, args.height) if args.width and args.height else multigpu.weak_scaling_frame(n)
-    cap = args.max_iters
-    fmt = {"rgba16f": bh.BH_OUT_RGBA16F, "rgba32f": bh.BH_OUT_RGBA32F, "bgra8": bh.BH_OUT_BGRA8_SRGB}[args.fmt]
-    ch_dtype = {bh.BH_OUT_RGBA16F: torch.float16, bh.BH_OUT_RGBA32F: torch.float32,
-                bh.BH_OUT_BGRA8_SRGB: torch.uint8}[fmt]
-    bpp = bh.BYTES_PER_PIXEL[fmt]
-    math_mode = bh.BH_MATH_EXACT if args.math == "exact" else bh.BH_MATH_FAST
-    sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
-             "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
-    sched |= {"auto": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[args.variant]
-
-    sky = bh.synthetic_sky(4096, 2048)
-    flags = bh.BH_SCENE_DEFAULT if args.surfaces == "on" else 0
-    scene = bh.Scene(W, H, sky=sky, device=local, max_iters=cap, math=math_mode, scene_flags=flags)
-    if args.camera != "A":
-        scene.update(bh.Camera.look_at(*CAMERAS[args.camera], W, H))
-    stream = torch.cuda.current_stream(dev)
-
-    if n == 1:
-        col = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
-        bo = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
-        shard = dict(layout=bh.BH_LAYOUT_ROWMAJOR)
-        my_px = W * H
-        pipe = None
-    else:
-        # weak scaling: each rank renders its (tx + 3ty) % n tiles into a packed buffer; frame i's
-        # gather to rank 0 (col only: rank 0 can recompute blackout_col) overlaps frame i+1's render.
-        # The shards are BH_LAYOUT_TILES_RGB (alpha, always 1, is not shipped: 3/4 of the bytes into
-        # rank 0's xGMI links); rank 0's unpack restores it.
-        stride = multigpu.packed_stride(W, H, n)
-        my_px = bh.shard_tile_count(W, H, rank, n) * 64
-        bo = torch.empty((stride, 3, 64), dtype=ch_dtype, device=dev)
-        frame = torch.empty((H, W, 4), dtype=ch_dtype, device=dev) if rank == 0 else None
-        shard = dict(layout=bh.BH_LAYOUT_TILES_RGB, shard_index=rank, shard_count=n)
-
-        def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
-            # throttled: overlaps the next render on this GPU (0.78 -> 0.73 ms rank-0 frame at N=8)
-            bh.tiles_unpack_rgb(gathered, frame, W, H, n, stride, fmt, stream=torch.cuda.current_stream(dev),
-                                rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
-
-        pipe = multigpu.GatherPipeline(lambda: torch.empty((stride, 3, 64), dtype=ch_dtype, device=dev),
-                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
-        col = pipe.buffer(0)
-
-    frame_no = [0]
-
-    def render_direct(**kw):
-        scene.render(col if pipe is None else pipe.buffer(frame_no[0]), bo, fmt=fmt, stream=stream,
-                     schedule=sched, **shard, **kw)
-
-    graph = None
-    if args.graph and n == 1:
-        render_direct()  # allocate the per-geometry buffers before capture
-        torch.cuda.synchronize(dev)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            scene.render(col, bo, fmt=fmt, stream=torch.cuda.current_stream(dev), schedule=sched, **shard)
-
-    def render(**kw):
-        if graph is not None and not kw:
-            graph.replay()
-        else:
-            render_direct(**kw)
-
-    def exchange():
-        if pipe is not None:
-            pipe.submit(frame_no[0])
-        frame_no[0] += 1
-
-    for _ in range(args.warmup):
-        render()
-        exchange()
-    if pipe is not None:
-        pipe.drain()
-    torch.cuda.synchronize(dev)
-
-    # timed region: barrier + synchronize on both sides; HIP events around every render launch on
-    # the stream the kernel runs on (kernel duration for the roofline)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if n > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        ev[i][0].record(stream)
-        render()
-        ev[i][1].record(stream)
-        exchange()
-    if pipe is not None:
-        pipe.drain()
-    torch.cuda.synchronize(dev)
-    if n > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if n > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    kern_avg_s = float(kern_ms.mean()) / 1e3
-
-    gather_ok = None
-    if args.verify_gather and n > 1 and rank == 0:
-        ref = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
-        scene.render(ref, None, fmt=fmt, stream=stream, schedule=sched)
-        torch.cuda.synchronize(dev)
-        gather_ok = bool(torch.equal(ref.view(torch.uint8), frame.view(torch.uint8)))
-        del ref
-
-    # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
-    # the loop's own count (what the reference iterates); sum_steps the updates actually executed
-    # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
-    px_shape = (H, W) if n == 1 else (stride * 64,)  # the layout's pixel index space
-    nrk_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
-    steps_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
-    render(dbg_n_rk=nrk_buf, dbg_steps=steps_buf)
-    torch.cuda.synchronize(dev)
-    sum_nrk = int(nrk_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
-    sum_steps = int(steps_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
-
-    if rank == 0:
-        pmc = _pmc_entry(W, H, cap, args)
-        value = W * H * args.steps / elapsed / 1e6
-        achieved_tf = sum_steps * F_STEP[flags] / kern_avg_s / 1e12
-        alg_bytes = my_px * (bpp if n == 1 else bpp * 3 // 4) * 2 + sky.nbytes
-        achieved_gbs = alg_bytes / kern_avg_s / 1e9
-        result = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "Mpix/s",
-            "n_gpus": n,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (splitmix64-seeded 4096x2048 RGBA8 sRGB sky; reference default camera)",
-            "config": {
-                "workload": f"{W}x{H} frame, cap {cap} RK steps, "
-                            f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}, "
-                            f"{args.fmt} col+blackout, {args.math} math"
-                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n}, RCCL gather of col (RGB planes) to rank 0 "
-                                                  "overlapped with the next frame, unpack on rank 0"),
-                "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
-                "schedule": args.schedule, "format": args.fmt,
-                "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
-                               else f"tile-sharded x{n}"
-                               + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
-            },
-            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
-                               + (", 3u>" if args.schedule.startswith("tile") and flags == 3
-                                  else (", 4294967295u>" if args.schedule.startswith("tile") else ">")), "launches": args.steps,
-                       "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
-                       "max_ms": round(float(kern_ms.max()), 5), "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
-                       "mean_n_rk": round(sum_nrk / my_px, 4), "frames_per_s": round(1.0 / kern_avg_s, 2)},
-            "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
-                         "traffic": pmc.get("hbm_bytes_per_launch"),
-                         "valu_busy": pmc.get("valu_busy_est"),
-                         "valu_lane_utilization": pmc.get("valu_lane_utilization"),
-                         "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps / avg "
-                                 "launch time (HIP events on the render stream); FP32 VALU-bound, no "
-                                 "MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU issue "
-                                 "cycles / SIMD cycles, both from rocprofv3 PMC passes of this configuration "
-                                 "(profiles/pmc_traffic.json)"},
-            "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS,
-                             "unit": "GB/s", "frac": round(achieved_gbs / PEAK_HBM_GBS, 5),
-                             "algorithmic_bytes_per_launch": alg_bytes,
-                             "note": "col+blackout outputs + the sky texture read once"},
-        }
-        if args.no_cpu or n > 1:
-            result["cpu_baseline"] = None
-        else:
-            result["cpu_baseline"], result["parity"] = _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched)
-        if gather_ok is not None:
-            result["gather_verified_bit_exact"] = gather_ok
-        print(json.dumps(result))
-    if n > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
-def _pmc_entry(W, H, cap, args):
-    """This configuration's entry of profiles/pmc_traffic.json (rocprofv3 PMC passes), or {}."""
-    p = ROOT / "profiles" / "pmc_traffic.json"
-    try:
-        return json.loads(p.read_text()).get(f"{W}x{H}_cap{cap}_{args.math}_{args.schedule}_{args.fmt}") or {}
-    except (OSError, ValueError):
-        return {}
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """Start this script as N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, as
+    torchrun sets them) and wait for all of them.  The parent never touches a GPU (it does not even
+    import torch), so the children are plain fork+exec of an uninitialised process.  If any rank
+    fails, the others are terminated (by PID) and the exit status is non-zero."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.discard(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    return rc
 
+
+# ---- host facts for the CPU baseline ----------------------------------------------------------------
 
 def _cpu_model() -> str:
     try:
@@ -298,22 +137,390 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
-    """cpu_baseline: the C oracle on the host cores over the same full frame, `cpu_reps` times
-    (bounded: ~1 s wall, ~15 core-seconds on the GPU box); parity: the GPU frame (fp32 output of the
-    same kernel and math mode) against that oracle frame, every pixel."""
+def host_cpus() -> dict:
+    """CPUs this process may run on: the affinity mask, and a cgroup v2 CPU quota if one is set
+    (a quota of q CPUs caps the host work per second at q cores, whatever the affinity says)."""
+    info = {"cpu": _cpu_model(), "nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "cgroup_quota_cpus": None, "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+# ---- CPU plumbing rehearsal (tests) ------------------------------------------------------------------
+
+def plumbing(args, rank: int, n: int) -> int:
+    """The N>1 data path without a GPU: every rank packs synthetic BH_LAYOUT_TILES_RGBM shards of a
+    small RGBA16F frame (multigpu.pack_rgbm_numpy, the march kernel's store), the GatherPipeline brings
+    each frame to rank 0 over gloo, and rank 0 restores col and blackout_col (unpack_rgbm_numpy, the
+    bh_tiles_unpack_rgbm mirror) and checks them against the frame."""
+    import torch
+    import torch.distributed as dist
+
+    from black_hole_ray_marching_amd import multigpu
+    if n > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("BH_PLUMBING_FAIL_RANK") == str(rank):  # test hook: a rank that dies mid-run
+        raise SystemExit(f"plumbing: rank {rank} failing on request")
+    W, H = (args.width or 100), (args.height or 52)
+    stride = multigpu.packed_stride(W, H, n)
+    tb = multigpu.rgbm_tile_bytes(1)
+    yy, xx = np.mgrid[0:H, 0:W]
+
+    def frame(i):
+        c = np.stack([(xx % 7) * 0.25, (yy % 5) * 0.25, ((xx + yy + i) % 3) * 0.5, np.ones_like(xx)], -1)
+        c32 = c.astype(np.float32)
+        zero = ((c32[..., 0] * c32[..., 0] + c32[..., 1] * c32[..., 1]) + c32[..., 2] * c32[..., 2]) < 1.0
+        return c32.astype(np.float16), zero
+
+    ok = []
+
+    def on_frame(i, gathered):
+        col, bo = multigpu.unpack_rgbm_numpy(gathered.numpy(), W, H, n, stride, np.float16, 1.0)
+        want, zero = frame(i)
+        want_bo = want.copy()
+        want_bo[zero, :3] = 0
+        ok.append(bool(np.array_equal(col.view(np.uint16), want.view(np.uint16))
+                       and np.array_equal(bo.view(np.uint16), want_bo.view(np.uint16))))
+
+    pipe = multigpu.GatherPipeline(lambda: torch.zeros((stride, tb), dtype=torch.uint8), rank, n, on_frame)
+    for i in range(args.steps):
+        c, z = frame(i)
+        pipe.buffer(i).copy_(torch.from_numpy(multigpu.pack_rgbm_numpy(c, z, rank, n, stride)))
+        pipe.submit(i)
+    pipe.drain()
+    world = dist.get_world_size() if n > 1 else 1
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": n, "steps": args.steps,
+                          "data": "plumbing (CPU, gloo, synthetic RGBM shards; no GPU, not a measurement)",
+                          "world_size": world, "backend": dist.get_backend() if n > 1 else None,
+                          "frames_checked": len(ok), "gather_verified_bit_exact": bool(ok) and all(ok)}))
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if (rank != 0 or (len(ok) == args.steps and all(ok))) else 3
+
+
+# ---- the measurement ---------------------------------------------------------------------------------
+
+def main() -> int:
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure a different N")
+    n = world
+    if args.plumbing:
+        return plumbing(args, rank, n)
+
+    import torch
+    import torch.distributed as dist
+
+    import black_hole_ray_marching_amd as bh
+    from black_hole_ray_marching_amd import multigpu
+
+    # BH_BENCH_REHEARSAL=1 (development only, never set by the driver): all ranks share cuda:0 and
+    # the gloo backend, to exercise the N>1 path (sharding, pipelined gather, unpack) on a 1-GPU box
+    rehearsal = os.environ.get("BH_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local = 0
+    elif torch.cuda.device_count() < n:  # counting devices does not initialise the GPU
+        raise SystemExit(f"--gpus {n}: only {torch.cuda.device_count()} GPUs visible")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if n > 1:
+        if rehearsal:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != n:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {n}")
+
+    if args.width and args.height:
+        W, H = args.width, args.height
+        workload = "custom"
+    elif args.workload == "weak":
+        W, H = multigpu.weak_scaling_frame(n)
+        workload = "weak"
+    else:
+        W, H = WORKLOADS[args.workload]
+        workload = args.workload
+    scaling = "weak" if workload == "weak" else "strong"
+    cap = args.max_iters
+    fmt = {"rgba16f": bh.BH_OUT_RGBA16F, "rgba32f": bh.BH_OUT_RGBA32F, "bgra8": bh.BH_OUT_BGRA8_SRGB}[args.fmt]
+    ch_dtype = {bh.BH_OUT_RGBA16F: torch.float16, bh.BH_OUT_RGBA32F: torch.float32,
+                bh.BH_OUT_BGRA8_SRGB: torch.uint8}[fmt]
+    bpp = bh.BYTES_PER_PIXEL[fmt]
+    math_mode = bh.BH_MATH_EXACT if args.math == "exact" else bh.BH_MATH_FAST
+    sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
+             "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
+    sched |= {"auto": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[args.variant]
+    if n > 1 and args.schedule == "persistent":
+        raise SystemExit("N>1 ships BH_LAYOUT_TILES_RGBM shards: tile or pair schedule only")
+
+    sky = bh.synthetic_sky(4096, 2048)
+    flags = bh.BH_SCENE_DEFAULT if args.surfaces == "on" else 0
+    scene = bh.Scene(W, H, sky=sky, device=local, max_iters=cap, math=math_mode, scene_flags=flags)
+    if args.camera != "A":
+        scene.update(bh.Camera.look_at(*CAMERAS[args.camera], W, H))
+    stream = torch.cuda.current_stream(dev)
+
+    D = args.frames_per_launch or auto_frames_per_launch(n, W, H, cap)
+    if not 1 <= D <= bh.BH_MAX_FRAMES:
+        raise SystemExit(f"--frames-per-launch must be 1..{bh.BH_MAX_FRAMES}")
+    if n == 1:
+        cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
+        bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
+        shard = dict(layout=bh.BH_LAYOUT_ROWMAJOR)
+        my_tiles = ((W + 7) // 8) * ((H + 7) // 8)
+        my_bytes = W * H * bpp * 2
+        pipe = None
+    else:
+        # each rank renders its (tx + 3ty) % n tiles of D frames per launch, col only (blackout target
+        # None == Option::None: its per-pixel decision travels as the RGBM mask), into one packed
+        # buffer; launch i's gather to rank 0 (all D frames in one collective) overlaps launch i+1's
+        # render; rank 0 unpacks every frame's col and blackout_col on a side stream
+        stride = multigpu.packed_stride(W, H, n)
+        tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+        my_tiles = bh.shard_tile_count(W, H, rank, n)
+        my_bytes = my_tiles * tb + (2 * W * H * bpp if rank == 0 else 0)
+        frame_cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
+        frame_bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
+        shard = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=rank, shard_count=n)
+        launch_frames = {}
+
+        def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
+            # gathered: (n * D * stride, tb), rank k's block of D frames at k * D * stride
+            for f in range(launch_frames.pop(i)):
+                bh.tiles_unpack_rgbm(gathered[f * stride:], frame_cols[f], frame_bos[f], W, H, n, D * stride, fmt,
+                                     stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+
+        pipe = multigpu.GatherPipeline(lambda: torch.empty((D * stride, tb), dtype=torch.uint8, device=dev),
+                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
+
+    launch_no = [0]
+
+    def launch(nf, **kw):
+        """One bh_render_frames launch of nf <= D frames (all of this scene's camera)."""
+        if pipe is None:
+            scene.render_frames(cols[:nf], bos[:nf], fmt=fmt, stream=stream, schedule=sched, **shard, **kw)
+        else:
+            buf = pipe.buffer(launch_no[0])
+            scene.render_frames([buf[f * stride:(f + 1) * stride] for f in range(nf)], None, fmt=fmt, stream=stream,
+                                schedule=sched, **shard, **kw)
+
+    graph = None
+    if args.graph and n == 1:
+        launch(D)  # allocate the per-geometry buffers before capture
+        torch.cuda.synchronize(dev)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            scene.render_frames(cols, bos, fmt=fmt, stream=torch.cuda.current_stream(dev), schedule=sched, **shard)
+
+    def render(nf):
+        if graph is not None and nf == D:
+            graph.replay()
+        else:
+            launch(nf)
+
+    def exchange(nf):
+        if pipe is not None:
+            launch_frames[launch_no[0]] = nf
+            pipe.submit(launch_no[0])
+        launch_no[0] += 1
+
+    def sizes(k):  # frames per launch covering k frames
+        return [min(D, k - i) for i in range(0, k, D)]
+
+    for nf in sizes(args.warmup):
+        render(nf)
+        exchange(nf)
+    if pipe is not None:
+        pipe.drain()
+    torch.cuda.synchronize(dev)
+
+    # timed region: barrier + synchronize on both sides; HIP events around every launch on the stream
+    # the kernel runs on (kernel duration for the roofline)
+    plan = sizes(args.steps)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i, nf in enumerate(plan):
+        ev[i][0].record(stream)
+        render(nf)
+        ev[i][1].record(stream)
+        exchange(nf)
+    if pipe is not None:
+        pipe.drain()
+    torch.cuda.synchronize(dev)
+    if n > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_rank = [elapsed]
+    if n > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        gl = [torch.zeros_like(t) for _ in range(n)]
+        dist.all_gather(gl, t)
+        per_rank = [float(x.item()) for x in gl]
+        elapsed = max(per_rank)
+    kern_ms = np.array([a.elapsed_time(b) for a, b in ev])       # per launch
+    frames_in = np.array(plan, dtype=np.float64)
+    kern_frame_s = float(kern_ms.sum() / frames_in.sum()) / 1e3   # launch time per frame
+    full = kern_ms[frames_in == D] if (frames_in == D).any() else kern_ms
+    kern_avg_s = float(full.mean()) / 1e3                        # a full launch (D frames)
+
+    gather_ok = None
+    if args.verify_gather and n > 1 and rank == 0:
+        ref_c = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
+        ref_b = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
+        scene.render(ref_c, ref_b, fmt=fmt, stream=stream, schedule=sched)
+        torch.cuda.synchronize(dev)
+        last = plan[-1]
+        gather_ok = all(bool(torch.equal(ref_c.view(torch.uint8), frame_cols[f].view(torch.uint8))
+                             and torch.equal(ref_b.view(torch.uint8), frame_bos[f].view(torch.uint8)))
+                        for f in range(last))
+        del ref_c, ref_b
+
+    # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
+    # the loop's own count (what the reference iterates); sum_steps the updates actually executed
+    # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
+    px_shape = (H, W) if n == 1 else (multigpu.packed_stride(W, H, n) * 64,)  # the layout's pixel index space
+    nrk_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
+    steps_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
+    launch(1, dbg_n_rk=[nrk_buf], dbg_steps=[steps_buf])
+    torch.cuda.synchronize(dev)
+    sum_nrk = int(nrk_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
+    sum_steps = int(steps_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
+
+    if rank == 0:
+        value = W * H * args.steps / elapsed / 1e6
+        # per launch: D frames' executed steps / the launch's average duration (HIP events)
+        achieved_tf = sum_steps * D * F_STEP[flags] / kern_avg_s / 1e12
+        alg_bytes = my_bytes * D + sky.nbytes
+        achieved_gbs = alg_bytes / kern_avg_s / 1e9
+        pmc = _pmc_entry(W, H, cap, args, n)
+        result = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mpix/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": scaling,
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (splitmix64-seeded 4096x2048 RGBA8 sRGB sky; reference default camera)",
+            "config": {
+                "workload": f"{workload}: {W}x{H} frame, cap {cap} RK steps, "
+                            f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}, "
+                            f"{args.fmt} col+blackout, {args.math} math"
+                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
+                                                  "(RGB planes + blackout mask) to rank 0 overlapped with the next "
+                                                  "frame, rank 0 unpacks col and blackout_col"),
+                "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
+                "schedule": args.schedule, "format": args.fmt, "frames_per_launch": D,
+                "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
+                               else f"tile-sharded x{n}"
+                               + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
+            },
+            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
+                               + (", 3u>" if args.schedule.startswith("tile") and flags == 3
+                                  else (", 4294967295u>" if args.schedule.startswith("tile") else ">")),
+                       "launches": len(plan), "frames_per_launch": D, "tiles_per_frame": my_tiles,
+                       "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(full.min()), 5),
+                       "max_ms": round(float(full.max()), 5), "ms_per_frame": round(kern_frame_s * 1e3, 5),
+                       "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
+                       "mean_n_rk": round(sum_nrk / (my_tiles * 64), 4), "frames_per_s": round(1.0 / kern_frame_s, 2),
+                       "note": "avg/min/max over full launches of frames_per_launch frames; sum_n_rk / sum_steps "
+                               "per frame (this rank's tiles)"},
+            "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
+                         "traffic": pmc.get("hbm_bytes_per_launch"),
+                         "valu_busy": pmc.get("valu_busy_est"),
+                         "valu_lane_utilization": pmc.get("valu_lane_utilization"),
+                         "pmc_source": pmc.get("source"),
+                         "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps x "
+                                 "frames_per_launch / avg launch time (HIP events on the render stream); FP32 "
+                                 "VALU-bound, no MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU "
+                                 "issue cycles / SIMD cycles, from the rocprofv3 PMC passes of this configuration "
+                                 "named in pmc_source (profiles/pmc_traffic.json), null if none"},
+            "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS,
+                             "unit": "GB/s", "frac": round(achieved_gbs / PEAK_HBM_GBS, 5),
+                             "algorithmic_bytes_per_launch": alg_bytes,
+                             "note": "this rank's outputs (N>1: its RGBM shard, and on rank 0 the two "
+                                     "unpacked targets) + the sky texture read once"},
+        }
+        if n > 1:
+            result["world_size"] = dist.get_world_size()
+            result["backend"] = dist.get_backend()
+            result["per_rank_s"] = [round(x, 6) for x in per_rank]
+        if args.no_cpu or n > 1:
+            result["cpu_baseline"] = None
+        else:
+            result["cpu_baseline"], result["parity"] = _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched, fmt)
+        if gather_ok is not None:
+            result["gather_verified_bit_exact"] = gather_ok
+        print(json.dumps(result), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
+    """Frames per launch: enough that each frame's serial tail (the few rays that march to the cap, ~0.9
+    us per step alone: DESIGN.md §5) overlaps the other frames' bulk.  Measured (tools/probe_inflight.py,
+    profiles/r02/inflight.log; ms per frame at D = 1/2/4/8): 4096x2048 0.658/0.633/0.621/0.614; its 1/8
+    shard 0.410/0.261/0.121/0.088; 8192x4096's 1/8 shard 0.612/0.334/0.323/0.317.  The most the kernel
+    argument carries (BH_MAX_FRAMES) is the best everywhere measured."""
+    return 8
+
+
+def _pmc_entry(W, H, cap, args, n):
+    """This configuration's entry of profiles/pmc_traffic.json (rocprofv3 PMC passes), or {}."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    key = f"{W}x{H}_cap{cap}_{args.camera}_{args.math}_{args.schedule}_{args.fmt}" + (f"_n{n}" if n > 1 else "")
+    try:
+        return json.loads(p.read_text()).get(key) or {}
+    except (OSError, ValueError):
+        return {}
+
+
+def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched, fmt):
+    """cpu_baseline: the C oracle (gcc -O3 -ffp-contract=off, OpenMP dynamic rows) on every CPU this
+    process may use, over the same full frame, `cpu_reps` times, plus a 1-thread leg on every 8th
+    row; parity: the GPU frame against that oracle frame, every pixel -- in RGBA32F (the fp32
+    result, bit-exact) AND in the timed format (RGBA16F: round-to-nearest-even of the oracle's fp32
+    words; BGRA8: its normative sRGB encode), col and blackout_col."""
     import torch
 
     import black_hole_ray_marching_amd as bh
     import oracle
 
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    host = host_cpus()
+    quota = host["cgroup_quota_cpus"]
+    threads = args.cpu_threads or (min(host["affinity"], max(1, int(quota))) if quota else host["affinity"])
     cu, U = scene.camera_uniform.to_bytes(), bytes(scene.uniforms.to_c())
     oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, 0, 64, threads=threads)  # warm-up
     times = []
+    o_col = o_bo = o_nrk = o_fate = None
     for _ in range(max(1, args.cpu_reps)):
         t0 = time.perf_counter()
-        o_col, _, o_nrk, o_fate = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, threads=threads)
+        o_col, o_bo, o_nrk, o_fate = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, threads=threads)
         times.append(time.perf_counter() - t0)
     cpu_s = float(np.median(times))
     sum_nrk = int(o_nrk.astype(np.int64).sum())
@@ -322,30 +529,50 @@ def _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched):
     _, _, s_nrk, _ = oracle.render_rows(cu, U, sky, W, H, cap, scene.scene_flags, 0, H, threads=1, row_step=8)
     one_s = time.perf_counter() - t0
     cpu_baseline = {"value": round(W * H / cpu_s / 1e6, 4), "unit": "Mpix/s", "cores": threads, "kind": "port",
-                    "sample": f"the full {W}x{H} cap-{cap} frame, x{len(times)} (median {cpu_s:.2f} s): C oracle "
-                              f"(oracle/bh_oracle.c, gcc -O2 -ffp-contract=off), OpenMP {threads} threads",
+                    "sample": f"the full {W}x{H} cap-{cap} frame, x{len(times)} (median {cpu_s:.3f} s): C oracle "
+                              f"(oracle/bh_oracle.c, gcc -O3 -ffp-contract=off), OpenMP {threads} threads, "
+                              "dynamic rows",
                     "n_rk_per_s": round(sum_nrk / cpu_s, 1),
                     "single_thread": {"value": round(s_nrk.size / one_s / 1e6, 4), "unit": "Mpix/s",
                                       "n_rk_per_s": round(int(s_nrk.astype(np.int64).sum()) / one_s, 1),
                                       "sample": f"every 8th row of the frame ({s_nrk.size} px, {one_s:.2f} s), 1 thread"},
-                    "host": {"cpu": _cpu_model(), "nproc": os.cpu_count(),
-                             "affinity": len(os.sched_getaffinity(0))}}
+                    "host": host}
     c32 = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+    b32 = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     nrk = torch.empty((H, W), dtype=torch.int16, device=dev)
     fate = torch.empty((H, W), dtype=torch.uint8, device=dev)
-    scene.render(c32, None, fmt=bh.BH_OUT_RGBA32F, stream=stream, dbg_n_rk=nrk, dbg_fate=fate, schedule=sched)
+    scene.render(c32, b32, fmt=bh.BH_OUT_RGBA32F, stream=stream, dbg_n_rk=nrk, dbg_fate=fate, schedule=sched)
+    ch = {bh.BH_OUT_RGBA16F: torch.float16, bh.BH_OUT_RGBA32F: torch.float32, bh.BH_OUT_BGRA8_SRGB: torch.uint8}[fmt]
+    tc = torch.empty((H, W, 4), dtype=ch, device=dev)
+    tbo = torch.empty((H, W, 4), dtype=ch, device=dev)
+    scene.render(tc, tbo, fmt=fmt, stream=stream, schedule=sched)
     torch.cuda.synchronize()
-    gc, gn, gf = c32.cpu().numpy(), nrk.cpu().numpy().view(np.uint16), fate.cpu().numpy()
+    gc, gb, gn, gf = c32.cpu().numpy(), b32.cpu().numpy(), nrk.cpu().numpy().view(np.uint16), fate.cpu().numpy()
     match = (gf == o_fate) & (gn == o_nrk)
     d = np.abs(gc[..., :3] - o_col[..., :3]).max(axis=-1)
-    parity = {"vs": "oracle/bh_oracle.c (normative restatement of src/black_hole_maybe.wgsl; parity unpinned "
-                    "against the WGSL itself, which cannot run here)",
+
+    def expect(x):  # the timed format's bytes of an fp32 oracle image
+        if fmt == bh.BH_OUT_RGBA16F:
+            return x.astype(np.float16).view(np.uint8)
+        if fmt == bh.BH_OUT_RGBA32F:
+            return x.view(np.uint8)
+        e = oracle.srgb_encode(x[..., :3])
+        return np.stack([e[..., 2], e[..., 1], e[..., 0], np.full(e.shape[:2], 255, np.uint8)], -1)
+
+    timed_ok = bool(np.array_equal(tc.cpu().numpy().view(np.uint8), expect(o_col))
+                    and np.array_equal(tbo.cpu().numpy().view(np.uint8), expect(o_bo)))
+    parity = {"vs": "oracle/bh_oracle.c: the normative restatement of src/black_hole_maybe.wgsl. PARITY "
+                    "UNPINNED against the WGSL itself (no WGSL runtime, no reference fixtures); a real WGSL "
+                    "driver's pow / atan2 / 8-bit sampler weights differ from these normative choices "
+                    "(DESIGN.md §3 'Parity envelope')",
               "pixels": int(match.size), "fate_nrk_match": round(float(match.mean()), 7),
               "max_abs_delta": float(d.max()), "max_abs_delta_fate_matched": float(d[match].max()),
-              "bit_exact": bool(np.array_equal(gc.view(np.uint32), o_col.view(np.uint32))),
+              "bit_exact": bool(np.array_equal(gc.view(np.uint32), o_col.view(np.uint32))
+                                and np.array_equal(gb.view(np.uint32), o_bo.view(np.uint32))),
+              "timed_format": args.fmt, "timed_format_bit_exact": timed_ok,
               "tolerance": 1e-4, "math": args.math}
     return cpu_baseline, parity
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

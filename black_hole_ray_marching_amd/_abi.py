@@ -19,13 +19,17 @@ BH_BLOOM_AUTO, BH_BLOOM_LITERAL = 0, 1
 BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
-BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB = 0, 1, 2
+BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM = 0, 1, 2, 3
+BH_ORDER_STATES = 32
+BH_MAX_FRAMES = 8
 BH_SCHED_TILE, BH_SCHED_PAIR, BH_SCHED_PERSISTENT = 0, 1, 2
 BH_SCHED_FLAG_STATIC_ORDER = 0x100
 BH_SCHED_FLAG_ISSUE_ORDER = 0x200   # exact math: force the source-order build of the kernels
 BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled build
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
+
+ABI_VERSION = 2
 
 BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
 
@@ -81,6 +85,8 @@ SIGNATURES = {
     "bh_destroy": (C.c_int, [C.c_void_p]),
     "bh_render": (C.c_int, [C.c_void_p, C.POINTER(bh_camera_uniform), C.POINTER(bh_uniforms),
                             C.POINTER(bh_render_desc), C.c_void_p]),
+    "bh_render_frames": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(bh_camera_uniform), C.POINTER(bh_uniforms),
+                                   C.POINTER(bh_render_desc), C.c_void_p]),
     "bh_shard_tile_count": (C.c_int64, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "bh_tiles_unpack": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                   C.c_uint64, C.c_uint32, C.c_void_p]),
@@ -88,6 +94,9 @@ SIGNATURES = {
                                       C.c_uint64, C.c_uint32, C.c_void_p]),
     "bh_tiles_unpack_rgb_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                            C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "bh_tiles_unpack_rgbm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                       C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "bh_tile_bytes": (C.c_int64, [C.c_uint32, C.c_uint32]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
     "bh_controller_update": (C.c_int, [C.POINTER(bh_controller), C.POINTER(bh_camera), C.c_float, C.c_int,
                                        C.POINTER(C.c_int)]),
@@ -123,7 +132,7 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.bh_abi_version() != 1:
+    if lib.bh_abi_version() != ABI_VERSION:
         raise RuntimeError("libbh_render.so ABI version mismatch")
     _lib = lib
     return lib

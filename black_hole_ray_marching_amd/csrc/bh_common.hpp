@@ -7,7 +7,22 @@
 
 namespace bh {
 
+// The per-frame part of a launch that renders several frames (bh_render_frames): camera, the
+// photon-sphere centre derived from its position, and the frame's outputs.
+struct FrameArgs {
+    float pos[3];
+    float c0[3], c1[3], c2[3];
+    float cps[3];
+    void* out_col;
+    void* out_blackout;
+    uint16_t* dbg_n_rk;
+    uint8_t* dbg_fate;
+    uint16_t* dbg_steps;
+};
+
 // Everything one launch needs, passed by value as the kernel argument (lives in SGPRs / kernarg).
+// The per-frame fields (pos, c0..c2, cps, outputs) are frame 0's; a multi-frame launch (n_frames > 1,
+// tile schedule) also carries every frame's in `frames` and each wave selects its own.
 struct MarchArgs {
     // camera uniform (src/black_hole_maybe.wgsl:9-17): ro0 and the three interpolated corner rays
     float pos[3];
@@ -41,6 +56,9 @@ struct MarchArgs {
     uint16_t* dbg_n_rk;
     uint8_t* dbg_fate;
     uint16_t* dbg_steps;
+    // frames of one launch (bh_render_frames): wave slot s marches frame s % n_frames, tile s / n_frames
+    uint32_t n_frames;
+    FrameArgs frames[BH_MAX_FRAMES];
 };
 
 // Shard ownership: tile (tx, ty) belongs to shard (tx + 3*ty) % S (SURVEY §8e diagonal interleave).
@@ -164,6 +182,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
                                                                          uint32_t block, uint32_t centre,
                                                                          uint32_t* counters, uint32_t* order,
                                                                          hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo,
+                                                                               uint32_t width, uint32_t height,
+                                                                               uint32_t shard_count, uint64_t stride_tiles,
+                                                                               uint32_t format, uint32_t rows_in_flight,
+                                                                               hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,
                                                                               uint32_t height, uint32_t shard_count,
                                                                               uint64_t stride_tiles, uint32_t format, uint32_t rows_in_flight,

@@ -25,12 +25,21 @@ struct bh_ctx {
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
     uint32_t cus = 0;                        // compute units of the device
-    // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order
-    uint8_t* tile_cost = nullptr;
-    uint32_t* order = nullptr;
-    uint32_t* order_counters = nullptr;  // 2 * ORDER_BUCKETS + 1 words (bh_tiles.hip order_scatter_kernel)
-    uint64_t order_cap = 0;              // tiles the two buffers hold
-    uint64_t order_key = ~0ull;          // (width, height, shard) the costs belong to
+    // temporal dispatch order (tile schedule): per-tile cost of the previous frame -> order, one state
+    // per (frame geometry, shard, stream).  Never freed before bh_destroy except by LRU eviction beyond
+    // BH_ORDER_STATES states, so a graph captured after the first call of a key keeps valid pointers,
+    // and renders on different streams (frames in flight) never share costs or counters.
+    struct OrderState {
+        uint32_t width = 0, height = 0, shard_index = 0, shard_count = 0;
+        void* stream = nullptr;
+        uint64_t last_use = 0;
+        bool valid = false;                  // costs and histogram agree (false: start afresh)
+        uint8_t* tile_cost = nullptr;
+        uint32_t* order = nullptr;
+        uint32_t* counters = nullptr;        // 2 * ORDER_BUCKETS + 1 words (bh_tiles.hip order_scatter_kernel)
+    };
+    std::vector<OrderState> orders;
+    uint64_t order_clock = 0;
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
     std::vector<uint32_t*> bloom_tex;
     uint64_t bloom_key = ~0ull;
@@ -438,9 +447,11 @@ int bh_destroy(bh_ctx* c) {
     if (c->enc) (void)hipFree(c->enc);
     if (c->enc_b) (void)hipFree(c->enc_b);
     if (c->counters) (void)hipFree(c->counters);
-    if (c->tile_cost) (void)hipFree(c->tile_cost);
-    if (c->order) (void)hipFree(c->order);
-    if (c->order_counters) (void)hipFree(c->order_counters);
+    for (auto& o : c->orders) {
+        if (o.tile_cost) (void)hipFree(o.tile_cost);
+        if (o.order) (void)hipFree(o.order);
+        if (o.counters) (void)hipFree(o.counters);
+    }
     for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
     (void)hipSetDevice(prev);
     delete c;
@@ -612,26 +623,101 @@ static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles,
     return d->max_iters <= 512u && (uint64_t)n_tiles >= 256ull * (cus ? cus : 256u);
 }
 
+// The temporal-order state of (geometry, shard, stream): found, or created (allocating; the LRU state
+// is evicted beyond BH_ORDER_STATES).  New states start with all costs 0 and an empty histogram.
+static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStream_t s, bh_ctx::OrderState** out) {
+    for (auto& o : c->orders)
+        if (o.width == d->width && o.height == d->height && o.shard_index == d->shard_index &&
+            o.shard_count == d->shard_count && o.stream == (void*)s) {
+            o.last_use = ++c->order_clock;
+            *out = &o;
+            return BH_OK;
+        }
+    bh_ctx::OrderState n;
+    n.width = d->width; n.height = d->height; n.shard_index = d->shard_index; n.shard_count = d->shard_count;
+    n.stream = (void*)s;
+    const size_t cw = (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t);
+    hipError_t he;
+    if ((he = hipMalloc(&n.tile_cost, nt)) != hipSuccess || (he = hipMalloc(&n.order, nt * sizeof(uint32_t))) != hipSuccess ||
+        (he = hipMalloc(&n.counters, cw)) != hipSuccess) {
+        if (n.tile_cost) (void)hipFree(n.tile_cost);
+        if (n.order) (void)hipFree(n.order);
+        return he == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(he, "hipMalloc(temporal order)");
+    }
+    if (c->orders.size() >= BH_ORDER_STATES) {  // evict the least recently used
+        size_t v = 0;
+        for (size_t i = 1; i < c->orders.size(); ++i)
+            if (c->orders[i].last_use < c->orders[v].last_use) v = i;
+        auto& o = c->orders[v];
+        (void)hipFree(o.tile_cost); (void)hipFree(o.order); (void)hipFree(o.counters);
+        c->orders.erase(c->orders.begin() + (long)v);
+    }
+    n.last_use = ++c->order_clock;
+    c->orders.push_back(n);
+    *out = &c->orders.back();
+    return BH_OK;
+}
+
+// Per-frame invariants with the oracle's op sequence (correctly rounded f32, no contraction):
+// c_ps = ((-normalize(ro0)) * 1.5) * RS (src/black_hole_maybe.wgsl:294).
+static void frame_args(const bh_camera_uniform* cam, float rs, const bh_render_desc* d, bh::FrameArgs* F) {
+    for (int k = 0; k < 3; ++k) {
+        F->pos[k] = cam->pos[k];
+        F->c0[k] = cam->world_tri[0][k];
+        F->c1[k] = cam->world_tri[1][k];
+        F->c2[k] = cam->world_tri[2][k];
+    }
+    const float x = F->pos[0], y = F->pos[1], z = F->pos[2];
+    const float len = std::sqrt((x * x + y * y) + z * z);
+    const float n[3] = {x / len, y / len, z / len};
+    for (int k = 0; k < 3; ++k) F->cps[k] = (-n[k] * 1.5f) * rs;
+    F->out_col = d->out_col; F->out_blackout = d->out_blackout;
+    F->dbg_n_rk = d->dbg_n_rk; F->dbg_fate = d->dbg_fate; F->dbg_steps = d->dbg_steps;
+}
+
+static bool same_launch(const bh_render_desc* a, const bh_render_desc* b) {
+    return a->width == b->width && a->height == b->height && a->max_iters == b->max_iters &&
+           a->scene_flags == b->scene_flags && a->format == b->format && a->math == b->math &&
+           a->layout == b->layout && a->shard_index == b->shard_index && a->shard_count == b->shard_count &&
+           a->schedule == b->schedule;
+}
+
 int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, const bh_render_desc* d,
               void* stream) {
-    if (!c || !cam || !U || !d || !d->out_col) return BH_ERR_INVALID_ARG;
+    return bh_render_frames(c, 1u, cam, U, d, stream);
+}
+
+int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams, const bh_uniforms* U,
+                     const bh_render_desc* descs, void* stream) {
+    if (!c || !cams || !U || !descs || n_frames == 0 || n_frames > BH_MAX_FRAMES) return BH_ERR_INVALID_ARG;
+    const bh_render_desc* d = &descs[0];
+    const bh_camera_uniform* cam = &cams[0];
+    if (!d->out_col) return BH_ERR_INVALID_ARG;
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
-    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGB) return BH_ERR_INVALID_ARG;
+    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGBM) return BH_ERR_INVALID_ARG;
     if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER | BH_SCHED_FLAG_ISSUE_ORDER | BH_SCHED_FLAG_LATENCY))) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
     if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
-    if (!screen_tri_default(cam)) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
+    for (uint32_t i = 0; i < n_frames; ++i) {
+        if (!descs[i].out_col || !same_launch(d, &descs[i])) return BH_ERR_INVALID_ARG;
+        if (!screen_tri_default(&cams[i])) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
+    }
+    if (d->layout == BH_LAYOUT_TILES_RGBM && (d->schedule & 0xFFu) == BH_SCHED_PERSISTENT) {
+        g_last_error = "BH_LAYOUT_TILES_RGBM needs the tile or pair schedule";
+        return BH_ERR_UNSUPPORTED;
+    }
+    if (n_frames > 1u && (d->schedule & 0xFFu) != BH_SCHED_TILE) {  // one launch per frame
+        for (uint32_t i = 0; i < n_frames; ++i) {
+            const int st = bh_render_frames(c, 1u, &cams[i], U, &descs[i], stream);
+            if (st != BH_OK) return st;
+        }
+        return BH_OK;
+    }
 
     bh::MarchArgs a;
     std::memset(&a, 0, sizeof(a));
-    for (int k = 0; k < 3; ++k) {
-        a.pos[k] = cam->pos[k];
-        a.c0[k] = cam->world_tri[0][k];
-        a.c1[k] = cam->world_tri[1][k];
-        a.c2[k] = cam->world_tri[2][k];
-    }
     a.rs = U->rs; a.dtm = U->delta_time_mult; a.max_dist = U->max_dist; a.dp = U->distortion_power;
     a.blackout_eh = U->blackout_eh;
     a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
@@ -639,23 +725,24 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;
     a.tiles_x = (d->width + 7u) / 8u; a.tiles_y = (d->height + 7u) / 8u;
     const uint64_t nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
-    if (nt > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
+    if (nt * n_frames > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
     a.n_tiles = (uint32_t)nt;
     // centre-out dispatch blocks of ~one tile row of this shard, centred on the black hole's row
     a.order_block = (uint32_t)((nt + a.tiles_y - 1u) / a.tiles_y);
     a.order_centre = bh_tile_row(cam, d->height);
     a.sky = c->sky; a.srgb_lut = c->lut; a.srgb_enc = c->enc; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
-    // per-frame invariants with the oracle's op sequence (correctly rounded f32, no contraction):
-    // c_ps = ((-normalize(ro0)) * 1.5) * RS (src/black_hole_maybe.wgsl:294), k = (DP * RS) * -1.5 (:126)
+    // k = (DP * RS) * -1.5 (:126); the per-frame fields (camera, c_ps, outputs)
+    a.kfac = (a.dp * a.rs) * -1.5f;
+    a.n_frames = n_frames;
+    for (uint32_t i = 0; i < n_frames; ++i) frame_args(&cams[i], a.rs, &descs[i], &a.frames[i]);
     {
-        const float x = a.pos[0], y = a.pos[1], z = a.pos[2];
-        const float len = std::sqrt((x * x + y * y) + z * z);
-        const float n[3] = {x / len, y / len, z / len};
-        for (int k = 0; k < 3; ++k) a.cps[k] = (-n[k] * 1.5f) * a.rs;
-        a.kfac = (a.dp * a.rs) * -1.5f;
+        const bh::FrameArgs& F = a.frames[0];
+        for (int k = 0; k < 3; ++k) {
+            a.pos[k] = F.pos[k]; a.c0[k] = F.c0[k]; a.c1[k] = F.c1[k]; a.c2[k] = F.c2[k]; a.cps[k] = F.cps[k];
+        }
+        a.out_col = F.out_col; a.out_blackout = F.out_blackout;
+        a.dbg_n_rk = F.dbg_n_rk; a.dbg_fate = F.dbg_fate; a.dbg_steps = F.dbg_steps;
     }
-    a.out_col = d->out_col; a.out_blackout = d->out_blackout;
-    a.dbg_n_rk = d->dbg_n_rk; a.dbg_fate = d->dbg_fate; a.dbg_steps = d->dbg_steps;
     if (a.n_tiles == 0) return BH_OK;
 
     int prev = 0;
@@ -663,36 +750,24 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (prev != c->device) (void)hipSetDevice(c->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uint32_t sched = d->schedule & 0xFFu;
+    bh_ctx::OrderState* os = nullptr;
     if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
-        // temporal order: (re)allocate on a new geometry (the only allocation bh_render ever makes:
-        // capture into a graph after one call per frame size), reset costs, build this frame's order
-        const uint64_t key = ((uint64_t)d->width << 40) ^ ((uint64_t)d->height << 20) ^
-                             ((uint64_t)d->shard_index << 8) ^ d->shard_count;
-        hipError_t he = hipSuccess;
-        if (key != c->order_key) {
-            if (nt > c->order_cap) {
-                if (c->tile_cost) (void)hipFree(c->tile_cost);
-                if (c->order) (void)hipFree(c->order);
-                c->tile_cost = nullptr; c->order = nullptr; c->order_cap = 0;
-                if ((he = hipMalloc(&c->tile_cost, nt)) == hipSuccess &&
-                    (he = hipMalloc(&c->order, nt * sizeof(uint32_t))) == hipSuccess)
-                    c->order_cap = nt;
-            }
-            if (he == hipSuccess && !c->order_counters)
-                he = hipMalloc(&c->order_counters, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t));
+        // temporal order of this (geometry, shard, stream): allocated at its first render only
+        int st = order_state(c, d, nt, s, &os);
+        if (st != BH_OK) { if (prev != c->device) (void)hipSetDevice(prev); return st; }
+        if (!os->valid) {
             // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent
-            if (he == hipSuccess)
-                he = hipMemsetAsync(c->order_counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
-            if (he == hipSuccess) he = hipMemsetAsync(c->tile_cost, 0, nt, s);
-            if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order buffers"); }
-            c->order_key = key;
+            hipError_t he = hipMemsetAsync(os->counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
+            if (he == hipSuccess) he = hipMemsetAsync(os->tile_cost, 0, nt, s);
+            if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order reset"); }
+            os->valid = true;
         }
-        int oe = bh_launch_build_order(c->tile_cost, a.n_tiles, a.order_block, a.order_centre, c->order_counters,
-                                       c->order, s);
-        if (oe != 0) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail((hipError_t)oe, "order kernels"); }
-        a.order = c->order;
-        a.tile_cost = c->tile_cost;
-        a.order_tot = c->order_counters;
+        int oe = bh_launch_build_order(os->tile_cost, a.n_tiles, a.order_block, a.order_centre, os->counters,
+                                       os->order, s);
+        if (oe != 0) { os->valid = false; if (prev != c->device) (void)hipSetDevice(prev); return hip_fail((hipError_t)oe, "order kernels"); }
+        a.order = os->order;
+        a.tile_cost = os->tile_cost;
+        a.order_tot = os->counters;
     }
     int e = d->math != BH_MATH_EXACT ? bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s)
             : march_variant_issue_order(d, a.n_tiles, c->cus)
@@ -701,8 +776,8 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     if (prev != c->device) (void)hipSetDevice(prev);
     if (e != 0) {
         // the costs and their histogram are written together by the march kernel; without it they
-        // may disagree, so the next frame starts the temporal order afresh
-        c->order_key = ~0ull;
+        // may disagree, so the next frame of this state starts the temporal order afresh
+        if (os) os->valid = false;
         return hip_fail((hipError_t)e, "march kernel launch");
     }
     return BH_OK;
@@ -737,6 +812,31 @@ int bh_tiles_unpack_rgb_rows(const void* packed, void* out, uint32_t width, uint
 int bh_tiles_unpack_rgb(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
                         uint64_t shard_stride_tiles, uint32_t format, void* stream) {
     return bh_tiles_unpack_rgb_rows(packed, out, width, height, shard_count, shard_stride_tiles, format, 0u, stream);
+}
+
+int bh_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo, uint32_t width, uint32_t height,
+                         uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
+                         void* stream) {
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
+    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < shard_count; ++k)
+        if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
+            return BH_ERR_INVALID_ARG;
+    int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, width, height, shard_count, shard_stride_tiles, format,
+                                        rows_in_flight, reinterpret_cast<hipStream_t>(stream));
+    if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
+    return BH_OK;
+}
+
+int64_t bh_tile_bytes(uint32_t layout, uint32_t format) {
+    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    const int64_t bpp = format == BH_OUT_RGBA32F ? 16 : format == BH_OUT_RGBA16F ? 8 : 4;
+    switch (layout) {
+        case BH_LAYOUT_TILES: return 64 * bpp;
+        case BH_LAYOUT_TILES_RGB: return 48 * bpp;
+        case BH_LAYOUT_TILES_RGBM: return 48 * bpp + 8;
+        default: return BH_ERR_INVALID_ARG;
+    }
 }
 
 }  // extern "C"

@@ -627,12 +627,13 @@ __device__ __forceinline__ void load_tables(const MarchArgs& a, float* tab) {
     }
 }
 
-// BH_LAYOUT_TILES_RGB store: pixel idx = tile * 64 + lane goes to three channel planes of its tile
+// BH_LAYOUT_TILES_RGB(M) store: pixel idx = tile * 64 + lane goes to three channel planes of its tile
 // (alpha, always 1, is dropped; the unpack restores it).  Each plane store of a wave is one
-// contiguous 64-element run.
-template <uint32_t FMT>
+// contiguous 64-element run.  TE = the tile's size in channel elements (192, or 192 + the 8-byte
+// blackout mask word of BH_LAYOUT_TILES_RGBM).
+template <uint32_t FMT, uint32_t TE>
 __device__ __forceinline__ void store_px_planar(void* base, size_t idx, v3 c, const float* enc) {
-    const size_t o = (idx >> 6) * 192u + (idx & 63u);
+    const size_t o = (idx >> 6) * TE + (idx & 63u);
     if constexpr (FMT == BH_OUT_RGBA32F) {
         float* p = reinterpret_cast<float*>(base) + o;
         p[0] = c.x; p[64] = c.y; p[128] = c.z;
@@ -646,14 +647,33 @@ __device__ __forceinline__ void store_px_planar(void* base, size_t idx, v3 c, co
     }
 }
 
+// Channel elements of one BH_LAYOUT_TILES_RGBM tile: three planes of 64, then the 8-byte mask word.
+template <uint32_t FMT>
+constexpr uint32_t rgbm_tile_elems() { return 192u + 8u / (FMT == BH_OUT_RGBA32F ? 4u : FMT == BH_OUT_RGBA16F ? 2u : 1u); }
+
 // fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
+// BH_LAYOUT_TILES_RGBM: every active lane of the calling wave must hold a pixel of the same tile
+// (true of the tile and pair schedules, bh_render rejects the others): the wave's ballot of the
+// blackout test is the tile's mask word, stored by its first active lane.
 template <uint32_t FMT>
 __device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab, size_t idx, v3 col, uint32_t n_rk,
                                             uint32_t fate, uint32_t steps) {
-    const v3 bo = dot(col, col) < 1.0f ? mk(0.0f, 0.0f, 0.0f) : col;
+    const bool zero = dot(col, col) < 1.0f;
+    const v3 bo = zero ? mk(0.0f, 0.0f, 0.0f) : col;
     if (a.layout == BH_LAYOUT_TILES_RGB) {
-        store_px_planar<FMT>(a.out_col, idx, col, tab + 256);
-        if (a.out_blackout) store_px_planar<FMT>(a.out_blackout, idx, bo, tab + 256);
+        store_px_planar<FMT, 192u>(a.out_col, idx, col, tab + 256);
+        if (a.out_blackout) store_px_planar<FMT, 192u>(a.out_blackout, idx, bo, tab + 256);
+    } else if (a.layout == BH_LAYOUT_TILES_RGBM) {
+        constexpr uint32_t TE = rgbm_tile_elems<FMT>();
+        constexpr uint32_t CB = FMT == BH_OUT_RGBA32F ? 4u : FMT == BH_OUT_RGBA16F ? 2u : 1u;
+        store_px_planar<FMT, TE>(a.out_col, idx, col, tab + 256);
+        if (a.out_blackout) store_px_planar<FMT, TE>(a.out_blackout, idx, bo, tab + 256);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(zero);
+        if ((uint32_t)(idx & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) {
+            const size_t w = ((idx >> 6) * TE + 192u) * CB / 8u;  // the mask word (8-byte aligned)
+            reinterpret_cast<uint64_t*>(a.out_col)[w] = m;
+            if (a.out_blackout) reinterpret_cast<uint64_t*>(a.out_blackout)[w] = m;
+        }
     } else {
         store_px<FMT>(a.out_col, idx, col, tab + 256);
         if (a.out_blackout) store_px<FMT>(a.out_blackout, idx, bo, tab + 256);
@@ -751,15 +771,41 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
     }
 }
 
+// The per-frame fields of frame f of a multi-frame launch: its camera (read before and in the march
+// loop) and its outputs (read after it).
+__device__ __forceinline__ void select_camera(MarchArgs& a, const FrameArgs& F) {
+    for (int k = 0; k < 3; ++k) {
+        a.pos[k] = F.pos[k]; a.c0[k] = F.c0[k]; a.c1[k] = F.c1[k]; a.c2[k] = F.c2[k]; a.cps[k] = F.cps[k];
+    }
+}
+__device__ __forceinline__ void select_outputs(MarchArgs& a, const FrameArgs& F) {
+    a.out_col = F.out_col; a.out_blackout = F.out_blackout;
+    a.dbg_n_rk = F.dbg_n_rk; a.dbg_fate = F.dbg_fate; a.dbg_steps = F.dbg_steps;
+}
+
+// Several frames in one launch (bh_render_frames): dispatch slot s is tile s / n_frames of the order
+// in frame s % n_frames, so every frame's expensive tiles start first and one frame's serial tail
+// overlaps the others' bulk instead of ending the launch alone.  Only frame 0
+// records the tile costs for the next launch's order (the histogram must count each tile once).
 template <uint32_t FMT, uint32_t SF>
-__global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
+__global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs A) {
     __shared__ float lut[lds_tables<FMT>()];
-    load_tables<FMT>(a, lut);
+    load_tables<FMT>(A, lut);
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t slot = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (slot >= a.n_tiles) return;  // wave-uniform
-    const uint32_t t = a.order ? a.order[slot] : centre_out(slot, a.n_tiles, a.order_block, a.order_centre);
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t nf = A.n_frames;
+    if (slot >= A.n_tiles * nf) return;  // wave-uniform
+    uint32_t fi = 0, j = slot;
+    if (nf > 1u) {
+        j = slot / nf;
+        fi = slot - j * nf;
+    }
+    MarchArgs a = A;
+    select_camera(a, A.frames[fi]);  // frames[0] == the top-level fields for a one-frame launch
+    if (fi != 0u) a.tile_cost = nullptr;
+    const uint32_t t = a.order ? a.order[j] : centre_out(j, a.n_tiles, a.order_block, a.order_centre);
+    if (t >= a.n_tiles) return;  // defensive: a corrupt order must not address outside the shard
     uint32_t tx, ty;
     shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
     const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
@@ -809,6 +855,12 @@ __global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs a) {
             __shared__ HistLds hist[4];  // 16 KiB per workgroup: 8 workgroups per CU still fit
             fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
         }
+        // the frame's output pointers are loaded here, from an opaque copy of the frame index: loaded
+        // up front they would hold 10 SGPRs through the march loop, over the 80 that keep 8
+        // workgroups per CU resident (MI355X_MICROARCH.md, Residency)
+        uint32_t fo = fi;
+        asm volatile("" : "+s"(fo));
+        select_outputs(a, A.frames[fo]);
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
     if (a.tile_cost) {

@@ -20,7 +20,7 @@ namespace {
 template <uint32_t FMT>
 int launch(const bh::MarchArgs& a, uint32_t schedule, uint32_t* counters, uint32_t grid, hipStream_t s) {
     if (schedule == BH_SCHED_TILE) {
-        const uint32_t blocks = (a.n_tiles + 3u) / 4u;
+        const uint32_t blocks = (a.n_tiles * a.n_frames + 3u) / 4u;
         if (a.scene_flags == BH_SCENE_DEFAULT)  // the reference's scene: flags folded at compile time
             hipLaunchKernelGGL((bh::BH_NS::march_tile_kernel<FMT, BH_SCENE_DEFAULT>), dim3(blocks), dim3(256), 0, s, a);
         else

@@ -25,11 +25,19 @@ template <> struct PixelT<4> { using T = uint32_t; };
 
 // PLANAR: BH_LAYOUT_TILES_RGB of the format whose pixel is BPP bytes (three planes of 64 channel
 // values of BPP/4 bytes, alpha restored); else BH_LAYOUT_TILES (whole pixels, any format).
-template <uint32_t BPP, bool PLANAR>
+// MASK (with PLANAR): BH_LAYOUT_TILES_RGBM, each tile followed by its 64-bit blackout mask; `out_bo`
+// (nullable) receives blackout_col: the masked pixels as (0, 0, 0, alpha), the others as col.
+template <uint32_t BPP> __device__ __forceinline__ typename PixelT<BPP>::T zero_px();
+template <> __device__ __forceinline__ uint4 zero_px<16>() { return make_uint4(0u, 0u, 0u, __float_as_uint(1.0f)); }
+template <> __device__ __forceinline__ uint2 zero_px<8>() { return make_uint2(0u, 0x3C00u << 16); }
+template <> __device__ __forceinline__ uint32_t zero_px<4>() { return 0xFF000000u; }
+
+template <uint32_t BPP, bool PLANAR, bool MASK = false>
 __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __restrict__ packed, void* __restrict__ out,
-                                                           UnpackGrid u) {
+                                                           void* __restrict__ out_bo, UnpackGrid u) {
     using P = typename PixelT<BPP>::T;
-    constexpr uint32_t TW = PLANAR ? 12u * BPP : 16u * BPP;  // 32-bit words per packed tile
+    static_assert(PLANAR || !MASK, "the mask travels with the planar layout only");
+    constexpr uint32_t TW = PLANAR ? 12u * BPP + (MASK ? 2u : 0u) : 16u * BPP;  // 32-bit words per packed tile
     __shared__ uint32_t lds[UNPACK_SPAN * TW];
     __shared__ uint64_t gsrc[UNPACK_SPAN];  // packed tile of each output tile of the span
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -73,6 +81,12 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
             v = c[e] | ((uint32_t)c[64 + e] << 8) | ((uint32_t)c[128 + e] << 16) | 0xFF000000u;
         }
         reinterpret_cast<P*>(out)[(size_t)py * u.width + px] = v;
+        if constexpr (MASK) {
+            if (out_bo) {
+                const uint32_t mw = tile[12u * BPP + (e >> 5)];  // the mask word's half holding bit e
+                reinterpret_cast<P*>(out_bo)[(size_t)py * u.width + px] = ((mw >> (e & 31u)) & 1u) ? zero_px<BPP>() : v;
+            }
+        }
     }
     }
 }
@@ -142,7 +156,10 @@ __global__ void __launch_bounds__(ORDER_THREADS) order_scatter_kernel(const uint
     __syncthreads();
 #pragma unroll
     for (uint32_t j = 0; j < ORDER_PER_LANE; ++j)
-        if (b[j] < ORDER_BUCKETS) order[base[b[j]] + woff[w][b[j]] + r[j]] = t[j];
+        if (b[j] < ORDER_BUCKETS) {
+            const uint32_t pos = base[b[j]] + woff[w][b[j]] + r[j];
+            if (pos < n) order[pos] = t[j];  // defensive: a histogram that disagrees with the costs
+        }
     if (threadIdx.x == 0) {
         __threadfence();
         ticket = atomicAdd(&counters[2 * ORDER_BUCKETS], 1u);
@@ -177,32 +194,46 @@ static void unpack_launch_shape(uint32_t width, uint32_t height, uint32_t shard_
                  rows_in_flight && rows_in_flight < tiles_y ? rows_in_flight : tiles_y);
 }
 
-template <bool PLANAR>
-static int unpack_launch(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
-                         uint64_t stride_tiles, uint32_t bpp, uint32_t rows_in_flight, hipStream_t s) {
+template <bool PLANAR, bool MASK>
+static int unpack_launch(const void* packed, void* out, void* out_bo, uint32_t width, uint32_t height,
+                         uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp, uint32_t rows_in_flight,
+                         hipStream_t s) {
     bh::UnpackGrid u;
     dim3 grid, block(256);
     unpack_launch_shape(width, height, shard_count, stride_tiles, rows_in_flight, &u, &grid);
     const uint32_t* p = static_cast<const uint32_t*>(packed);
     switch (bpp) {
-        case 16: hipLaunchKernelGGL((bh::tiles_unpack_kernel<16, PLANAR>), grid, block, 0, s, p, out, u); break;
-        case 8: hipLaunchKernelGGL((bh::tiles_unpack_kernel<8, PLANAR>), grid, block, 0, s, p, out, u); break;
-        case 4: hipLaunchKernelGGL((bh::tiles_unpack_kernel<4, PLANAR>), grid, block, 0, s, p, out, u); break;
+        case 16: hipLaunchKernelGGL((bh::tiles_unpack_kernel<16, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
+        case 8: hipLaunchKernelGGL((bh::tiles_unpack_kernel<8, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
+        case 4: hipLaunchKernelGGL((bh::tiles_unpack_kernel<4, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }
 
+static uint32_t format_bpp(uint32_t format) {
+    return format == BH_OUT_RGBA32F ? 16u : format == BH_OUT_RGBA16F ? 8u : format == BH_OUT_BGRA8_SRGB ? 4u : 0u;
+}
+
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height,
                                       uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp,
                                       hipStream_t s) {
-    return unpack_launch<false>(packed, out, width, height, shard_count, stride_tiles, bpp, 0u, s);
+    return unpack_launch<false, false>(packed, out, nullptr, width, height, shard_count, stride_tiles, bpp, 0u, s);
 }
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,
                                                                               uint32_t height, uint32_t shard_count,
                                                                               uint64_t stride_tiles, uint32_t format,
                                                                               uint32_t rows_in_flight, hipStream_t s) {
-    const uint32_t bpp = format == BH_OUT_RGBA32F ? 16u : format == BH_OUT_RGBA16F ? 8u : format == BH_OUT_BGRA8_SRGB ? 4u : 0u;
-    return unpack_launch<true>(packed, out, width, height, shard_count, stride_tiles, bpp, rows_in_flight, s);
+    return unpack_launch<true, false>(packed, out, nullptr, width, height, shard_count, stride_tiles, format_bpp(format),
+                                      rows_in_flight, s);
+}
+
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo,
+                                                                               uint32_t width, uint32_t height,
+                                                                               uint32_t shard_count, uint64_t stride_tiles,
+                                                                               uint32_t format, uint32_t rows_in_flight,
+                                                                               hipStream_t s) {
+    return unpack_launch<true, true>(packed, out, out_bo, width, height, shard_count, stride_tiles, format_bpp(format),
+                                     rows_in_flight, s);
 }

@@ -83,6 +83,61 @@ def planar_to_packed(planar: np.ndarray, alpha) -> np.ndarray:
     return px.reshape(n * 64, 4)
 
 
+CHANNEL_BYTES = {0: 4, 1: 2, 2: 1}  # bh_out_format -> bytes per channel (RGBA32F, RGBA16F, BGRA8)
+
+
+def rgbm_tile_bytes(fmt: int) -> int:
+    """Bytes of one BH_LAYOUT_TILES_RGBM tile (include/bh_render.h): three planes of 64 channel values,
+    then the 64-bit blackout mask word."""
+    return 192 * CHANNEL_BYTES[fmt] + 8
+
+
+def pack_rgbm_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: int) -> np.ndarray:
+    """Host mirror of the march kernel's BH_LAYOUT_TILES_RGBM store for shard k: `col` (H, W, 4) in the
+    format's memory order (uint8 / float16 / float32 channels), `zero` (H, W) bool = the pixel's
+    blackout_col is 0 (dot(col, col) < 1 in fp32).  Returns (stride, tile_bytes) uint8; pixels outside
+    the frame are 0 and their mask bits clear."""
+    H, W, _ = col.shape
+    cb = col.dtype.itemsize
+    out = np.zeros((stride, 192 * cb + 8), np.uint8)
+    lane = np.arange(64)
+    for t, (tx, ty) in enumerate(shard_tiles(W, H, k, S)):
+        px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
+        ok = (px < W) & (py < H)
+        planes = np.zeros((3, 64), col.dtype)
+        planes[:, ok] = col[py[ok], px[ok], :3].T
+        out[t, :192 * cb] = planes.view(np.uint8).ravel()
+        zt = np.zeros(64, bool)
+        zt[ok] = zero[py[ok], px[ok]]
+        m = sum(1 << int(i) for i in lane[zt])
+        out[t, 192 * cb:] = np.frombuffer(np.uint64(m).tobytes(), np.uint8)
+    return out
+
+
+def unpack_rgbm_numpy(packed: np.ndarray, width: int, height: int, S: int, stride: int, dtype, alpha):
+    """Host mirror of bh_tiles_unpack_rgbm: gathered (S * stride, tile_bytes) uint8 -> (col, blackout),
+    each (height, width, 4) of `dtype` with the constant `alpha` restored; blackout = col with the
+    masked pixels' RGB zeroed."""
+    cb = np.dtype(dtype).itemsize
+    col = np.zeros((height, width, 4), dtype)
+    bo = np.zeros((height, width, 4), dtype)
+    lane = np.arange(64)
+    for k in range(S):
+        for t, (tx, ty) in enumerate(shard_tiles(width, height, k, S)):
+            tile = packed[k * stride + t]
+            planes = tile[:192 * cb].view(dtype).reshape(3, 64)
+            m = tile[192 * cb:].view(np.uint64)[0]
+            zero = ((m >> lane.astype(np.uint64)) & np.uint64(1)).astype(bool)
+            px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
+            ok = (px < width) & (py < height)
+            col[py[ok], px[ok], :3] = planes[:, ok].T
+            col[py[ok], px[ok], 3] = alpha
+            keep = ok & ~zero
+            bo[py[keep], px[keep], :3] = planes[:, keep].T
+            bo[py[ok], px[ok], 3] = alpha
+    return col, bo
+
+
 def gather_packed(packed, rank: int, world: int, gathered=None, group=None):
     """Gather every rank's packed tile buffer (same shape on all ranks) to rank 0.
 

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
-from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
+from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
                    BH_OUT_RGBA32F, BH_OUT_BGRA8_SRGB, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
 
 MAX_ITERATIONS = 1000  # src/black_hole_maybe.wgsl:85
@@ -194,15 +194,23 @@ def _ptr(t) -> int | None:
     return t.data_ptr()
 
 
-def _check_size(t, need: int, name: str) -> None:
+def tile_bytes(layout: int, fmt: int) -> int:
+    """Bytes of one 8x8 tile of a BH_LAYOUT_TILES* layout in format `fmt` (bh_tile_bytes)."""
+    n = load().bh_tile_bytes(layout, fmt)
+    if n < 0:
+        raise BhError(int(n), "bh_tile_bytes")
+    return int(n)
+
+
+def _check_size(t, need: int, name: str, what: str = "render") -> None:
     """Host-side bounds check of a caller buffer (tensor-like objects; raw pointers are trusted)."""
     if t is None or isinstance(t, int) or not hasattr(t, "element_size"):
         return
     have = t.numel() * t.element_size()
     if have < need:
-        raise BhError(_abi.BH_ERR_INVALID_ARG, f"render: {name} holds {have} bytes, the frame needs {need}")
+        raise BhError(_abi.BH_ERR_INVALID_ARG, f"{what}: {name} holds {have} bytes, needs {need}")
     if hasattr(t, "is_contiguous") and not t.is_contiguous():
-        raise BhError(_abi.BH_ERR_INVALID_ARG, f"render: {name} must be contiguous")
+        raise BhError(_abi.BH_ERR_INVALID_ARG, f"{what}: {name} must be contiguous")
 
 
 class Scene:
@@ -252,15 +260,8 @@ class Scene:
             self.camera = camera
         self.camera_uniform.update(self.camera)
 
-    def render(self, output, blackout_output=None, *, fmt: int = BH_OUT_RGBA32F, stream=None,
-               dbg_n_rk=None, dbg_fate=None, math: int | None = None, layout: int = BH_LAYOUT_ROWMAJOR,
-               shard_index: int = 0, shard_count: int = 1, width: int | None = None,
-               height: int | None = None, schedule: int = 0, dbg_steps=None) -> None:
-        """Scene::render (src/scene.rs:470-522): one pass writing `col` and optionally `blackout_col`.
-
-        `output`/`blackout_output`: caller-owned device buffers (torch tensors or raw pointers).
-        Asynchronous on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None = current).
-        """
+    def _desc(self, output, blackout_output, fmt, dbg_n_rk, dbg_fate, math, layout, shard_index, shard_count,
+              width, height, schedule, dbg_steps) -> _abi.bh_render_desc:
         if output is None:
             raise BhError(_abi.BH_ERR_INVALID_ARG, "render: output is required")
         if not self.render_blackout and blackout_output is not None:
@@ -272,12 +273,14 @@ class Scene:
         d.math = self.math if math is None else math
         d.layout, d.shard_index, d.shard_count = layout, shard_index, shard_count
         d.schedule = schedule
+        bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
         if layout == BH_LAYOUT_ROWMAJOR:
             px = d.width * d.height
+            col_bytes = px * bpp
         else:
-            px = shard_tile_count(d.width, d.height, shard_index, shard_count) * 64
-        bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
-        col_bytes = px * bpp * 3 // 4 if layout == BH_LAYOUT_TILES_RGB else px * bpp
+            nt = shard_tile_count(d.width, d.height, shard_index, shard_count)
+            px = nt * 64
+            col_bytes = nt * tile_bytes(layout, fmt) if bpp and layout <= BH_LAYOUT_TILES_RGBM else px * bpp
         _check_size(output, col_bytes, "output")
         _check_size(blackout_output, col_bytes, "blackout_output")
         _check_size(dbg_n_rk, px * 2, "dbg_n_rk")
@@ -285,9 +288,43 @@ class Scene:
         _check_size(dbg_steps, px * 2, "dbg_steps")
         d.out_col, d.out_blackout = _ptr(output), _ptr(blackout_output)
         d.dbg_n_rk, d.dbg_fate, d.dbg_steps = _ptr(dbg_n_rk), _ptr(dbg_fate), _ptr(dbg_steps)
+        return d
+
+    def render(self, output, blackout_output=None, *, fmt: int = BH_OUT_RGBA32F, stream=None,
+               dbg_n_rk=None, dbg_fate=None, math: int | None = None, layout: int = BH_LAYOUT_ROWMAJOR,
+               shard_index: int = 0, shard_count: int = 1, width: int | None = None,
+               height: int | None = None, schedule: int = 0, dbg_steps=None) -> None:
+        """Scene::render (src/scene.rs:470-522): one pass writing `col` and optionally `blackout_col`.
+
+        `output`/`blackout_output`: caller-owned device buffers (torch tensors or raw pointers).
+        Asynchronous on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None = current).
+        """
+        d = self._desc(output, blackout_output, fmt, dbg_n_rk, dbg_fate, math, layout, shard_index, shard_count,
+                       width, height, schedule, dbg_steps)
         check(self.lib.bh_render(self._ctx, C.byref(self.camera_uniform.c), C.byref(self.uniforms.to_c()),
                                  C.byref(d), _stream_handle(stream)), "bh_render")
 
+    def render_frames(self, outputs, blackout_outputs=None, *, cameras=None, fmt: int = BH_OUT_RGBA32F, stream=None,
+                      dbg_n_rk=None, dbg_fate=None, dbg_steps=None, math: int | None = None,
+                      layout: int = BH_LAYOUT_ROWMAJOR, shard_index: int = 0, shard_count: int = 1,
+                      width: int | None = None, height: int | None = None, schedule: int = 0) -> None:
+        """Several frames in one launch (bh_render_frames, up to BH_MAX_FRAMES): frame i renders with
+        cameras[i] (CameraUniform; default: this scene's camera for every frame) into outputs[i] /
+        blackout_outputs[i]; each frame's result is exactly render()'s."""
+        n = len(outputs)
+        if not 1 <= n <= _abi.BH_MAX_FRAMES:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, f"render_frames: 1..{_abi.BH_MAX_FRAMES} frames, got {n}")
+        per = lambda v: v if v is not None else [None] * n  # noqa: E731
+        bos, nrks, fates, steps = per(blackout_outputs), per(dbg_n_rk), per(dbg_fate), per(dbg_steps)
+        cams = cameras if cameras is not None else [self.camera_uniform] * n
+        if not (len(bos) == len(nrks) == len(fates) == len(steps) == len(cams) == n):
+            raise BhError(_abi.BH_ERR_INVALID_ARG, "render_frames: per-frame lists must have one entry per frame")
+        descs = (_abi.bh_render_desc * n)(*[self._desc(outputs[i], bos[i], fmt, nrks[i], fates[i], math, layout,
+                                                       shard_index, shard_count, width, height, schedule, steps[i])
+                                            for i in range(n)])
+        cu = (_abi.bh_camera_uniform * n)(*[c.c for c in cams])
+        check(self.lib.bh_render_frames(self._ctx, n, cu, C.byref(self.uniforms.to_c()), descs,
+                                        _stream_handle(stream)), "bh_render_frames")
 
     def bloom(self, col, blackout, out, *, levels: int = 3, schedule: int = 0, width: int | None = None,
               height: int | None = None, stream=None) -> None:
@@ -296,6 +333,9 @@ class Scene:
         the reference's (src/state.rs:125)."""
         if col is None or blackout is None or out is None:
             raise BhError(_abi.BH_ERR_INVALID_ARG, "bloom: col, blackout and out are required")
+        need = (width or self.width) * (height or self.height) * 4
+        for t, name in ((col, "col"), (blackout, "blackout"), (out, "out")):
+            _check_size(t, need, name, "bloom")
         check(self.lib.bh_bloom(self._ctx, _ptr(col), _ptr(blackout), width or self.width, height or self.height,
                                 levels, schedule, _ptr(out), _stream_handle(stream)), "bh_bloom")
 
@@ -314,8 +354,18 @@ def _stream_handle(stream) -> int | None:
     return stream.cuda_stream
 
 
+def _check_unpack(packed, outs, width, height, shard_count, shard_stride_tiles, packed_tile_bytes, out_bpp, what):
+    # shard k's tiles start at k * shard_stride_tiles: the last shard's block ends the buffer's use
+    last = shard_tile_count(width, height, shard_count - 1, shard_count) if shard_count >= 1 else 0
+    _check_size(packed, ((shard_count - 1) * shard_stride_tiles + last) * packed_tile_bytes, "packed", what)
+    for t, name in outs:
+        _check_size(t, width * height * out_bpp, name, what)
+
+
 def tiles_unpack(packed, out, width: int, height: int, shard_count: int, shard_stride_tiles: int,
                  bytes_per_pixel: int, stream=None) -> None:
+    _check_unpack(packed, [(out, "out")], width, height, shard_count, shard_stride_tiles, 64 * bytes_per_pixel,
+                  bytes_per_pixel, "tiles_unpack")
     check(load().bh_tiles_unpack(_ptr(packed), _ptr(out), width, height, shard_count, shard_stride_tiles,
                                  bytes_per_pixel, _stream_handle(stream)), "bh_tiles_unpack")
 
@@ -324,6 +374,9 @@ def tiles_unpack_rgb(packed, out, width: int, height: int, shard_count: int, sha
                      fmt: int, stream=None, rows_in_flight: int = 0) -> None:
     """bh_tiles_unpack_rgb(_rows): gathered BH_LAYOUT_TILES_RGB shards of format `fmt` -> row-major
     frame; rows_in_flight > 0 throttles it for overlap with a render (include/bh_render.h)."""
+    bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+    _check_unpack(packed, [(out, "out")], width, height, shard_count, shard_stride_tiles, 48 * bpp, bpp,
+                  "tiles_unpack_rgb")
     if rows_in_flight:
         check(load().bh_tiles_unpack_rgb_rows(_ptr(packed), _ptr(out), width, height, shard_count,
                                               shard_stride_tiles, fmt, rows_in_flight, _stream_handle(stream)),
@@ -333,8 +386,20 @@ def tiles_unpack_rgb(packed, out, width: int, height: int, shard_count: int, sha
                                          fmt, _stream_handle(stream)), "bh_tiles_unpack_rgb")
 
 
+def tiles_unpack_rgbm(packed, out_col, out_blackout, width: int, height: int, shard_count: int,
+                      shard_stride_tiles: int, fmt: int, stream=None, rows_in_flight: int = 0) -> None:
+    """bh_tiles_unpack_rgbm: gathered BH_LAYOUT_TILES_RGBM shards -> both Scene::render targets, row-major
+    (`out_blackout` None == Option::None)."""
+    bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+    _check_unpack(packed, [(out_col, "out_col"), (out_blackout, "out_blackout")], width, height, shard_count,
+                  shard_stride_tiles, tile_bytes(BH_LAYOUT_TILES_RGBM, fmt) if bpp else 0, bpp, "tiles_unpack_rgbm")
+    check(load().bh_tiles_unpack_rgbm(_ptr(packed), _ptr(out_col), _ptr(out_blackout), width, height, shard_count,
+                                      shard_stride_tiles, fmt, rows_in_flight, _stream_handle(stream)),
+          "bh_tiles_unpack_rgbm")
+
+
 __all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
-           "tiles_unpack_rgb",
+           "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM",
            "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_LAYOUT_TILES_RGB", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -28,9 +28,15 @@
  * Conventions: every function returns BH_OK (0) or a negative bh_status; nothing aborts or throws
  * across the ABI.  Output pointers are caller-owned DEVICE pointers (the reference's consumer, Bloom,
  * owns its textures and lends views: src/bloom.rs:31-37).  bh_render is asynchronous on the given
- * HIP stream (NULL = the legacy default stream) and performs no allocation or synchronisation, so a
- * caller may capture it into a hipGraph.  One bh_ctx per device; a ctx is not thread-safe, distinct
- * ctx objects may be used from distinct threads (one per rank).
+ * HIP stream (NULL = the legacy default stream) and never synchronises the host.  The tile
+ * schedule's temporal dispatch order keeps small per-(frame geometry, shard, stream) device buffers
+ * in the ctx: the FIRST bh_render of such a key allocates them (hipMalloc, not capturable); every
+ * later call with that key allocates nothing and may be captured into a hipGraph.  Those buffers
+ * are never freed or moved before bh_destroy (a captured graph keeps valid pointers), except that a
+ * ctx holds at most BH_ORDER_STATES keys and evicts the least recently used beyond that (re-capture
+ * graphs after rendering more keys than that).  Renders of one ctx on different streams use
+ * different order state, so they may run concurrently (frames in flight).  One bh_ctx per device; a
+ * ctx is not thread-safe, distinct ctx objects may be used from distinct threads (one per rank).
  */
 #ifndef BH_RENDER_H
 #define BH_RENDER_H
@@ -42,7 +48,10 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 1
+#define BH_ABI_VERSION 2
+
+/* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
+#define BH_ORDER_STATES 32
 
 typedef enum {
     BH_OK = 0,
@@ -113,10 +122,18 @@ typedef enum {
     BH_LAYOUT_TILES = 1,    /* the shard's 8x8 tiles packed in shard order, 64 pixels per tile,
                                pixel (x & 7) + 8 * (y & 7) inside a tile; pixels outside the frame
                                are left untouched */
-    BH_LAYOUT_TILES_RGB = 2 /* BH_LAYOUT_TILES without alpha (both targets' alpha is always 1,
+    BH_LAYOUT_TILES_RGB = 2, /* BH_LAYOUT_TILES without alpha (both targets' alpha is always 1,
                                src/black_hole_maybe.wgsl:369): each tile is three planes of 64
                                channel values in the format's memory order less alpha (R, G, B for
                                RGBA16F/RGBA32F; B, G, R for BGRA8), 3/4 of the bytes to gather */
+    BH_LAYOUT_TILES_RGBM = 3 /* BH_LAYOUT_TILES_RGB plus, after each tile's three planes, one 64-bit
+                               little-endian word whose bit i is set when pixel i of the tile has
+                               blackout_col == 0, i.e. dot(col, col) < 1 in fp32 (src/black_hole_maybe.wgsl:365-368):
+                               the multi-GPU transport.  blackout_col is a per-pixel function of the
+                               fp32 col, but not of its quantised RGBA16F / BGRA8 bytes, so the decision
+                               travels with them (0.125 B/pixel) and the gathered col alone restores both
+                               targets bit for bit (bh_tiles_unpack_rgbm).  Tile bytes: 776 (RGBA32F),
+                               392 (RGBA16F), 200 (BGRA8).  Schedules TILE and PAIR only. */
 } bh_layout;
 
 /* Work schedule of the march kernel (same results, different speed). */
@@ -213,6 +230,18 @@ int bh_destroy(bh_ctx* ctx);
 int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* uniforms,
               const bh_render_desc* desc, void* hip_stream);
 
+/* Several frames in ONE launch: n_frames (1..BH_MAX_FRAMES) calls of Scene::render -- e.g. consecutive
+ * frames of an offline camera path, cameras[i] for frame i -- with one `uniforms` and descs that agree in
+ * everything but their output and debug pointers (frame size, cap, scene, format, math, layout, shard,
+ * schedule; else BH_ERR_INVALID_ARG).  Each frame's results are exactly bh_render's.  With the tile
+ * schedule the frames' tiles are interleaved in one grid (slot s = tile s / n of frame s % n, most
+ * expensive tiles first), so the frames' serial tails -- the few rays that march to the cap -- overlap
+ * each other's bulk instead of each ending a launch alone; other schedules run n launches.  The
+ * temporal order of (geometry, shard, stream) learns from frame 0 of each call. */
+#define BH_MAX_FRAMES 8
+int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* cameras, const bh_uniforms* uniforms,
+                     const bh_render_desc* descs, void* hip_stream);
+
 /* Bloom::render (src/bloom.rs:53-71): the reference's Kawase bloom + remix chain over the scene's two
  * targets, on BGRA8-sRGB images (bh_render with BH_OUT_BGRA8_SRGB): `col` (full_image_input),
  * `blackout` (blackout_input) -> `out` (the surface), all width x height, row-major, device memory.
@@ -249,6 +278,16 @@ int bh_tiles_unpack_rgb(const void* packed, void* out_rowmajor, uint32_t width, 
 int bh_tiles_unpack_rgb_rows(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
                              uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
                              uint32_t rows_in_flight, void* hip_stream);
+
+/* Rank 0 of the multi-GPU frame: gathered BH_LAYOUT_TILES_RGBM shards of `format` -> BOTH targets of
+ * Scene::render (src/scene.rs:476-509), row-major: `out_col` (alpha restored) and, unless NULL
+ * (== Option::None), `out_blackout` = the tile mask's pixels zeroed (alpha kept), else col.  Equal
+ * bit for bit to a single-GPU two-target bh_render.  `rows_in_flight` as bh_tiles_unpack_rgb_rows. */
+int bh_tiles_unpack_rgbm(const void* packed, void* out_col, void* out_blackout, uint32_t width, uint32_t height,
+                         uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
+                         uint32_t rows_in_flight, void* hip_stream);
+/* Bytes of one tile of `layout` (BH_LAYOUT_TILES*) in `format`, or a negative bh_status. */
+int64_t bh_tile_bytes(uint32_t layout, uint32_t format);
 
 /* The BGRA8 sRGB encoder's threshold table: out[k] (k = 1..255) = the smallest float x with
  * encode(x) >= k, out[0] = 0, out[256] = +inf; encode(x) = the largest k with x >= out[k]. */

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     lib = bh.load()
-    assert lib.bh_abi_version() == 1
+    assert lib.bh_abi_version() == _abi.ABI_VERSION == 2
     assert lib.bh_status_string(0) == b"ok"
     assert lib.bh_status_string(-1) == b"invalid argument"
 
@@ -201,3 +201,59 @@ def test_load_sky_decodes_to_rgba8(tmp_path):
     j = bh.load_sky(tmp_path / "sky.jpg")
     assert j.shape == (64, 128, 4) and (j[..., 3] == 255).all()
     assert np.abs(j[..., :3].astype(int) - sky[..., :3]).mean() < 6  # lossy, but the same picture
+
+
+def test_tile_bytes_of_every_layout():
+    """include/bh_render.h: RGBM tiles are the three RGB planes plus one 8-byte blackout mask word."""
+    for fmt, bpp in bh.BYTES_PER_PIXEL.items():
+        assert bh.tile_bytes(bh.BH_LAYOUT_TILES, fmt) == 64 * bpp
+        assert bh.tile_bytes(bh.BH_LAYOUT_TILES_RGB, fmt) == 48 * bpp
+        assert bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt) == 48 * bpp + 8 == multigpu.rgbm_tile_bytes(fmt)
+        assert bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt) % 8 == 0  # the mask word stays 8-byte aligned
+    with pytest.raises(bh.BhError):
+        bh.tile_bytes(bh.BH_LAYOUT_ROWMAJOR, bh.BH_OUT_RGBA16F)
+    with pytest.raises(bh.BhError):
+        bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, 9)
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 8])
+@pytest.mark.parametrize("dtype,alpha", [(np.float16, 1.0), (np.float32, 1.0), (np.uint8, 255)])
+def test_rgbm_pack_unpack_mirror_restores_both_targets(S, dtype, alpha):
+    """Host mirrors of the RGBM transport (the march kernel's store, bh_tiles_unpack_rgbm): the gathered
+    shards restore col and blackout_col = col with the masked pixels zeroed, alpha restored; partial
+    tiles (100 x 52) included.  The mask is what makes blackout exact: it is decided on the fp32 col,
+    so a quantised col alone cannot always reproduce it."""
+    W, H = 100, 52
+    rng = np.random.default_rng(S)
+    col = rng.integers(0, 255, (H, W, 4)).astype(dtype) if dtype == np.uint8 else \
+        rng.random((H, W, 4)).astype(dtype)
+    col[..., 3] = alpha
+    zero = rng.random((H, W)) < 0.3
+    stride = multigpu.packed_stride(W, H, S)
+    packed = np.concatenate([multigpu.pack_rgbm_numpy(col, zero, k, S, stride) for k in range(S)])
+    assert packed.shape == (S * stride, multigpu.rgbm_tile_bytes({np.float32: 0, np.float16: 1, np.uint8: 2}[dtype]))
+    c, b = multigpu.unpack_rgbm_numpy(packed, W, H, S, stride, dtype, alpha)
+    want_b = col.copy()
+    want_b[zero, :3] = 0
+    assert np.array_equal(c.view(np.uint8), col.view(np.uint8))
+    assert np.array_equal(b.view(np.uint8), want_b.view(np.uint8))
+
+
+def test_scene_wrappers_reject_undersized_buffers():
+    """bloom and the unpack wrappers check buffer sizes on the host (a BhError, not an
+    out-of-bounds device access); numpy arrays stand in for device tensors (no launch happens)."""
+    torch = pytest.importorskip("torch")
+    small = torch.zeros(10, dtype=torch.uint8)
+    big = torch.zeros(1 << 16, dtype=torch.uint8)
+    with pytest.raises(bh.BhError, match="packed"):
+        bh.tiles_unpack_rgbm(small, big, None, 16, 16, 2, 4, bh.BH_OUT_BGRA8_SRGB)
+    with pytest.raises(bh.BhError, match="out_col"):
+        bh.tiles_unpack_rgbm(big, small, None, 16, 16, 2, 4, bh.BH_OUT_BGRA8_SRGB)
+    with pytest.raises(bh.BhError, match="out_blackout"):
+        bh.tiles_unpack_rgbm(big, big, small, 16, 16, 2, 4, bh.BH_OUT_BGRA8_SRGB)
+    with pytest.raises(bh.BhError, match="packed"):
+        bh.tiles_unpack_rgb(small, big, 16, 16, 2, 4, bh.BH_OUT_BGRA8_SRGB)
+    with pytest.raises(bh.BhError, match="out"):
+        bh.tiles_unpack(big, small, 16, 16, 2, 4, 4)
+    with pytest.raises(bh.BhError, match="must be contiguous"):
+        bh.tiles_unpack(big, big.view(256, 256).t(), 16, 16, 2, 4, 4)
