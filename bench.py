@@ -410,7 +410,7 @@ def main() -> int:
         achieved_tf = sum_steps * D * F_STEP[flags] / kern_avg_s / 1e12
         alg_bytes = my_bytes * D + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
-        pmc = _pmc_entry(W, H, cap, args, n)
+        pmc = _pmc_entry(W, H, cap, args, n, D)
         result = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -490,10 +490,15 @@ def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     return 8
 
 
-def _pmc_entry(W, H, cap, args, n):
+def pmc_key(W, H, cap, camera, math, schedule, fmt, n, D) -> str:
+    """Key of a configuration in profiles/pmc_traffic.json (tools/pmc_summary.py writes it)."""
+    return f"{W}x{H}_cap{cap}_{camera}_{math}_{schedule}_{fmt}_n{n}_D{D}"
+
+
+def _pmc_entry(W, H, cap, args, n, D):
     """This configuration's entry of profiles/pmc_traffic.json (rocprofv3 PMC passes), or {}."""
     p = ROOT / "profiles" / "pmc_traffic.json"
-    key = f"{W}x{H}_cap{cap}_{args.camera}_{args.math}_{args.schedule}_{args.fmt}" + (f"_n{n}" if n > 1 else "")
+    key = pmc_key(W, H, cap, args.camera, args.math, args.schedule, args.fmt, n, D)
     try:
         return json.loads(p.read_text()).get(key) or {}
     except (OSError, ValueError):
