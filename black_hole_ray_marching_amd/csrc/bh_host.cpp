@@ -611,16 +611,20 @@ int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_inde
     return (int64_t)bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, shard_index, shard_count);
 }
 
-// Which build of the exact kernels runs a frame (BH_SCHED_FLAG_ISSUE_ORDER / _LATENCY force one).  The
-// source-order build issues the bulk of the steps faster (headline 0.644 vs 0.687 ms), the machine-
-// scheduled one runs a lone wave's serial step chain faster (cap 1000: 0.82 vs 0.95 ms; 1920x1080:
-// 0.216 vs 0.253 ms).  A frame is throughput-bound when every CU has many tiles to issue while the
-// few capped waves march (>= 256 tiles per CU) and the cap keeps those waves' chains shorter than the
-// bulk (max_iters <= 512): A/B r01, DESIGN.md §5 item 8.
-static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles, uint32_t cus) {
+// Which build of the exact kernels runs a launch (BH_SCHED_FLAG_ISSUE_ORDER / _LATENCY force one).  The
+// source-order build issues the bulk of the steps faster; the machine-scheduled one, whose tail loop
+// also runs the packed step, marches a lone wave's serial chain faster.  A launch is throughput-bound
+// when its tiles in flight (all frames') outlast the capped rays' chains: about 384 tiles per CU at
+// cap 512 (the bulk runs ~1.2 us per tile and CU, a cap-512 chain ~0.45 ms), scaled by the cap.
+// Measured (A/B r02, profiles/r02/variants.log, ms per frame, source-order / scheduled): 4096x2048
+// cap 512 one frame (512 tiles/CU) 0.644 / 0.687; its 1/8 shard 0.445 / 0.363; 8192x4096's 1/8 shard
+// 0.61 / 0.39; cap 1000 camera C 0.957 / 0.737; 1920x1080 cap 256 0.253 / 0.205; in 8-frame launches
+// cap 1000 0.669 / 0.698, 1920x1080 0.165 / 0.171, 8192x4096's 1/8 shard 0.322 / 0.337.
+static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles, uint32_t n_frames, uint32_t cus) {
     if (d->schedule & BH_SCHED_FLAG_ISSUE_ORDER) return true;
     if (d->schedule & BH_SCHED_FLAG_LATENCY) return false;
-    return d->max_iters <= 512u && (uint64_t)n_tiles >= 256ull * (cus ? cus : 256u);
+    const uint64_t tiles = (uint64_t)n_tiles * n_frames;
+    return tiles * 512ull >= 384ull * (cus ? cus : 256u) * d->max_iters;
 }
 
 // The temporal-order state of (geometry, shard, stream): found, or created (allocating; the LRU state
@@ -770,7 +774,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
         a.order_tot = os->counters;
     }
     int e = d->math != BH_MATH_EXACT ? bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s)
-            : march_variant_issue_order(d, a.n_tiles, c->cus)
+            : march_variant_issue_order(d, a.n_tiles, a.n_frames, c->cus)
                 ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
                 : bh_launch_march_exact_lat(a, sched, c->counters, c->grid_exact, s);
     if (prev != c->device) (void)hipSetDevice(prev);

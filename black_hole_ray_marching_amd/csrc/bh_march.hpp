@@ -492,6 +492,143 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
 __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 #endif
 
+#ifndef BH_TAIL_PACKED
+#define BH_TAIL_PACKED 0
+#endif
+#if !BH_FAST && BH_TAIL_PACKED
+// ---- the tail's step, in packed FP32 (exact mode) ---------------------------------------------------
+// The same arithmetic as step_bf<true, XOps<true>> -- every rounding identical, in the same order, the
+// same guards -- with the x and y components of each vector in one 64-bit register pair, so that one
+// v_pk_{add,mul,fma}_f32 does both.  It runs only in the cycle-watch loop (march_cycles), i.e. in waves
+// still marching after PRIO_ITERS iterations, which are few per SIMD: a wave alone issues a packed op
+// in the slot of a scalar one (tools/ubench/lone_wave.hip: 4.6 vs 4.7 cycles, profiles/r02/lone_wave.log),
+// so the tail's serial step chain gets shorter; at 8 waves per SIMD a packed op costs more than two
+// scalar ones (5.7 vs 2 x 2.3 cycles), so the bulk keeps the scalar step.
+typedef float f2 __attribute__((ext_vector_type(2)));
+struct p3 { f2 xy; float z; };
+__device__ __forceinline__ p3 pk(v3 a) { return {f2{a.x, a.y}, a.z}; }
+__device__ __forceinline__ v3 unpk(p3 a) { return mk(a.xy.x, a.xy.y, a.z); }
+__device__ __forceinline__ f2 bc(float s) { return f2{s, s}; }
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ p3 padd(p3 a, p3 b) { return {a.xy + b.xy, a.z + b.z}; }
+__device__ __forceinline__ p3 psub(p3 a, p3 b) { return {a.xy - b.xy, a.z - b.z}; }
+__device__ __forceinline__ p3 psmul(float s, p3 a) { return {bc(s) * a.xy, s * a.z}; }  // s*x == x*s
+// dot(a, b) = (a.x*b.x + a.y*b.y) + a.z*b.z
+__device__ __forceinline__ float pdot(p3 a, p3 b) {
+    const f2 m = a.xy * b.xy;
+    return (m.x + m.y) + a.z * b.z;
+}
+// div_core of the three components by one refined reciprocal
+__device__ __forceinline__ p3 pdiv(p3 n, const crm::Rcp& R) {
+    const p3 y{n.xy * bc(R.r), n.z * R.r};
+    const p3 e{pfma(bc(R.d), y.xy, -n.xy), __builtin_fmaf(R.d, y.z, -n.z)};
+    return {pfma(-e.xy, bc(R.r), y.xy), __builtin_fmaf(-e.z, R.r, y.z)};
+}
+__device__ __forceinline__ p3 pdiv6(p3 x) {
+    constexpr float R6 = 1.0f / 6.0f;
+    const p3 y{x.xy * bc(R6), x.z * R6};
+    const p3 e{pfma(y.xy, bc(6.0f), -x.xy), __builtin_fmaf(y.z, 6.0f, -x.z)};
+    return {pfma(-e.xy, bc(R6), y.xy), __builtin_fmaf(-e.z, R6, y.z)};
+}
+__device__ __forceinline__ p3 padd2(p3 a, p3 b) {  // a + 2b, as XOps<true>::add2
+    return {pfma(bc(2.0f), b.xy, a.xy), __builtin_fmaf(2.0f, b.z, a.z)};
+}
+
+struct PkGuard {
+    bool bad = false;
+    uint32_t kmin;
+    float amin, amin6;
+};
+
+// rd_derivative as XOps<true>::accel_qs<K>
+template <int K>
+__device__ __forceinline__ p3 paccel_qs(p3 p, float s, float q, float sq, PkGuard& G) {
+    const float Q = (q * q) * sq;
+    const p3 n = psmul(s, p);
+    G.bad |= crm::div_d_bad(Q);
+    if constexpr (K == 1) G.kmin = crm::kmin3(crm::key(n.xy.x), crm::key(n.xy.y), crm::key(n.z));
+    else if constexpr (K == 2) G.amin = XOps<true>::absmin3(n.xy.x, n.xy.y, n.z);
+    else G.amin = XOps<true>::absmin3(G.amin, n.xy.x, n.xy.y, n.z);
+    return pdiv(n, crm::rcp_refined(Q));
+}
+template <int K>
+__device__ __forceinline__ p3 paccel(p3 p, float s, PkGuard& G) {
+    const float q = pdot(p, p);
+    return paccel_qs<K>(p, s, q, crm::sqrt_core(q), G);
+}
+
+// step_bf<true, XOps<true>, SF> with packed pairs (see above): same contract (`out` is not written for
+// the fates decided before the RK update), `G.bad` set when an operand left a core's domain.
+template <uint32_t SF>
+__device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
+                                          PkGuard& G, uint32_t& fate) {
+    const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
+    const p3 ro = pk(in.ro), rd = pk(in.rd);
+    const float travelled = in.travelled, s = in.s;
+    const uint32_t n_rk = in.n_rk;
+    const f2 sq_xy = ro.xy * ro.xy;                 // x*x, y*y
+    const float zz0 = ro.z * ro.z;
+    const float r2 = (sq_xy.x + sq_xy.y) + zz0;     // dot(ro, ro)
+    const float r = crm::sqrt_core(r2);
+    const bool bo_on = a.blackout_eh != 0u;
+    const bool not_out = !(r2 > R2_GT1);
+    bool ingoing = false;
+    if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = pdot(rd, ro) < 0.0f;
+    const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
+    // sdf (XOps::sdf): disc from rho^2 = x*x + z*z, markers from the near sphere of each pair
+    const float rho2 = sq_xy.x + zz0;
+    const float rho = crm::sqrt_core(rho2);
+    const float disc = fmaxf(fmaxf(rho - 6.0f * a.rs, -(rho - 3.0f * a.rs)), fabsf(ro.xy.y - 0.0f) - 0.02f);
+    const float dz = -10.0f - ro.z, zz = dz * dz;
+    const f2 t{10.0f - fabsf(ro.xy.x), 10.0f - fabsf(ro.xy.y)};  // (tx, ty)
+    const f2 t2 = t * t;                                            // (tx*tx, ty*ty)
+    // (qy, qx) = ((xx + ty*ty) + zz, (yy + tx*tx) + zz); tx*tx + yy == yy + tx*tx exactly
+    const f2 qyx = (sq_xy + t2.yx) + bc(zz);
+    const float qm = fminf(qyx.x, qyx.y);
+    const float m = crm::sqrt_core(qm) - 0.5f;
+    const float ds = fminf((scene_flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
+                           (scene_flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
+    G.bad |= crm::sqrt_bad2(rho2, qm);
+    const bool surface = ds < MIN_DIST;
+    if (blackout | surface) {
+        fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+        return true;
+    }
+    const p3 dc = psub(pk(f.cps), ro);
+    const float qps = pdot(dc, dc);
+    const float dps = crm::sqrt_core(qps) - 0.075f;
+    G.bad |= crm::sqrt_bad(qps);
+    const float dist = fminf(ds, dps);
+    const float dt = fminf(dist * 0.9f, a.dtm * r);
+    const p3 ro_k1 = psmul(dt, rd);
+    const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, G));
+    const p3 ro_k2 = psmul(dt, padd(rd, psmul(0.5f, rd_k1)));
+    const p3 rd_k2 = psmul(dt, paccel<2>(padd(ro, psmul(0.5f, ro_k1)), s, G));
+    const p3 ro_k3 = psmul(dt, padd(rd, psmul(0.5f, rd_k2)));
+    const p3 rd_k3 = psmul(dt, paccel<3>(padd(ro, psmul(0.5f, ro_k2)), s, G));
+    const p3 ro_k4 = psmul(dt, padd(rd, rd_k3));
+    const p3 rd_k4 = psmul(dt, paccel<4>(padd(ro, ro_k3), s, G));
+    const p3 sro = padd(padd2(padd2(ro_k1, ro_k2), ro_k3), ro_k4);
+    const p3 srd = padd(padd2(padd2(rd_k1, rd_k2), rd_k3), rd_k4);
+    G.amin6 = XOps<true>::absmin3(XOps<true>::absmin3(sro.xy.x, sro.xy.y, sro.z), srd.xy.x, srd.xy.y, srd.z);
+    const p3 dro = pdiv6(sro), drd = pdiv6(srd);
+    G.bad |= G.kmin < crm::KEY_MIN;
+    G.bad |= !(G.amin >= crm::DIV_N_MIN);
+    G.bad |= !(G.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
+    G.bad |= !(fabsf(s) <= 0x1p30f);
+    const float ntr = travelled + dt;
+    out.s = s;
+    out.outside = not_out ? in.outside : 1u;
+    out.ro = unpk(padd(ro, dro));
+    out.rd = unpk(padd(rd, drd));
+    out.travelled = ntr;
+    out.n_rk = n_rk + 1u;
+    const bool escape = ntr > a.max_dist;
+    fate = escape ? (uint32_t)BH_FATE_ESCAPE : (uint32_t)BH_FATE_CAP;
+    return escape | (n_rk + 1u >= a.max_iters);
+}
+#endif
+
 // One iteration for one ray from `in` into `out` (step_bf<true> contract: `out` is not written for
 // fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
 template <uint32_t SF = SF_DYN>
@@ -520,8 +657,34 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
 #endif
 }
 
-// One iteration for one ray in place (persistent schedule, the tile schedule's cycle watch):
-// BH_FATE_* if the ray terminates, else 0xFF.
+// One iteration of a tail wave (the tile schedule's cycle watch), in place: BH_FATE_* if the ray
+// terminates, else 0xFF.  The latency build of the exact kernels (BH_TAIL_PACKED, bh_march_exact_lat.hip)
+// runs the packed step, with the same rare IEEE re-run: a lone tail wave's step 0.89 -> 0.79 us, config
+// 5 (one frame, cap 1000) 0.824 -> 0.734 ms.  The issue-order build keeps the scalar step: in
+// multi-frame launches the tail waves share their SIMDs with other frames' bulk, where a packed op
+// costs more than two scalar ones, and the packed tail measured 0.4 % slower there (A/B r02,
+// profiles/r02/ab_tail.log).
+template <uint32_t SF = SF_DYN>
+__device__ __forceinline__ uint32_t march_step_tail(const MarchArgs& a, const Frame& f, RayState& st) {
+#if BH_FAST || !BH_TAIL_PACKED
+    RayState t = st;
+    uint32_t fate;
+    const bool done = march_step_io<SF>(a, f, st, t, fate);
+#else
+    RayState t = st;
+    uint32_t fate;
+    PkGuard G;
+    bool done = step_tail<SF>(a, f, st, t, G, fate);
+    if (__builtin_expect(G.bad, 0)) {
+        XOps<false> Y;
+        done = step_bf<true, XOps<false>, SF>(a, f, st, t, Y, fate);
+    }
+#endif
+    st = t;
+    return done ? fate : 0xFFu;
+}
+
+// One iteration for one ray in place (persistent schedule): BH_FATE_* if the ray terminates, else 0xFF.
 template <uint32_t SF = SF_DYN>
 __device__ __forceinline__ uint32_t march_step(const MarchArgs& a, const Frame& f, RayState& st) {
     // t = st / st = t rather than a select on the fate: the copies fill the tail waves' dependency
@@ -752,7 +915,7 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
         H.a[p][0][lane] = make_float4(st.ro.x, st.ro.y, st.ro.z, st.travelled);
         H.a[p][1][lane] = make_float4(st.rd.x, st.rd.y, st.rd.z, __uint_as_float(st.outside));
         h1 = state_hash(st);
-        const uint32_t fate = march_step<SF>(a, f, st);
+        const uint32_t fate = march_step_tail<SF>(a, f, st);
         if (fate != 0xFFu) { steps = st.n_rk; return fate; }
         if (state_hash(st) == h2) {
             const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];

@@ -147,8 +147,9 @@ typedef enum {
 /* OR into `schedule` to use the static centre-out order only (no per-tile cost feedback). */
 #define BH_SCHED_FLAG_STATIC_ORDER 0x100u
 /* Exact math: which build of the march kernels runs (same bits either way).  By default bh_render
- * picks per frame: the source-order build when the frame is throughput-bound (>= 256 tiles per CU
- * and max_iters <= 512), else the machine-scheduled build, whose lone tail waves step faster.
+ * picks per launch: the source-order build when it is throughput-bound (its tiles in flight, over
+ * all frames of a bh_render_frames launch, >= 384 per CU x max_iters / 512), else the
+ * machine-scheduled build, whose lone tail waves step faster (packed-FP32 tail step).
  * These flags force one (BH_SCHED_FLAG_ISSUE_ORDER wins if both are set). */
 #define BH_SCHED_FLAG_ISSUE_ORDER 0x200u
 #define BH_SCHED_FLAG_LATENCY 0x400u

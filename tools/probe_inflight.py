@@ -22,12 +22,14 @@ def main():
     p.add_argument("--modes", default="streams,batch")
     p.add_argument("--cap", type=int, default=512)
     p.add_argument("--k", type=int, default=96)
+    p.add_argument("--variant", choices=["auto", "issue", "latency"], default="auto")
     args = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
     dev = torch.device("cuda:0")
     sky = bh.synthetic_sky()
     fmt = bh.BH_OUT_RGBA16F
+    sched = {"auto": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[args.variant]
     for fr in args.frames.split(","):
         W, H = map(int, fr.split("x"))
         scene = bh.Scene(W, H, sky=sky, max_iters=args.cap, math=bh.BH_MATH_EXACT)
@@ -49,11 +51,11 @@ def main():
                         if mode == "streams":
                             for i in range(k):
                                 c, b = bufs[i % D]
-                                scene.render(c, b, fmt=fmt, stream=streams[i % D], **kw)
+                                scene.render(c, b, fmt=fmt, stream=streams[i % D], schedule=sched, **kw)
                         else:
                             for _ in range(0, k, D):
                                 scene.render_frames([c for c, _ in bufs], None if S > 1 else [b for _, b in bufs],
-                                                    fmt=fmt, stream=streams[0], **kw)
+                                                    fmt=fmt, stream=streams[0], schedule=sched, **kw)
 
                     run(4 * D + 8)
                     torch.cuda.synchronize()
@@ -62,7 +64,7 @@ def main():
                     run(k)
                     torch.cuda.synchronize()
                     ms = (time.perf_counter() - t0) / k * 1e3
-                    print(json.dumps({"frame": fr, "S": S, "mode": mode, "depth": D, "ms_per_frame": round(ms, 4),
+                    print(json.dumps({"frame": fr, "S": S, "mode": mode, "variant": args.variant, "depth": D, "ms_per_frame": round(ms, 4),
                                       "frame_Mpix_per_s": round(W * H / ms / 1e3, 1)}), flush=True)
         scene.close()
 
