@@ -25,6 +25,8 @@ def load() -> C.CDLL:
                                         C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                         C.c_int]
+        lib.bho_render_rows_variant.restype = C.c_int
+        lib.bho_render_rows_variant.argtypes = lib.bho_render_rows.argtypes + [C.c_uint32]
         lib.bho_trace_ray.restype = C.c_int
         lib.bho_trace_ray.argtypes = [C.c_float * 3, C.c_float * 3, C.c_void_p, C.c_void_p, C.c_uint32,
                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_float * 3,
@@ -45,9 +47,10 @@ def load() -> C.CDLL:
 
 def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: int, height: int,
                 max_iters: int, scene_flags: int, row0: int = 0, row1: int | None = None,
-                threads: int = 0, blackout: bool = True, row_step: int = 1):
+                threads: int = 0, blackout: bool = True, row_step: int = 1, variant: int = 0):
     """Oracle render of rows row0, row0+row_step, ... < row1.  camera_uniform/uniforms: the
-    112-/32-byte ABI structs.
+    112-/32-byte ABI structs.  variant: 0 = the normative arithmetic (every parity test); else
+    V_* bits, the parity-envelope variants of DESIGN.md §3 (what a real WGSL driver may do instead).
 
     Returns (col (R,W,4) f32, blackout (R,W,4) f32 or None, n_rk (R,W) u16, fate (R,W) u8).
     """
@@ -61,12 +64,17 @@ def render_rows(camera_uniform: bytes, uniforms: bytes, sky: np.ndarray, width: 
     fate = np.empty((rows, width), np.uint8)
     cam = C.create_string_buffer(bytes(camera_uniform), 112)
     uni = C.create_string_buffer(bytes(uniforms), 32)
-    st = lib.bho_render_rows(cam, uni, sky.ctypes.data, sky.shape[1], sky.shape[0], width, height, max_iters,
-                             scene_flags, row0, row1, row_step, col.ctypes.data, bo.ctypes.data if bo is not None else None,
-                             n_rk.ctypes.data, fate.ctypes.data, threads)
+    args = (cam, uni, sky.ctypes.data, sky.shape[1], sky.shape[0], width, height, max_iters,
+            scene_flags, row0, row1, row_step, col.ctypes.data, bo.ctypes.data if bo is not None else None,
+            n_rk.ctypes.data, fate.ctypes.data, threads)
+    st = lib.bho_render_rows_variant(*args, variant) if variant else lib.bho_render_rows(*args)
     if st != 0:
         raise ValueError(f"bho_render_rows failed: {st}")
     return col, bo, n_rk, fate
+
+
+# parity-envelope variants (oracle/bh_oracle.c BHO_V_*)
+V_POW_EXP2LOG2, V_TEX_8BIT, V_TEX_NEAREST, V_ATAN2F = 1, 2, 4, 8
 
 
 def trace_ray(ro0, rd0, uniforms: bytes, sky: np.ndarray, max_iters: int, scene_flags: int):

@@ -50,6 +50,18 @@ static inline v3 cross(v3 a, v3 b) {
 static inline float pow25(float q) { return (q * q) * sqrtf(q); }
 static inline float pow15(float c) { return c * sqrtf(c); }
 
+/* Parity-envelope variants (bho_render_rows_variant; DESIGN.md §3 "Parity envelope"): choices a real
+ * WGSL implementation may make where WGSL leaves precision to the implementation, instead of the
+ * normative ones above.  0 = normative (what every parity test uses). */
+#define BHO_V_POW_EXP2LOG2 1u /* pow(x, e) = exp2(e * log2(x)) in f32 (how GPU compilers lower pow) */
+#define BHO_V_TEX_8BIT 2u     /* bilinear weights quantised to 8 fractional bits (texture units) */
+#define BHO_V_TEX_NEAREST 4u  /* LOD 0 treated as minification: min_filter = Nearest (src/texture.rs:66-67) */
+#define BHO_V_ATAN2F 8u       /* atan2 evaluated in f32 (libm atan2f) */
+static inline float powv(float x, float e, uint32_t variant) {
+    if (!(variant & BHO_V_POW_EXP2LOG2)) return e == 2.5f ? pow25(x) : pow15(x);
+    return x > 0.0f ? exp2f(e * log2f(x)) : (x == 0.0f ? 0.0f : NAN);
+}
+
 /* constants, src/black_hole_maybe.wgsl:80-85 (abstract floats rounded to f32 at use) */
 #define MIN_DIST 0.001f
 #define TWO_PI 6.28318530718f
@@ -60,6 +72,7 @@ typedef struct {
     uint32_t BLACKOUT_EH;
     uint32_t flags;
     uint32_t max_iters;
+    uint32_t variant;  /* BHO_V_* (0 = normative) */
 } params;
 
 /* sdf_sphere, :91-93 — length(centre - p) - r */
@@ -98,7 +111,7 @@ static inline float sdf(const params* P, v3 p) {
 /* rd_derivative, :125-127 — ((((DP * RS) * -1.5) * h2) * ro) / pow(dot(ro, ro), 2.5) */
 static inline v3 rd_derivative(const params* P, v3 ro, float h2) {
     float s = ((P->DP * P->RS) * -1.5f) * h2;
-    return divs(smul(s, ro), pow25(dot(ro, ro)));
+    return divs(smul(s, ro), powv(dot(ro, ro), 2.5f, P->variant));
 }
 /* get_delta_photon_rk4, :134-151 */
 static inline void rk4(const params* P, v3 ro, v3 rd, float dt, float h2, v3* dro, v3* drd) {
@@ -118,6 +131,7 @@ typedef struct {
     const uint8_t* tex;
     uint32_t w, h;
     float lut[256];
+    uint32_t variant;  /* BHO_V_TEX_* */
 } sky_t;
 
 /* Rgba8UnormSrgb texel fetch + decode (src/texture.rs:41) */
@@ -130,12 +144,18 @@ static inline int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo 
 /* textureSampleLevel(t_diffuse, s_diffuse, uv, 0.0).xyz with the sampler of src/texture.rs:62-70 */
 static v3 sample_bilinear(const sky_t* S, float u, float v) {
     if (u != u || v != v) return texel(S, 0, 0); /* Q8 */
+    if (S->variant & BHO_V_TEX_NEAREST) {
+        int32_t nx = (int32_t)floorf(fminf(fmaxf(u, 0.0f), 1.0f) * (float)S->w);
+        int32_t ny = (int32_t)floorf(fminf(fmaxf(v, 0.0f), 1.0f) * (float)S->h);
+        return texel(S, clampi(nx, 0, (int32_t)S->w - 1), clampi(ny, 0, (int32_t)S->h - 1));
+    }
     float tx = u * (float)S->w - 0.5f;
     float ty = v * (float)S->h - 0.5f;
     tx = fminf(fmaxf(tx, -1.0f), (float)S->w);
     ty = fminf(fmaxf(ty, -1.0f), (float)S->h);
     float fx0 = floorf(tx), fy0 = floorf(ty);
     float a = tx - fx0, b = ty - fy0;
+    if (S->variant & BHO_V_TEX_8BIT) { a = rintf(a * 256.0f) / 256.0f; b = rintf(b * 256.0f) / 256.0f; }
     int32_t x0 = (int32_t)fx0, y0 = (int32_t)fy0;
     int32_t x1 = clampi(x0 + 1, 0, (int32_t)S->w - 1), y1 = clampi(y0 + 1, 0, (int32_t)S->h - 1);
     x0 = clampi(x0, 0, (int32_t)S->w - 1);
@@ -188,12 +208,13 @@ static v3 get_col_state(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_
     FINAL();
 #undef FINAL
     v3 n = normalize(rd);                                       /* :330 */
-    float az = (float)atan2((double)n.z, (double)n.x);          /* :332 */
+    float az = (P->variant & BHO_V_ATAN2F) ? atan2f(n.z, n.x)
+                                           : (float)atan2((double)n.z, (double)n.x); /* :332 */
     float x = (az + ONE_PI) / TWO_PI;                           /* :334 */
     float y = (n.y + 1.0f) * 0.5f;                              /* :336 */
     v3 col = sample_bilinear(S, x, 1.0f - y);                   /* :341 */
-    col.y = pow15(col.y);                                       /* :342 */
-    col.z = pow15(col.z);                                       /* :343 */
+    col.y = powv(col.y, 1.5f, P->variant);                      /* :342 */
+    col.z = powv(col.z, 1.5f, P->variant);                      /* :343 */
     return col;
 }
 static v3 get_col(const params* P, const sky_t* S, v3 ro0, v3 rd0, uint32_t* n_rk, uint32_t* fate) {
@@ -273,7 +294,7 @@ int bho_screen_tri_is_default(const bh_camera_uniform* cam) {
  * n_rk (u16) / fate (u8): one per pixel, may be NULL.  threads <= 0: OpenMP default.
  * Returns 0, or -1 on invalid arguments.
  */
-int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
+static int render_rows_v(uint32_t variant, const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
                     uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
                     uint32_t max_iters, uint32_t scene_flags, uint32_t row0, uint32_t row1,
                     uint32_t row_step, float* out_col, float* out_blackout, uint16_t* n_rk, uint8_t* fate,
@@ -284,9 +305,9 @@ int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     if (!bho_screen_tri_is_default(cam)) return -2;
     params P;
     P.RS = U->rs; P.DTM = U->delta_time_mult; P.MAX_DIST = U->max_dist; P.DP = U->distortion_power;
-    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters;
+    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters; P.variant = variant;
     sky_t S;
-    S.tex = sky; S.w = sky_w; S.h = sky_h;
+    S.tex = sky; S.w = sky_w; S.h = sky_h; S.variant = variant;
     bho_srgb_lut(S.lut);
     v3 ro0 = mk(cam->pos[0], cam->pos[1], cam->pos[2]);
     if (row_step == 0) row_step = 1;
@@ -320,6 +341,23 @@ int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     return 0;
 }
 
+int bho_render_rows(const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
+                    uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
+                    uint32_t max_iters, uint32_t scene_flags, uint32_t row0, uint32_t row1,
+                    uint32_t row_step, float* out_col, float* out_blackout, uint16_t* n_rk, uint8_t* fate,
+                    int threads) {
+    return render_rows_v(0u, cam, U, sky, sky_w, sky_h, width, height, max_iters, scene_flags, row0, row1, row_step, out_col, out_blackout, n_rk, fate, threads);
+}
+
+/* bho_render_rows with a parity-envelope variant (BHO_V_* bits; test infrastructure for DESIGN.md §3). */
+int bho_render_rows_variant(const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
+                    uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
+                    uint32_t max_iters, uint32_t scene_flags, uint32_t row0, uint32_t row1,
+                    uint32_t row_step, float* out_col, float* out_blackout, uint16_t* n_rk, uint8_t* fate,
+                    int threads, uint32_t variant) {
+    return render_rows_v(variant, cam, U, sky, sky_w, sky_h, width, height, max_iters, scene_flags, row0, row1, row_step, out_col, out_blackout, n_rk, fate, threads);
+}
+
 /* Trace one pixel (debug/KAT helper): writes final ro, rd (6 floats) too. */
 int bho_trace_pixel(const bh_camera_uniform* cam, const bh_uniforms* U, const uint8_t* sky,
                     uint32_t sky_w, uint32_t sky_h, uint32_t width, uint32_t height,
@@ -328,9 +366,9 @@ int bho_trace_pixel(const bh_camera_uniform* cam, const bh_uniforms* U, const ui
     if (px >= width || py >= height) return -1;
     params P;
     P.RS = U->rs; P.DTM = U->delta_time_mult; P.MAX_DIST = U->max_dist; P.DP = U->distortion_power;
-    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters;
+    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters; P.variant = 0;
     sky_t S;
-    S.tex = sky; S.w = sky_w; S.h = sky_h;
+    S.tex = sky; S.w = sky_w; S.h = sky_h; S.variant = 0;
     bho_srgb_lut(S.lut);
     v3 ro0 = mk(cam->pos[0], cam->pos[1], cam->pos[2]);
     v3 rd0 = normalize(pixel_dir(cam, width, height, px, py));
@@ -346,9 +384,9 @@ int bho_trace_ray(const float ro0_in[3], const float rd0_in[3], const bh_uniform
                   uint32_t scene_flags, float out_rgb[3], uint32_t* n_rk, uint32_t* fate, float* out_state) {
     params P;
     P.RS = U->rs; P.DTM = U->delta_time_mult; P.MAX_DIST = U->max_dist; P.DP = U->distortion_power;
-    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters;
+    P.BLACKOUT_EH = U->blackout_eh; P.flags = scene_flags; P.max_iters = max_iters; P.variant = 0;
     sky_t S;
-    S.tex = sky; S.w = sky_w; S.h = sky_h;
+    S.tex = sky; S.w = sky_w; S.h = sky_h; S.variant = 0;
     bho_srgb_lut(S.lut);
     v3 col = get_col_state(&P, &S, mk(ro0_in[0], ro0_in[1], ro0_in[2]), mk(rd0_in[0], rd0_in[1], rd0_in[2]),
                            n_rk, fate, out_state);

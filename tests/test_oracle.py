@@ -219,3 +219,29 @@ def test_marker_pair_reduction():
     both_nan = np.isnan(got) & np.isnan(ref)
     assert np.array_equal(got.view(np.uint32)[~both_nan], ref.view(np.uint32)[~both_nan])
     assert np.array_equal(np.isnan(got), np.isnan(ref))
+
+
+def test_parity_envelope_variants_leave_the_normative_path_untouched():
+    """oracle.render_rows(variant=...) is test infrastructure for DESIGN.md §3's parity envelope: the
+    normative path (variant 0, what every parity test uses) is bit-identical through either entry
+    point, and the texture-filter variants change colours only, never a ray's fate or step count."""
+    import black_hole_ray_marching_amd as bh
+    import oracle
+    from tests._cases import camera_uniform, uniforms
+    sky = bh.synthetic_sky(512, 256)
+    W, H = 64, 32
+    cu, U = camera_uniform("A", W, H).to_bytes(), bytes(uniforms().to_c())
+    ref = oracle.render_rows(cu, U, sky, W, H, 512, 3)
+    lib = oracle.load()
+    col = np.empty((H, W, 4), np.float32)
+    n = np.empty((H, W), np.uint16)
+    f = np.empty((H, W), np.uint8)
+    import ctypes as C
+    assert lib.bho_render_rows_variant(C.create_string_buffer(cu, 112), C.create_string_buffer(U, 32),
+                                       np.ascontiguousarray(sky).ctypes.data, 512, 256, W, H, 512, 3, 0, H, 1,
+                                       col.ctypes.data, None, n.ctypes.data, f.ctypes.data, 0, 0) == 0
+    assert np.array_equal(col.view(np.uint32), ref[0].view(np.uint32))
+    for v in (oracle.V_TEX_8BIT, oracle.V_TEX_NEAREST, oracle.V_ATAN2F):
+        got = oracle.render_rows(cu, U, sky, W, H, 512, 3, variant=v)
+        assert np.array_equal(got[2], ref[2]) and np.array_equal(got[3], ref[3])
+        assert not np.array_equal(got[0].view(np.uint32), ref[0].view(np.uint32))
