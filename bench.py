@@ -46,7 +46,7 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md chip t
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
 
 # tile rows in flight of rank 0's unpack (bh_tiles_unpack_rgbm rows_in_flight)
-UNPACK_ROWS_IN_FLIGHT = 16
+UNPACK_ROWS_IN_FLIGHT = 64
 
 WORKLOADS = {"strong": (4096, 2048), "config4": (8192, 4096)}
 

@@ -38,25 +38,38 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
     using P = typename PixelT<BPP>::T;
     static_assert(PLANAR || !MASK, "the mask travels with the planar layout only");
     constexpr uint32_t TW = PLANAR ? 12u * BPP + (MASK ? 2u : 0u) : 16u * BPP;  // 32-bit words per packed tile
-    __shared__ uint32_t lds[UNPACK_SPAN * TW];
+    static_assert(TW % 2u == 0u, "packed tiles are whole 8-byte words");
+    constexpr uint32_t TD = TW / 2u;                                // 8-byte words per packed tile
+    constexpr uint32_t PER = (UNPACK_SPAN * TD + 255u) / 256u;      // staged words per thread
+    __shared__ uint2 lds2[UNPACK_SPAN * TD];
+    const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds2);
     __shared__ uint64_t gsrc[UNPACK_SPAN];  // packed tile of each output tile of the span
-    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
     const uint32_t tx0 = blockIdx.x * UNPACK_SPAN;
     const uint32_t tiles_y = (u.height + 7u) / 8u;
+    const uint32_t span = min(UNPACK_SPAN, u.tiles_x - tx0);       // tiles of the span inside the frame
+    const uint2* src = reinterpret_cast<const uint2*>(packed);
     for (uint32_t ty = blockIdx.y; ty < tiles_y; ty += gridDim.y) {  // grid-stride over tile rows
     __syncthreads();  // the previous row's LDS reads are done
-    if (threadIdx.x < UNPACK_SPAN && tx0 + threadIdx.x < u.tiles_x) {
+    if (threadIdx.x < span) {
         uint32_t k;
         const uint32_t t = shard_tile_index(tx0 + threadIdx.x, ty, u.tiles_x, u.shard_count, &k);
-        gsrc[threadIdx.x] = (uint64_t)k * u.stride_tiles + t;
+        gsrc[threadIdx.x] = ((uint64_t)k * u.stride_tiles + t) * TD;
     }
     __syncthreads();
-    // wave w stages tiles w, w+4, ...: at any time the 4 waves read 4 neighbouring tiles, i.e.
-    // neighbouring runs of (up to) 4 shards
-    for (uint32_t j = w; j < UNPACK_SPAN && tx0 + j < u.tiles_x; j += 4u) {
-        const uint32_t* src = packed + gsrc[j] * TW;
+    // Stage the span's packed tiles: consecutive threads take consecutive 8-byte words of a tile, and
+    // a shard's tiles of one row are consecutive in its buffer, so each shard's share of the span is
+    // one coalesced run.  Every load is issued before the first LDS store (PER loads in flight per
+    // thread instead of one tile's worth per wave at a time).
+    uint2 v[PER];
 #pragma unroll
-        for (uint32_t i = lane; i < TW; i += 64u) lds[j * TW + i] = src[i];
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t i = threadIdx.x + 256u * q, j = i / TD;
+        if (j < span) v[q] = src[gsrc[j] + (i - j * TD)];
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < PER; ++q) {
+        const uint32_t i = threadIdx.x + 256u * q;
+        if (i / TD < span) lds2[i] = v[q];
     }
     __syncthreads();
     const uint32_t x = threadIdx.x, px = tx0 * 8u + x;
