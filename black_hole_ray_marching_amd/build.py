@@ -29,9 +29,14 @@ COMMON = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno
 TU_FLAGS = {
     # packed FP32 has no throughput advantage on gfx950 (tools/ubench/valu_rates.hip): no SLP packing.
     # No machine scheduling (pre- or post-RA): the step's source order issues faster than the
-    # scheduler's interleavings (0.687 -> 0.644 ms headline, A/B r01).
+    # scheduler's interleavings (0.687 -> 0.644 ms headline, A/B r01).  No
+    # machine LICM: it hoists loop-invariant materialisations (e.g. the shading's f64 constants) out of
+    # the frame-independent loops and lengthens live ranges; off, 0.6226 -> 0.6168 ms per frame
+    # headline, 1920x1080 0.162 -> 0.159 ms (A/B r02, profiles/r02b/ab_nolicm.log; the scheduled
+    # build below got slower with it, 0.736 -> 0.768 ms at cap 1000, so it keeps LICM).
     "bh_march_exact.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize",
-                           "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
+                           "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0",
+                           "-mllvm", "-disable-machine-licm"],
     # the same kernels WITH machine scheduling: shorter per-step latency for tail-bound frames
     "bh_march_exact_lat.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-slp-vectorize"],
     # the fast (tolerance) kernels: no machine scheduling either (0.468 -> 0.440 ms headline, A/B r01)

@@ -161,6 +161,9 @@ __host__ __device__ inline uint32_t centre_out(uint32_t b, uint32_t n, uint32_t 
 namespace bh {
 // Dispatch-order buckets by the previous frame's per-tile cost (max n_rk / 2): expensive first.
 constexpr uint32_t ORDER_BUCKETS = 6;
+// Words of a temporal-order state's counters: [0, B-1) the cost histogram, [B, 2B) the order kernel's
+// cursors, [2B] its block ticket.
+constexpr uint32_t ORDER_WORDS = 2 * ORDER_BUCKETS + 1;
 __host__ __device__ inline uint32_t cost_bucket(uint32_t c) {
     return c >= 128u ? 0u : c >= 64u ? 1u : c >= 32u ? 2u : c >= 20u ? 3u : c >= 12u ? 4u : 5u;
 }

@@ -36,7 +36,7 @@ struct bh_ctx {
         bool valid = false;                  // costs and histogram agree (false: start afresh)
         uint8_t* tile_cost = nullptr;
         uint32_t* order = nullptr;
-        uint32_t* counters = nullptr;        // 2 * ORDER_BUCKETS + 1 words (bh_tiles.hip order_scatter_kernel)
+        uint32_t* counters = nullptr;        // ORDER_WORDS words (bh_common.hpp)
     };
     std::vector<OrderState> orders;
     uint64_t order_clock = 0;
@@ -640,7 +640,7 @@ static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStrea
     bh_ctx::OrderState n;
     n.width = d->width; n.height = d->height; n.shard_index = d->shard_index; n.shard_count = d->shard_count;
     n.stream = (void*)s;
-    const size_t cw = (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t);
+    const size_t cw = bh::ORDER_WORDS * sizeof(uint32_t);
     hipError_t he;
     if ((he = hipMalloc(&n.tile_cost, nt)) != hipSuccess || (he = hipMalloc(&n.order, nt * sizeof(uint32_t))) != hipSuccess ||
         (he = hipMalloc(&n.counters, cw)) != hipSuccess) {
@@ -761,7 +761,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
         if (st != BH_OK) { if (prev != c->device) (void)hipSetDevice(prev); return st; }
         if (!os->valid) {
             // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent
-            hipError_t he = hipMemsetAsync(os->counters, 0, (2 * bh::ORDER_BUCKETS + 1) * sizeof(uint32_t), s);
+            hipError_t he = hipMemsetAsync(os->counters, 0, bh::ORDER_WORDS * sizeof(uint32_t), s);
             if (he == hipSuccess) he = hipMemsetAsync(os->tile_cost, 0, nt, s);
             if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order reset"); }
             os->valid = true;

@@ -8,11 +8,10 @@ namespace {
 template <uint32_t FMT>
 int launch(const bh::MarchArgs& a, uint32_t schedule, uint32_t* counters, uint32_t grid, hipStream_t s) {
     if (schedule == BH_SCHED_TILE) {
-        const uint32_t blocks = (a.n_tiles * a.n_frames + 3u) / 4u;
         if (a.scene_flags == BH_SCENE_DEFAULT)  // the reference's scene: flags folded at compile time
-            hipLaunchKernelGGL((bh::fast::march_tile_kernel<FMT, BH_SCENE_DEFAULT>), dim3(blocks), dim3(256), 0, s, a);
+            bh::fast::launch_tile_schedule<FMT, BH_SCENE_DEFAULT>(a, s);
         else
-            hipLaunchKernelGGL((bh::fast::march_tile_kernel<FMT, bh::fast::SF_DYN>), dim3(blocks), dim3(256), 0, s, a);
+            bh::fast::launch_tile_schedule<FMT, bh::fast::SF_DYN>(a, s);
     } else if (schedule == BH_SCHED_PAIR) {
         const uint32_t pairs = (a.n_tiles + 1u) / 2u;
         hipLaunchKernelGGL(bh::fast::march_pair_kernel<FMT>, dim3((pairs + 3u) / 4u), dim3(256), 0, s, a);
