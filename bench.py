@@ -67,6 +67,10 @@ def parse(argv=None):
     p.add_argument("--height", type=int, default=0)
     p.add_argument("--max-iters", type=int, default=512)
     p.add_argument("--camera", choices=["A", "B", "C"], default="A")
+    p.add_argument("--orbit-deg", type=float, default=0.2, help="--camera-path orbit: degrees per frame")
+    p.add_argument("--camera-path", choices=["fixed", "orbit"], default="fixed",
+                   help="orbit: frame i's camera is the chosen one rotated about the y axis by i x 0.2 degrees "
+                        "(an offline camera path: every frame of a multi-frame launch has its own camera)")
     p.add_argument("--surfaces", choices=["on", "off"], default="on",
                    help="off = scene_flags 0 (no disc, no markers: BASELINE config 1's scene)")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline / parity leg")
@@ -84,7 +88,20 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
-CAMERAS = {"B": ((0.0, 3.0, -20.0), (0.0, 0.0, 0.0)), "C": ((0.0, 6.0, -12.0), (0.0, 0.0, 0.0))}
+CAMERAS = {"A": ((0.0, 0.0, -20.0), (0.0, 0.0, 0.0)),   # == Scene::new's camera (src/scene.rs:68-76)
+           "B": ((0.0, 3.0, -20.0), (0.0, 0.0, 0.0)), "C": ((0.0, 6.0, -12.0), (0.0, 0.0, 0.0))}
+ORBIT_DEG_PER_FRAME = 0.2
+
+
+def orbit_camera(bh, camera: str, i: int, W: int, H: int, deg: float = ORBIT_DEG_PER_FRAME):
+    """Camera uniform of frame i of the orbit path: the named camera's position rotated about the y axis
+    through the black hole by i * deg degrees, looking at the origin."""
+    pos, target = CAMERAS[camera]
+    a = np.radians(deg * i)
+    p = (pos[0] * np.cos(a) + pos[2] * np.sin(a), pos[1], -pos[0] * np.sin(a) + pos[2] * np.cos(a))
+    cu = bh.CameraUniform()
+    cu.update(bh.Camera.look_at(tuple(float(v) for v in p), target, W, H))
+    return cu
 
 
 # ---- rank launcher (no torchrun) --------------------------------------------------------------------
@@ -309,15 +326,28 @@ def main() -> int:
                                        rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
 
     launch_no = [0]
+    frame_no = [0]   # frames launched so far (the orbit path's frame index)
+    orbit = {}       # frame index -> CameraUniform, built outside the timed region
+
+    def cams(nf):
+        if args.camera_path == "fixed":
+            return None
+        return [orbit[frame_no[0] + f] for f in range(nf)]
 
     def launch(nf, **kw):
-        """One bh_render_frames launch of nf <= D frames (all of this scene's camera)."""
+        """One bh_render_frames launch of nf <= D frames (this scene's camera, or the orbit path's)."""
         if pipe is None:
-            scene.render_frames(cols[:nf], bos[:nf], fmt=fmt, stream=stream, schedule=sched, **shard, **kw)
+            scene.render_frames(cols[:nf], bos[:nf], cameras=cams(nf), fmt=fmt, stream=stream, schedule=sched,
+                                **shard, **kw)
         else:
             buf = pipe.buffer(launch_no[0])
-            scene.render_frames([buf[f * stride:(f + 1) * stride] for f in range(nf)], None, fmt=fmt, stream=stream,
-                                schedule=sched, **shard, **kw)
+            scene.render_frames([buf[f * stride:(f + 1) * stride] for f in range(nf)], None, cameras=cams(nf), fmt=fmt,
+                                stream=stream, schedule=sched, **shard, **kw)
+
+    if args.camera_path == "orbit":
+        if args.graph:
+            raise SystemExit("--graph replays one launch's cameras: use --camera-path fixed")
+        orbit.update({i: orbit_camera(bh, args.camera, i, W, H, args.orbit_deg) for i in range(args.warmup + args.steps + D)})
 
     graph = None
     if args.graph and n == 1:
@@ -338,6 +368,7 @@ def main() -> int:
             launch_frames[launch_no[0]] = nf
             pipe.submit(launch_no[0])
         launch_no[0] += 1
+        frame_no[0] += nf
 
     def sizes(k):  # frames per launch covering k frames
         return [min(D, k - i) for i in range(0, k, D)]
@@ -383,26 +414,35 @@ def main() -> int:
 
     gather_ok = None
     if args.verify_gather and n > 1 and rank == 0:
+        # every frame of the last launch against a single-GPU render of that frame's camera
         ref_c = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
         ref_b = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
-        scene.render(ref_c, ref_b, fmt=fmt, stream=stream, schedule=sched)
-        torch.cuda.synchronize(dev)
         last = plan[-1]
-        gather_ok = all(bool(torch.equal(ref_c.view(torch.uint8), frame_cols[f].view(torch.uint8))
-                             and torch.equal(ref_b.view(torch.uint8), frame_bos[f].view(torch.uint8)))
-                        for f in range(last))
+        first = frame_no[0] - last  # frame index of the last launch's first frame
+        gather_ok = True
+        for f in range(last):
+            if args.camera_path == "orbit":
+                scene.render_frames([ref_c], [ref_b], cameras=[orbit[first + f]], fmt=fmt, stream=stream,
+                                    schedule=sched)
+            else:
+                scene.render(ref_c, ref_b, fmt=fmt, stream=stream, schedule=sched)
+            torch.cuda.synchronize(dev)
+            gather_ok = gather_ok and bool(torch.equal(ref_c.view(torch.uint8), frame_cols[f].view(torch.uint8))
+                                           and torch.equal(ref_b.view(torch.uint8), frame_bos[f].view(torch.uint8)))
         del ref_c, ref_b
 
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
     # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
     px_shape = (H, W) if n == 1 else (multigpu.packed_stride(W, H, n) * 64,)  # the layout's pixel index space
-    nrk_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
-    steps_buf = torch.zeros(px_shape, dtype=torch.int16, device=dev)
-    launch(1, dbg_n_rk=[nrk_buf], dbg_steps=[steps_buf])
+    nm = 1 if args.camera_path == "fixed" else D  # orbit: every frame of a launch (own cameras), averaged
+    frame_no[0] = 0
+    nrk_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
+    steps_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
+    launch(nm, dbg_n_rk=nrk_bufs, dbg_steps=steps_bufs)
     torch.cuda.synchronize(dev)
-    sum_nrk = int(nrk_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
-    sum_steps = int(steps_buf.cpu().numpy().view(np.uint16).astype(np.int64).sum())
+    sum_nrk = sum(int(b.cpu().numpy().view(np.uint16).astype(np.int64).sum()) for b in nrk_bufs) // nm
+    sum_steps = sum(int(b.cpu().numpy().view(np.uint16).astype(np.int64).sum()) for b in steps_bufs) // nm
 
     if rank == 0:
         value = W * H * args.steps / elapsed / 1e6
@@ -426,12 +466,14 @@ def main() -> int:
             "data": "synthetic (splitmix64-seeded 4096x2048 RGBA8 sRGB sky; reference default camera)",
             "config": {
                 "workload": f"{workload}: {W}x{H} frame, cap {cap} RK steps, "
-                            f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}, "
+                            f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}"
+                            + (f" orbiting {args.orbit_deg} deg/frame" if args.camera_path == "orbit" else "") + ", "
                             f"{args.fmt} col+blackout, {args.math} math"
                             + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
                                                   "(RGB planes + blackout mask) to rank 0 overlapped with the next "
                                                   "frame, rank 0 unpacks col and blackout_col"),
-                "width": W, "height": H, "max_iters": cap, "camera": args.camera, "math": args.math,
+                "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
+                "math": args.math,
                 "schedule": args.schedule, "format": args.fmt, "frames_per_launch": D,
                 "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
                                else f"tile-sharded x{n}"

@@ -65,3 +65,33 @@ extern "C" int chip_clock_probe(unsigned long long* out, int blocks, int spin, h
     hipLaunchKernelGGL(chip_clock_kernel, dim3(blocks), dim3(64), 0, s, out, spin);
     return (int)hipGetLastError();
 }
+
+// Heavy-load clock probe: `blocks` x 256 threads (all waves resident at 8 per SIMD when blocks = 8 x
+// CUs), each lane running 8 independent FMA chains for `spin` iterations -- VALU-bound like a frame.
+// out[b] = {d(memtime), d(memrealtime), xcc} of each block's first wave.
+__global__ void __launch_bounds__(256) heavy_clock_kernel(unsigned long long* out, int spin) {
+    const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    float x[8];
+    for (int c = 0; c < 8; ++c) x[c] = threadIdx.x * 1e-3f + c;
+    for (int i = 0; i < spin; ++i) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) x[c] = __builtin_fmaf(x[c], 0.999f, 1e-3f);
+    }
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned int xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
+    float s = 0.0f;
+    for (int c = 0; c < 8; ++c) s += x[c];
+    if (threadIdx.x == 0) {
+        out[4 * blockIdx.x + 0] = c1 - c0;
+        out[4 * blockIdx.x + 1] = r1 - r0;
+        out[4 * blockIdx.x + 2] = xcc;
+        out[4 * blockIdx.x + 3] = __float_as_uint(s);
+    }
+}
+
+extern "C" int heavy_clock_probe(unsigned long long* out, int blocks, int spin, hipStream_t s) {
+    hipLaunchKernelGGL(heavy_clock_kernel, dim3(blocks), dim3(256), 0, s, out, spin);
+    return (int)hipGetLastError();
+}
