@@ -273,9 +273,9 @@ int bh_tiles_unpack_rgb(const void* packed, void* out_rowmajor, uint32_t width, 
 
 /* As bh_tiles_unpack_rgb with at most `rows_in_flight` 8-pixel tile rows of the frame in flight at
  * once (0 = all; the kernel grid-strides over the rest).  For an unpack that overlaps a render on
- * the same GPU (rank 0 of the multi-GPU pipeline): a small value (16) keeps it from displacing the
- * render's waves -- slower alone, but rank 0's render + unpack frame measured 0.78 -> 0.73 ms at
- * the N=8 frame. */
+ * the same GPU (rank 0 of the multi-GPU pipeline) a bounded value keeps it from displacing the
+ * render's waves: at N=8 on the 4096x2048 frame, rank 0's render + unpack measured 0.099 ms per
+ * frame with 64 rows in flight, 0.100 with all, 0.138 with 16. */
 int bh_tiles_unpack_rgb_rows(const void* packed, void* out_rowmajor, uint32_t width, uint32_t height,
                              uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
                              uint32_t rows_in_flight, void* hip_stream);
