@@ -479,7 +479,7 @@ def main() -> int:
                                else f"tile-sharded x{n}"
                                + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
             },
-            "kernel": {"name": f"bh::{args.math}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
+            "kernel": {"name": f"bh::{kernel_ns(args, my_tiles, D, cap, dev)}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
                                + (", 3u>" if args.schedule.startswith("tile") and flags == 3
                                   else (", 4294967295u>" if args.schedule.startswith("tile") else ">")),
                        "launches": len(plan), "frames_per_launch": D, "tiles_per_frame": my_tiles,
@@ -523,6 +523,19 @@ def main() -> int:
     return 0
 
 
+def kernel_ns(args, tiles: int, D: int, cap: int, dev) -> str:
+    """Namespace of the march kernel bh_render runs: the fast build, or which of the two exact builds
+    (bh_host.cpp march_variant_issue_order: source-order `exact` when the launch's tiles in flight,
+    tiles x frames x 512 >= 384 x CUs x cap; else the scheduled `exact_lat`)."""
+    if args.math != "exact":
+        return "fast"
+    if args.variant != "auto":
+        return "exact" if args.variant == "issue" else "exact_lat"
+    import torch
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    return "exact" if tiles * D * 512 >= 384 * cus * cap else "exact_lat"
+
+
 def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     """Frames per launch: enough that each frame's serial tail (the few rays that march to the cap, ~0.9
     us per step alone: DESIGN.md §5) overlaps the other frames' bulk.  Measured (tools/probe_inflight.py,
@@ -539,6 +552,8 @@ def pmc_key(W, H, cap, camera, math, schedule, fmt, n, D) -> str:
 
 def _pmc_entry(W, H, cap, args, n, D):
     """This configuration's entry of profiles/pmc_traffic.json (rocprofv3 PMC passes), or {}."""
+    if args.camera_path != "fixed":
+        return {}  # the profiled configurations are fixed-camera ones
     p = ROOT / "profiles" / "pmc_traffic.json"
     key = pmc_key(W, H, cap, args.camera, args.math, args.schedule, args.fmt, n, D)
     try:
