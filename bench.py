@@ -82,6 +82,9 @@ def parse(argv=None):
                    help="N>1: rank 0 compares both assembled targets with its own full-frame render (bitwise)")
     p.add_argument("--frames-per-launch", type=int, default=0,
                    help="frames rendered by one bh_render_frames launch (1..8; 0 = auto, DESIGN.md §5 item 9)")
+    p.add_argument("--root-ratio", default="auto",
+                   help="N>1: rank 0's tile share relative to each other rank's (it also unpacks every frame): "
+                        "'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain (tx + 3ty) %% N interleave")
     p.add_argument("--plumbing", action="store_true",
                    help="no GPU: the N-rank launch, gather pipeline and RGBM unpack on CPU (gloo) with "
                         "synthetic shards (tests only; prints no measurement)")
@@ -142,6 +145,17 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
+def root_weights(args, n: int):
+    """The weighted partition of an N>1 run (rank 0 lighter, it also unpacks), or None for the plain
+    interleave (N = 1 or --root-ratio 1)."""
+    if n == 1:
+        return None
+    from black_hole_ray_marching_amd import multigpu
+    ratio = multigpu.auto_root_ratio(n) if args.root_ratio == "auto" else float(args.root_ratio)
+    w = multigpu.root_weights(n, ratio)
+    return None if len(set(w)) == 1 else w
+
+
 # ---- host facts for the CPU baseline ----------------------------------------------------------------
 
 def _cpu_model() -> str:
@@ -184,7 +198,8 @@ def plumbing(args, rank: int, n: int) -> int:
     if os.environ.get("BH_PLUMBING_FAIL_RANK") == str(rank):  # test hook: a rank that dies mid-run
         raise SystemExit(f"plumbing: rank {rank} failing on request")
     W, H = (args.width or 100), (args.height or 52)
-    stride = multigpu.packed_stride(W, H, n)
+    weights = root_weights(args, n)
+    stride = multigpu.packed_stride(W, H, n, weights)
     tb = multigpu.rgbm_tile_bytes(1)
     yy, xx = np.mgrid[0:H, 0:W]
 
@@ -197,7 +212,7 @@ def plumbing(args, rank: int, n: int) -> int:
     ok = []
 
     def on_frame(i, gathered):
-        col, bo = multigpu.unpack_rgbm_numpy(gathered.numpy(), W, H, n, stride, np.float16, 1.0)
+        col, bo = multigpu.unpack_rgbm_numpy(gathered.numpy(), W, H, n, stride, np.float16, 1.0, weights)
         want, zero = frame(i)
         want_bo = want.copy()
         want_bo[zero, :3] = 0
@@ -207,7 +222,7 @@ def plumbing(args, rank: int, n: int) -> int:
     pipe = multigpu.GatherPipeline(lambda: torch.zeros((stride, tb), dtype=torch.uint8), rank, n, on_frame)
     for i in range(args.steps):
         c, z = frame(i)
-        pipe.buffer(i).copy_(torch.from_numpy(multigpu.pack_rgbm_numpy(c, z, rank, n, stride)))
+        pipe.buffer(i).copy_(torch.from_numpy(multigpu.pack_rgbm_numpy(c, z, rank, n, stride, weights)))
         pipe.submit(i)
     pipe.drain()
     world = dist.get_world_size() if n > 1 else 1
@@ -215,6 +230,7 @@ def plumbing(args, rank: int, n: int) -> int:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": n, "steps": args.steps,
                           "data": "plumbing (CPU, gloo, synthetic RGBM shards; no GPU, not a measurement)",
                           "world_size": world, "backend": dist.get_backend() if n > 1 else None,
+                          "partition_weights": weights,
                           "frames_checked": len(ok), "gather_verified_bit_exact": bool(ok) and all(ok)}))
     if n > 1:
         dist.barrier()
@@ -295,6 +311,7 @@ def main() -> int:
     D = args.frames_per_launch or auto_frames_per_launch(n, W, H, cap)
     if not 1 <= D <= bh.BH_MAX_FRAMES:
         raise SystemExit(f"--frames-per-launch must be 1..{bh.BH_MAX_FRAMES}")
+    weights = None
     if n == 1:
         cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
         bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
@@ -307,20 +324,29 @@ def main() -> int:
         # None == Option::None: its per-pixel decision travels as the RGBM mask), into one packed
         # buffer; launch i's gather to rank 0 (all D frames in one collective) overlaps launch i+1's
         # render; rank 0 unpacks every frame's col and blackout_col on a side stream
-        stride = multigpu.packed_stride(W, H, n)
+        weights = root_weights(args, n)
+        part = bh.Partition(W, H, weights, device=local) if weights else None
+        stride = max(part.counts) if part else multigpu.packed_stride(W, H, n)
         tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
-        my_tiles = bh.shard_tile_count(W, H, rank, n)
+        my_tiles = part.counts[rank] if part else bh.shard_tile_count(W, H, rank, n)
         my_bytes = my_tiles * tb + (2 * W * H * bpp if rank == 0 else 0)
         frame_cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         frame_bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         shard = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=rank, shard_count=n)
+        if part:
+            shard["partition"] = part
         launch_frames = {}
 
         def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
             # gathered: (n * D * stride, tb), rank k's block of D frames at k * D * stride
             for f in range(launch_frames.pop(i)):
-                bh.tiles_unpack_rgbm(gathered[f * stride:], frame_cols[f], frame_bos[f], W, H, n, D * stride, fmt,
-                                     stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+                if part:
+                    bh.tiles_unpack_rgbm_partition(gathered[f * stride:], frame_cols[f], frame_bos[f], part, D * stride,
+                                                   fmt, stream=torch.cuda.current_stream(dev),
+                                                   rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+                else:
+                    bh.tiles_unpack_rgbm(gathered[f * stride:], frame_cols[f], frame_bos[f], W, H, n, D * stride, fmt,
+                                         stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
 
         pipe = multigpu.GatherPipeline(lambda: torch.empty((D * stride, tb), dtype=torch.uint8, device=dev),
                                        rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
@@ -434,7 +460,7 @@ def main() -> int:
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
     # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
-    px_shape = (H, W) if n == 1 else (multigpu.packed_stride(W, H, n) * 64,)  # the layout's pixel index space
+    px_shape = (H, W) if n == 1 else (stride * 64,)  # the layout's pixel index space
     nm = 1 if args.camera_path == "fixed" else D  # orbit: every frame of a launch (own cameras), averaged
     frame_no[0] = 0
     nrk_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
@@ -477,7 +503,9 @@ def main() -> int:
                 "schedule": args.schedule, "format": args.fmt, "frames_per_launch": D,
                 "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
                                else f"tile-sharded x{n}"
+                               + (f", weighted partition {weights} (rank 0 also unpacks)" if n > 1 and weights else "")
                                + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
+                **({"partition_weights": weights, "tiles_per_rank_max": stride} if n > 1 else {}),
             },
             "kernel": {"name": f"bh::{kernel_ns(args, my_tiles, D, cap, dev)}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
                                + (", 3u>" if args.schedule.startswith("tile") and flags == 3

@@ -29,7 +29,7 @@ BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled bu
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
 
@@ -65,7 +65,7 @@ class bh_render_desc(C.Structure):
                 ("layout", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
                 ("schedule", C.c_uint32), ("out_col", C.c_void_p), ("out_blackout", C.c_void_p),
                 ("dbg_n_rk", C.c_void_p), ("dbg_fate", C.c_void_p),
-                ("dbg_steps", C.c_void_p)]
+                ("dbg_steps", C.c_void_p), ("partition", C.c_void_p)]
 
 
 assert C.sizeof(bh_camera_uniform) == 112
@@ -97,6 +97,14 @@ SIGNATURES = {
     "bh_tiles_unpack_rgbm": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                        C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]),
     "bh_tile_bytes": (C.c_int64, [C.c_uint32, C.c_uint32]),
+    "bh_partition_create": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_int,
+                                      C.POINTER(C.c_void_p)]),
+    "bh_partition_destroy": (C.c_int, [C.c_void_p]),
+    "bh_partition_tile_count": (C.c_int64, [C.c_void_p, C.c_uint32]),
+    "bh_partition_map": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.c_void_p,
+                                   C.c_void_p]),
+    "bh_tiles_unpack_rgbm_partition": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                 C.c_uint32, C.c_uint32, C.c_void_p]),
     "bh_srgb_encode_table": (C.c_int, [C.c_void_p]),
     "bh_controller_update": (C.c_int, [C.POINTER(bh_controller), C.POINTER(bh_camera), C.c_float, C.c_int,
                                        C.POINTER(C.c_int)]),

@@ -39,6 +39,7 @@ struct MarchArgs {
     uint32_t order_block;      // centre-out dispatch: shard-local tiles permuted in blocks of this
     uint32_t order_centre;     //   many tiles (~ one tile row), starting at block order_centre
     const uint32_t* order;     // optional dispatch order (slot -> shard-local tile), else centre-out
+    const uint32_t* tile_list; // optional (weighted partition): shard-local tile -> tx | ty << 16
     uint8_t* tile_cost;        // optional output: per shard-local tile, min(255, max n_rk / 2)
     uint32_t* order_tot;       // with tile_cost: per-bucket tile counts of those costs (buckets < B-1)
     // per-frame invariants, computed on the host with the same correctly rounded f32 ops as the
@@ -188,6 +189,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_build_order(const
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo,
                                                                                uint32_t width, uint32_t height,
                                                                                uint32_t shard_count, uint64_t stride_tiles,
+                                                                               const uint32_t* tile_loc,
                                                                                uint32_t format, uint32_t rows_in_flight,
                                                                                hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(const void* packed, void* out, uint32_t width,

@@ -31,6 +31,7 @@ struct bh_ctx {
     // and renders on different streams (frames in flight) never share costs or counters.
     struct OrderState {
         uint32_t width = 0, height = 0, shard_index = 0, shard_count = 0;
+        const void* partition = nullptr;
         void* stream = nullptr;
         uint64_t last_use = 0;
         bool valid = false;                  // costs and histogram agree (false: start afresh)
@@ -43,6 +44,15 @@ struct bh_ctx {
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
     std::vector<uint32_t*> bloom_tex;
     uint64_t bloom_key = ~0ull;
+};
+
+// A weighted tile partition (include/bh_render.h, bh_partition_create).
+struct bh_partition {
+    uint32_t width = 0, height = 0, shard_count = 0, tiles_x = 0, tiles_y = 0;
+    int device = 0;
+    std::vector<uint32_t> count, offset;  // per shard: tiles, first entry in tile_list
+    uint32_t* tile_list = nullptr;        // device: every shard's tiles in packed order (tx | ty << 16)
+    uint32_t* tile_loc = nullptr;         // device: per tile (ty * tiles_x + tx): packed index | shard << 24
 };
 
 namespace {
@@ -632,13 +642,14 @@ static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles,
 static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStream_t s, bh_ctx::OrderState** out) {
     for (auto& o : c->orders)
         if (o.width == d->width && o.height == d->height && o.shard_index == d->shard_index &&
-            o.shard_count == d->shard_count && o.stream == (void*)s) {
+            o.shard_count == d->shard_count && o.partition == (const void*)d->partition && o.stream == (void*)s) {
             o.last_use = ++c->order_clock;
             *out = &o;
             return BH_OK;
         }
     bh_ctx::OrderState n;
     n.width = d->width; n.height = d->height; n.shard_index = d->shard_index; n.shard_count = d->shard_count;
+    n.partition = d->partition;
     n.stream = (void*)s;
     const size_t cw = bh::ORDER_WORDS * sizeof(uint32_t);
     hipError_t he;
@@ -683,7 +694,7 @@ static bool same_launch(const bh_render_desc* a, const bh_render_desc* b) {
     return a->width == b->width && a->height == b->height && a->max_iters == b->max_iters &&
            a->scene_flags == b->scene_flags && a->format == b->format && a->math == b->math &&
            a->layout == b->layout && a->shard_index == b->shard_index && a->shard_count == b->shard_count &&
-           a->schedule == b->schedule;
+           a->schedule == b->schedule && a->partition == b->partition;
 }
 
 int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, const bh_render_desc* d,
@@ -728,7 +739,22 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     a.format = d->format; a.layout = d->layout;
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;
     a.tiles_x = (d->width + 7u) / 8u; a.tiles_y = (d->height + 7u) / 8u;
-    const uint64_t nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
+    uint64_t nt;
+    if (const bh_partition* P = d->partition) {
+        if (P->width != d->width || P->height != d->height || P->shard_count != d->shard_count ||
+            P->device != c->device || d->layout == BH_LAYOUT_ROWMAJOR) {
+            g_last_error = "partition: frame size, shard count, device or layout do not match";
+            return BH_ERR_INVALID_ARG;
+        }
+        if ((d->schedule & 0xFFu) != BH_SCHED_TILE) {
+            g_last_error = "a weighted partition needs the tile schedule";
+            return BH_ERR_UNSUPPORTED;
+        }
+        nt = P->count[d->shard_index];
+        a.tile_list = P->tile_list + P->offset[d->shard_index];
+    } else {
+        nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
+    }
     if (nt * n_frames > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
     a.n_tiles = (uint32_t)nt;
     // centre-out dispatch blocks of ~one tile row of this shard, centred on the black hole's row
@@ -826,8 +852,123 @@ int bh_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo, uint32_t w
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
             return BH_ERR_INVALID_ARG;
-    int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, width, height, shard_count, shard_stride_tiles, format,
-                                        rows_in_flight, reinterpret_cast<hipStream_t>(stream));
+    int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, width, height, shard_count, shard_stride_tiles, nullptr,
+                                        format, rows_in_flight, reinterpret_cast<hipStream_t>(stream));
+    if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
+    return BH_OK;
+}
+
+namespace {
+// Owner of each residue (tx + 3 ty) mod M, M = sum(weights): smooth weighted round robin, so each shard's
+// residues are spread evenly over the M.  Empty if the weights are unusable.
+std::vector<uint32_t> partition_owners(uint32_t S, const uint32_t* w) {
+    uint64_t M = 0;
+    for (uint32_t k = 0; k < S; ++k) M += w[k];
+    if (M == 0 || M > 4096) return {};
+    std::vector<uint32_t> owner(M);
+    std::vector<int64_t> cw(S, 0);
+    for (uint64_t v = 0; v < M; ++v) {
+        uint32_t best = 0;
+        for (uint32_t k = 0; k < S; ++k) {
+            cw[k] += w[k];
+            if (cw[k] > cw[best]) best = k;
+        }
+        owner[v] = best;
+        cw[best] -= (int64_t)M;
+    }
+    return owner;
+}
+}  // namespace
+
+int bh_partition_map(uint32_t width, uint32_t height, uint32_t S, const uint32_t* weights, uint32_t* owner_out,
+                     uint32_t* index_out) {
+    if (width == 0 || height == 0 || width > 65536u || height > 65536u || S == 0 || S > 256 || !weights)
+        return BH_ERR_INVALID_ARG;
+    const std::vector<uint32_t> owner = partition_owners(S, weights);
+    if (owner.empty()) return BH_ERR_INVALID_ARG;
+    const uint32_t M = (uint32_t)owner.size(), tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
+    std::vector<uint32_t> next(S, 0);
+    for (uint32_t ty = 0; ty < ty_n; ++ty)
+        for (uint32_t tx = 0; tx < tx_n; ++tx) {
+            const uint32_t k = owner[(tx + 3ull * ty) % M];
+            const size_t t = (size_t)ty * tx_n + tx;
+            if (owner_out) owner_out[t] = k;
+            if (index_out) index_out[t] = next[k];
+            ++next[k];
+        }
+    return BH_OK;
+}
+
+int bh_partition_create(uint32_t width, uint32_t height, uint32_t S, const uint32_t* weights, int device,
+                        bh_partition** out) {
+    if (!out) return BH_ERR_INVALID_ARG;
+    *out = nullptr;
+    const uint32_t tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
+    const size_t n = (size_t)tx_n * ty_n;
+    if (n >= (1u << 24)) return BH_ERR_INVALID_ARG;  // packed indices carry 24 bits
+    std::vector<uint32_t> owner(n), index(n);
+    int st = bh_partition_map(width, height, S, weights, owner.data(), index.data());
+    if (st != BH_OK) return st;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return BH_ERR_NO_DEVICE;
+    bh_partition* P = new (std::nothrow) bh_partition;
+    if (!P) return BH_ERR_OUT_OF_MEMORY;
+    P->width = width; P->height = height; P->shard_count = S; P->tiles_x = tx_n; P->tiles_y = ty_n;
+    P->device = device;
+    P->count.assign(S, 0);
+    for (size_t t = 0; t < n; ++t) ++P->count[owner[t]];
+    P->offset.assign(S, 0);
+    for (uint32_t k = 1; k < S; ++k) P->offset[k] = P->offset[k - 1] + P->count[k - 1];
+    std::vector<uint32_t> list(n), loc(n);
+    for (size_t t = 0; t < n; ++t) {
+        const uint32_t k = owner[t];
+        list[P->offset[k] + index[t]] = (uint32_t)(t % tx_n) | (uint32_t)(t / tx_n) << 16;
+        loc[t] = index[t] | k << 24;
+    }
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    hipError_t e;
+    if ((e = hipMalloc(&P->tile_list, n * 4)) != hipSuccess || (e = hipMalloc(&P->tile_loc, n * 4)) != hipSuccess ||
+        (e = hipMemcpy(P->tile_list, list.data(), n * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(P->tile_loc, loc.data(), n * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+        st = e == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "partition tables");
+        if (P->tile_list) (void)hipFree(P->tile_list);
+        if (P->tile_loc) (void)hipFree(P->tile_loc);
+        delete P;
+        (void)hipSetDevice(prev);
+        return st;
+    }
+    (void)hipSetDevice(prev);
+    *out = P;
+    return BH_OK;
+}
+
+int bh_partition_destroy(bh_partition* P) {
+    if (!P) return BH_OK;
+    int prev = 0;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(P->device);
+    if (P->tile_list) (void)hipFree(P->tile_list);
+    if (P->tile_loc) (void)hipFree(P->tile_loc);
+    (void)hipSetDevice(prev);
+    delete P;
+    return BH_OK;
+}
+
+int64_t bh_partition_tile_count(const bh_partition* P, uint32_t shard_index) {
+    if (!P || shard_index >= P->shard_count) return BH_ERR_INVALID_ARG;
+    return P->count[shard_index];
+}
+
+int bh_tiles_unpack_rgbm_partition(const void* packed, void* out, void* out_bo, const bh_partition* P,
+                                   uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
+                                   void* stream) {
+    if (!packed || !out || !P || format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < P->shard_count; ++k)
+        if (P->count[k] > shard_stride_tiles) return BH_ERR_INVALID_ARG;
+    int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, P->width, P->height, P->shard_count, shard_stride_tiles,
+                                        P->tile_loc, format, rows_in_flight, reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
     return BH_OK;
 }

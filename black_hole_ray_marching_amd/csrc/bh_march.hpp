@@ -966,7 +966,13 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     const uint32_t t = a.order ? a.order[j] : centre_out(j, a.n_tiles, a.order_block, a.order_centre);
     if (t >= a.n_tiles) return;  // defensive: a corrupt order must not address outside the shard
     uint32_t tx, ty;
-    shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
+    if (a.tile_list) {  // weighted partition (bh_partition): the shard's tile list
+        const uint32_t v = a.tile_list[t];
+        tx = v & 0xFFFFu;
+        ty = v >> 16;
+    } else {
+        shard_tile_coords(t, a.tiles_x, a.shard_index, a.shard_count, &tx, &ty);
+    }
     const uint32_t px = tx * 8u + (lane & 7u), py = ty * 8u + (lane >> 3);
     const bool valid = px < a.width && py < a.height;
     const Frame f = make_frame(a);

@@ -17,6 +17,7 @@ constexpr uint32_t UNPACK_SPAN = 32;
 struct UnpackGrid {
     uint32_t width, height, tiles_x, shard_count;
     uint64_t stride_tiles;
+    const uint32_t* tile_loc;  // weighted partition: tile -> its packed index | shard << 24 (else the interleave)
 };
 template <uint32_t BPP> struct PixelT;
 template <> struct PixelT<16> { using T = uint4; };
@@ -51,8 +52,14 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
     for (uint32_t ty = blockIdx.y; ty < tiles_y; ty += gridDim.y) {  // grid-stride over tile rows
     __syncthreads();  // the previous row's LDS reads are done
     if (threadIdx.x < span) {
-        uint32_t k;
-        const uint32_t t = shard_tile_index(tx0 + threadIdx.x, ty, u.tiles_x, u.shard_count, &k);
+        uint32_t k, t;
+        if (u.tile_loc) {
+            const uint32_t v = u.tile_loc[(size_t)ty * u.tiles_x + tx0 + threadIdx.x];
+            k = v >> 24;
+            t = v & 0xFFFFFFu;
+        } else {
+            t = shard_tile_index(tx0 + threadIdx.x, ty, u.tiles_x, u.shard_count, &k);
+        }
         gsrc[threadIdx.x] = ((uint64_t)k * u.stride_tiles + t) * TD;
     }
     __syncthreads();
@@ -201,6 +208,7 @@ static void unpack_launch_shape(uint32_t width, uint32_t height, uint32_t shard_
                                 uint32_t rows_in_flight, bh::UnpackGrid* u, dim3* grid) {
     u->width = width; u->height = height; u->tiles_x = (width + 7u) / 8u; u->shard_count = shard_count;
     u->stride_tiles = stride_tiles;
+    u->tile_loc = nullptr;
     const uint32_t tiles_y = (height + 7u) / 8u;
     // rows_in_flight tile rows per grid pass (0: all), the kernel grid-strides over the rest
     *grid = dim3((u->tiles_x + bh::UNPACK_SPAN - 1u) / bh::UNPACK_SPAN,
@@ -210,10 +218,11 @@ static void unpack_launch_shape(uint32_t width, uint32_t height, uint32_t shard_
 template <bool PLANAR, bool MASK>
 static int unpack_launch(const void* packed, void* out, void* out_bo, uint32_t width, uint32_t height,
                          uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp, uint32_t rows_in_flight,
-                         hipStream_t s) {
+                         hipStream_t s, const uint32_t* tile_loc = nullptr) {
     bh::UnpackGrid u;
     dim3 grid, block(256);
     unpack_launch_shape(width, height, shard_count, stride_tiles, rows_in_flight, &u, &grid);
+    u.tile_loc = tile_loc;
     const uint32_t* p = static_cast<const uint32_t*>(packed);
     switch (bpp) {
         case 16: hipLaunchKernelGGL((bh::tiles_unpack_kernel<16, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
@@ -245,8 +254,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgb(
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo,
                                                                                uint32_t width, uint32_t height,
                                                                                uint32_t shard_count, uint64_t stride_tiles,
+                                                                               const uint32_t* tile_loc,
                                                                                uint32_t format, uint32_t rows_in_flight,
                                                                                hipStream_t s) {
     return unpack_launch<true, true>(packed, out, out_bo, width, height, shard_count, stride_tiles, format_bpp(format),
-                                     rows_in_flight, s);
+                                     rows_in_flight, s, tile_loc);
 }

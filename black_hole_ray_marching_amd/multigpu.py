@@ -36,11 +36,49 @@ def shard_tile_count(width: int, height: int, k: int, S: int) -> int:
     return sum(shard_row_count(tx, r, k, S) for r in range(ty))
 
 
-def shard_tiles(width: int, height: int, k: int, S: int) -> np.ndarray:
-    """(n, 2) array of (tx, ty) for shard k, in its packed order (row-major over owned tiles)."""
+def partition_owners(weights) -> list[int]:
+    """Owner of each residue v of (tx + 3*ty) mod M, M = sum(weights), for a weighted partition
+    (bh_host.cpp partition_owners: smooth weighted round robin)."""
+    M = sum(int(w) for w in weights)
+    if M <= 0 or M > 4096:
+        raise ValueError("weights must sum to 1..4096")
+    cw = [0] * len(weights)
+    out = []
+    for _ in range(M):
+        best = 0
+        for k, w in enumerate(weights):
+            cw[k] += int(w)
+            if cw[k] > cw[best]:
+                best = k
+        out.append(best)
+        cw[best] -= M
+    return out
+
+
+def shard_tiles(width: int, height: int, k: int, S: int, weights=None) -> np.ndarray:
+    """(n, 2) array of (tx, ty) for shard k, in its packed order (row-major over owned tiles).
+    weights: a weighted partition (bh_partition_create), else the (tx + 3*ty) % S interleave."""
     tiles_x, tiles_y = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+    if weights is not None:
+        own = np.array(partition_owners(weights))
+        ty, tx = np.divmod(np.arange(tiles_x * tiles_y), tiles_x)
+        m = own[(tx + 3 * ty) % len(own)] == k
+        return np.stack([tx[m], ty[m]], -1).astype(np.int64).reshape(-1, 2)
     out = [(tx, ty) for ty in range(tiles_y) for tx in range(shard_row_start(ty, k, S), tiles_x, S)]
     return np.array(out, dtype=np.int64).reshape(-1, 2)
+
+
+def root_weights(n: int, root_ratio: float, unit: int = 20) -> list[int]:
+    """Weights of a partition in which rank 0 (which also unpacks every frame) takes root_ratio of
+    another rank's share: [round(unit * root_ratio)] + [unit] * (n - 1)."""
+    return [max(0, int(round(unit * root_ratio)))] + [unit] * (n - 1)
+
+
+def auto_root_ratio(n: int) -> float:
+    """Rank 0's share relative to the others' when it also unpacks both targets of every frame: its
+    unpack costs it ~2.5 % x N of a shard's render time (measured 4 / 7 / 15 % at
+    N = 2 / 4 / 8 on the 4096x2048 frame, 23 % for 8192x4096 at N = 8)."""
+    return max(0.0, 1.0 - 0.025 * n)
 
 
 def shard_tile_index(tx: int, ty: int, width: int, height: int, S: int) -> tuple[int, int]:
@@ -55,8 +93,10 @@ def shard_tile_index(tx: int, ty: int, width: int, height: int, S: int) -> tuple
     return k, (ty // P) * per + pre + tx // S
 
 
-def packed_stride(width: int, height: int, S: int) -> int:
+def packed_stride(width: int, height: int, S: int, weights=None) -> int:
     """Tiles per rank in the gather buffer (the largest shard; smaller shards are padded)."""
+    if weights is not None:
+        return max(len(shard_tiles(width, height, k, S, weights)) for k in range(S))
     return max(shard_tile_count(width, height, k, S) for k in range(S))
 
 
@@ -92,7 +132,7 @@ def rgbm_tile_bytes(fmt: int) -> int:
     return 192 * CHANNEL_BYTES[fmt] + 8
 
 
-def pack_rgbm_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: int) -> np.ndarray:
+def pack_rgbm_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: int, weights=None) -> np.ndarray:
     """Host mirror of the march kernel's BH_LAYOUT_TILES_RGBM store for shard k: `col` (H, W, 4) in the
     format's memory order (uint8 / float16 / float32 channels), `zero` (H, W) bool = the pixel's
     blackout_col is 0 (dot(col, col) < 1 in fp32).  Returns (stride, tile_bytes) uint8; pixels outside
@@ -101,7 +141,7 @@ def pack_rgbm_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: i
     cb = col.dtype.itemsize
     out = np.zeros((stride, 192 * cb + 8), np.uint8)
     lane = np.arange(64)
-    for t, (tx, ty) in enumerate(shard_tiles(W, H, k, S)):
+    for t, (tx, ty) in enumerate(shard_tiles(W, H, k, S, weights)):
         px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
         ok = (px < W) & (py < H)
         planes = np.zeros((3, 64), col.dtype)
@@ -114,7 +154,7 @@ def pack_rgbm_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: i
     return out
 
 
-def unpack_rgbm_numpy(packed: np.ndarray, width: int, height: int, S: int, stride: int, dtype, alpha):
+def unpack_rgbm_numpy(packed: np.ndarray, width: int, height: int, S: int, stride: int, dtype, alpha, weights=None):
     """Host mirror of bh_tiles_unpack_rgbm: gathered (S * stride, tile_bytes) uint8 -> (col, blackout),
     each (height, width, 4) of `dtype` with the constant `alpha` restored; blackout = col with the
     masked pixels' RGB zeroed."""
@@ -123,7 +163,7 @@ def unpack_rgbm_numpy(packed: np.ndarray, width: int, height: int, S: int, strid
     bo = np.zeros((height, width, 4), dtype)
     lane = np.arange(64)
     for k in range(S):
-        for t, (tx, ty) in enumerate(shard_tiles(width, height, k, S)):
+        for t, (tx, ty) in enumerate(shard_tiles(width, height, k, S, weights)):
             tile = packed[k * stride + t]
             planes = tile[:192 * cb].view(dtype).reshape(3, 64)
             m = tile[192 * cb:].view(np.uint64)[0]

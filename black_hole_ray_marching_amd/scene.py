@@ -261,7 +261,7 @@ class Scene:
         self.camera_uniform.update(self.camera)
 
     def _desc(self, output, blackout_output, fmt, dbg_n_rk, dbg_fate, math, layout, shard_index, shard_count,
-              width, height, schedule, dbg_steps) -> _abi.bh_render_desc:
+              width, height, schedule, dbg_steps, partition=None) -> _abi.bh_render_desc:
         if output is None:
             raise BhError(_abi.BH_ERR_INVALID_ARG, "render: output is required")
         if not self.render_blackout and blackout_output is not None:
@@ -278,7 +278,13 @@ class Scene:
             px = d.width * d.height
             col_bytes = px * bpp
         else:
-            nt = shard_tile_count(d.width, d.height, shard_index, shard_count)
+            if partition is not None:
+                if (partition.width, partition.height, partition.shard_count) != (d.width, d.height, shard_count):
+                    raise BhError(_abi.BH_ERR_INVALID_ARG, "render: the partition's frame size / shard count differ")
+                d.partition = partition.handle
+                nt = partition.tile_count(shard_index)
+            else:
+                nt = shard_tile_count(d.width, d.height, shard_index, shard_count)
             px = nt * 64
             col_bytes = nt * tile_bytes(layout, fmt) if bpp and layout <= BH_LAYOUT_TILES_RGBM else px * bpp
         _check_size(output, col_bytes, "output")
@@ -293,21 +299,22 @@ class Scene:
     def render(self, output, blackout_output=None, *, fmt: int = BH_OUT_RGBA32F, stream=None,
                dbg_n_rk=None, dbg_fate=None, math: int | None = None, layout: int = BH_LAYOUT_ROWMAJOR,
                shard_index: int = 0, shard_count: int = 1, width: int | None = None,
-               height: int | None = None, schedule: int = 0, dbg_steps=None) -> None:
+               height: int | None = None, schedule: int = 0, dbg_steps=None, partition=None) -> None:
         """Scene::render (src/scene.rs:470-522): one pass writing `col` and optionally `blackout_col`.
 
         `output`/`blackout_output`: caller-owned device buffers (torch tensors or raw pointers).
         Asynchronous on `stream` (a torch.cuda.Stream, a raw hipStream_t int, or None = current).
         """
         d = self._desc(output, blackout_output, fmt, dbg_n_rk, dbg_fate, math, layout, shard_index, shard_count,
-                       width, height, schedule, dbg_steps)
+                       width, height, schedule, dbg_steps, partition)
         check(self.lib.bh_render(self._ctx, C.byref(self.camera_uniform.c), C.byref(self.uniforms.to_c()),
                                  C.byref(d), _stream_handle(stream)), "bh_render")
 
     def render_frames(self, outputs, blackout_outputs=None, *, cameras=None, fmt: int = BH_OUT_RGBA32F, stream=None,
                       dbg_n_rk=None, dbg_fate=None, dbg_steps=None, math: int | None = None,
                       layout: int = BH_LAYOUT_ROWMAJOR, shard_index: int = 0, shard_count: int = 1,
-                      width: int | None = None, height: int | None = None, schedule: int = 0) -> None:
+                      width: int | None = None, height: int | None = None, schedule: int = 0,
+                      partition=None) -> None:
         """Several frames in one launch (bh_render_frames, up to BH_MAX_FRAMES): frame i renders with
         cameras[i] (CameraUniform; default: this scene's camera for every frame) into outputs[i] /
         blackout_outputs[i]; each frame's result is exactly render()'s."""
@@ -320,7 +327,8 @@ class Scene:
         if not (len(bos) == len(nrks) == len(fates) == len(steps) == len(cams) == n):
             raise BhError(_abi.BH_ERR_INVALID_ARG, "render_frames: per-frame lists must have one entry per frame")
         descs = (_abi.bh_render_desc * n)(*[self._desc(outputs[i], bos[i], fmt, nrks[i], fates[i], math, layout,
-                                                       shard_index, shard_count, width, height, schedule, steps[i])
+                                                       shard_index, shard_count, width, height, schedule, steps[i],
+                                                       partition)
                                             for i in range(n)])
         cu = (_abi.bh_camera_uniform * n)(*[c.c for c in cams])
         check(self.lib.bh_render_frames(self._ctx, n, cu, C.byref(self.uniforms.to_c()), descs,
@@ -398,7 +406,67 @@ def tiles_unpack_rgbm(packed, out_col, out_blackout, width: int, height: int, sh
           "bh_tiles_unpack_rgbm")
 
 
-__all__ = ["Camera", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+class Partition:
+    """bh_partition (include/bh_render.h): a weighted tile partition of a width x height frame over
+    shard_count shards -- shard k owns weights[k] of every sum(weights) residues of (tx + 3*ty), each
+    shard's packed order row-major over its tiles.  Pass it to Scene.render / render_frames
+    (layout BH_LAYOUT_TILES*) and to tiles_unpack_rgbm."""
+
+    def __init__(self, width: int, height: int, weights, device: int = 0) -> None:
+        self.width, self.height = width, height
+        self.weights = [int(w) for w in weights]
+        self.shard_count = len(self.weights)
+        w = (C.c_uint32 * self.shard_count)(*self.weights)
+        h = C.c_void_p()
+        check(load().bh_partition_create(width, height, self.shard_count, w, device, C.byref(h)), "bh_partition_create")
+        self.handle = h.value
+        self.counts = [self.tile_count(k) for k in range(self.shard_count)]
+
+    def tile_count(self, shard_index: int) -> int:
+        n = load().bh_partition_tile_count(self.handle, shard_index)
+        if n < 0:
+            raise BhError(int(n), "bh_partition_tile_count")
+        return int(n)
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            load().bh_partition_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def partition_map(width: int, height: int, weights):
+    """bh_partition_map (host only): (owner, index) per tile t = ty * tiles_x + tx, as numpy arrays."""
+    tiles = ((width + 7) // 8) * ((height + 7) // 8)
+    owner = np.zeros(tiles, np.uint32)
+    index = np.zeros(tiles, np.uint32)
+    w = (C.c_uint32 * len(weights))(*[int(x) for x in weights])
+    check(load().bh_partition_map(width, height, len(weights), w, owner.ctypes.data, index.ctypes.data),
+          "bh_partition_map")
+    return owner, index
+
+
+def tiles_unpack_rgbm_partition(packed, out_col, out_blackout, partition: "Partition", shard_stride_tiles: int,
+                                fmt: int, stream=None, rows_in_flight: int = 0) -> None:
+    """bh_tiles_unpack_rgbm_partition: gathered BH_LAYOUT_TILES_RGBM shards of `partition` -> both targets."""
+    bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+    S = partition.shard_count
+    _check_size(packed, ((S - 1) * shard_stride_tiles + partition.counts[-1]) * (tile_bytes(BH_LAYOUT_TILES_RGBM, fmt)
+                                                                                if bpp else 0), "packed",
+                "tiles_unpack_rgbm_partition")
+    for t, name in ((out_col, "out_col"), (out_blackout, "out_blackout")):
+        _check_size(t, partition.width * partition.height * bpp, name, "tiles_unpack_rgbm_partition")
+    check(load().bh_tiles_unpack_rgbm_partition(_ptr(packed), _ptr(out_col), _ptr(out_blackout), partition.handle,
+                                                shard_stride_tiles, fmt, rows_in_flight, _stream_handle(stream)),
+          "bh_tiles_unpack_rgbm_partition")
+
+
+__all__ = ["Camera", "Partition", "partition_map", "tiles_unpack_rgbm_partition", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
            "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM",
            "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",

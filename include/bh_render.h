@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 2
+#define BH_ABI_VERSION 3
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
@@ -162,6 +162,8 @@ typedef enum {
 
 #define BH_TILE 8u           /* tile edge in pixels (multi-GPU sharding and BH_LAYOUT_TILES) */
 
+typedef struct bh_partition bh_partition;
+
 typedef struct {
     uint32_t width, height;   /* frame size in pixels */
     uint32_t max_iters;       /* MAX_ITERATIONS (WGSL const 1000, src/black_hole_maybe.wgsl:85), 1..65535 */
@@ -179,6 +181,9 @@ typedef struct {
     uint16_t* dbg_steps;      /* optional: RK4 iterations actually executed per pixel; below dbg_n_rk
                                  only where a ray that had entered an exact cycle (see DESIGN.md
                                  "Cycle fast-forward") was advanced to the cap without iterating */
+    const bh_partition* partition; /* optional, BH_LAYOUT_TILES* only: a weighted tile partition
+                                 (bh_partition_create) with this frame size and shard_count, used
+                                 instead of the default (tx + 3*ty) % shard_count interleave */
 } bh_render_desc;
 
 typedef struct bh_ctx bh_ctx;
@@ -287,6 +292,30 @@ int bh_tiles_unpack_rgb_rows(const void* packed, void* out_rowmajor, uint32_t wi
 int bh_tiles_unpack_rgbm(const void* packed, void* out_col, void* out_blackout, uint32_t width, uint32_t height,
                          uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format,
                          uint32_t rows_in_flight, void* hip_stream);
+/* Weighted tile partitions (multi-GPU).  The default ownership gives every shard 1/shard_count of
+ * the tiles; a partition gives shard k weights[k] of every M = sum(weights) residues: tile (tx, ty)
+ * belongs to owner[(tx + 3*ty) % M], the M residues dealt to the shards by smooth weighted round
+ * robin (each shard's residues spread evenly over the M), so that a shard with more work beside its
+ * render -- rank 0, which also unpacks every frame -- can take a smaller share.  A shard's packed
+ * order is row-major over its tiles, as for the default interleave.  weights[k] may be 0 (a shard
+ * that renders nothing); M <= 4096.  The partition holds device tables on `device` (each shard's
+ * tile list, and every tile's shard and packed index for the unpack); destroy it after the renders
+ * and unpacks that use it have completed. */
+int bh_partition_create(uint32_t width, uint32_t height, uint32_t shard_count, const uint32_t* weights, int device,
+                        bh_partition** out);
+int bh_partition_destroy(bh_partition* partition);
+/* Tiles owned by `shard_index` (a shard's packed buffer holds this many tiles), or a negative status. */
+int64_t bh_partition_tile_count(const bh_partition* partition, uint32_t shard_index);
+/* Host only (no device needed): the same partition's map, tile t = ty * tiles_x + tx:
+ * owner_out[t] = its shard, index_out[t] = its index in that shard's packed order (arrays of
+ * tiles_x * tiles_y entries; either may be NULL). */
+int bh_partition_map(uint32_t width, uint32_t height, uint32_t shard_count, const uint32_t* weights, uint32_t* owner_out,
+                     uint32_t* index_out);
+/* bh_tiles_unpack_rgbm for shards rendered with `partition` (its frame size and shard count). */
+int bh_tiles_unpack_rgbm_partition(const void* packed, void* out_col, void* out_blackout, const bh_partition* partition,
+                                   uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
+                                   void* hip_stream);
+
 /* Bytes of one tile of `layout` (BH_LAYOUT_TILES*) in `format`, or a negative bh_status. */
 int64_t bh_tile_bytes(uint32_t layout, uint32_t format);
 

@@ -268,3 +268,72 @@ def test_render_frames_rejects_mixed_descs(torch_cuda, sky_small):
     assert scene.lib.bh_render_frames(scene._ctx, 2, cu, __import__("ctypes").byref(scene.uniforms.to_c()), d,
                                       None) == bh._abi.BH_ERR_INVALID_ARG
     scene.close()
+
+
+# ---- weighted partitions (bh_partition: rank 0 lighter, it also unpacks) ---------------------------
+
+@pytest.mark.parametrize("fmt", [bh.BH_OUT_RGBA32F, bh.BH_OUT_RGBA16F, bh.BH_OUT_BGRA8_SRGB])
+@pytest.mark.parametrize("weights", [[1, 2], [18, 20, 20], [16] + [20] * 7, [0, 3, 3, 3], [5, 1, 7]])
+def test_partition_shards_unpack_both_targets(torch_cuda, sky_full, weights, fmt):
+    """Shards of a weighted partition, rendered in BH_LAYOUT_TILES_RGBM (col only) several frames per
+    launch, unpack with bh_tiles_unpack_rgbm_partition to both targets of a single-GPU render, bit for
+    bit; each shard's tiles are exactly its share of the host map (bh_partition_map)."""
+    torch = torch_cuda
+    from black_hole_ray_marching_amd import multigpu
+    W, H = 200, 100  # 25 x 13 tiles, a partial bottom tile row
+    S = len(weights)
+    dt = getattr(torch, DT[fmt])
+    scene = bh.Scene(W, H, sky=sky_full, max_iters=512, math=bh.BH_MATH_EXACT)
+    cams = [camera_uniform(c, W, H) for c in ("D", "A")]
+    part = bh.Partition(W, H, weights)
+    owner, _ = bh.partition_map(W, H, weights)
+    assert part.counts == [int((owner == k).sum()) for k in range(S)]
+    assert part.counts == [len(multigpu.shard_tiles(W, H, k, S, weights)) for k in range(S)]
+    tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+    stride = max(part.counts)
+    D = len(cams)
+    packed = torch.zeros((S * D * stride, tb), dtype=torch.uint8, device="cuda")
+    for rep in range(2):  # the second launch runs the learned order of the partition's shards
+        for k in range(S):
+            if part.counts[k] == 0:
+                continue
+            blk = packed[k * D * stride:(k + 1) * D * stride]
+            scene.render_frames([blk[f * stride:f * stride + part.counts[k]] for f in range(D)], None, cameras=cams,
+                                fmt=fmt, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=k, shard_count=S, partition=part)
+    for f, cu in enumerate(cams):
+        scene.camera_uniform = cu
+        ref_c = torch.zeros((H, W, 4), dtype=dt, device="cuda")
+        ref_b = torch.zeros_like(ref_c)
+        scene.render(ref_c, ref_b, fmt=fmt)
+        out_c = torch.full((H, W, 4), 7, dtype=dt, device="cuda")
+        out_b = torch.full((H, W, 4), 7, dtype=dt, device="cuda")
+        bh.tiles_unpack_rgbm_partition(packed[f * stride:], out_c, out_b, part, D * stride, fmt, rows_in_flight=3)
+        torch.cuda.synchronize()
+        assert torch.equal(out_c.view(torch.uint8), ref_c.view(torch.uint8)), (weights, f)
+        assert torch.equal(out_b.view(torch.uint8), ref_b.view(torch.uint8)), (weights, f)
+    part.close()
+    scene.close()
+
+
+def test_partition_rejects_mismatches(torch_cuda, sky_small):
+    """A partition is bound to its frame size, shard count and the tile schedule; other schedules and
+    row-major layouts are refused with a status, never rendered with the wrong map."""
+    torch = torch_cuda
+    W, H = 96, 64
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=64, math=bh.BH_MATH_EXACT)
+    part = bh.Partition(W, H, [1, 2])
+    buf = torch.zeros((part.counts[1], bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, bh.BH_OUT_RGBA16F)), dtype=torch.uint8,
+                      device="cuda")
+    with pytest.raises(bh.BhError):
+        scene.render(buf, None, fmt=bh.BH_OUT_RGBA16F, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=1, shard_count=2,
+                     partition=part, schedule=bh.BH_SCHED_PAIR)
+    with pytest.raises(bh.BhError):
+        scene.render(buf, None, fmt=bh.BH_OUT_RGBA16F, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=1, shard_count=3,
+                     partition=part)
+    other = bh.Partition(W, 56, [1, 2])
+    with pytest.raises(bh.BhError):
+        scene.render(buf, None, fmt=bh.BH_OUT_RGBA16F, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=1, shard_count=2,
+                     partition=other)
+    other.close()
+    part.close()
+    scene.close()

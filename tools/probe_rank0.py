@@ -1,11 +1,12 @@
 """Rank 0's per-frame GPU work in bench.py's N>1 path, on one GPU: its own shard render of D frames per
 launch (BH_LAYOUT_TILES_RGBM, col only; render stream) with the unpack of the previous launch's D
-gathered frames into both row-major targets (bh_tiles_unpack_rgbm, side stream, throttled to
-`rows` tile rows in flight) running beside it.  Every other rank only renders, so
-max(rank 0's frame, a shard render) is the predicted N-GPU frame time without the transport.
+gathered frames into both row-major targets (side stream, `rows` tile rows in flight) running beside
+it, and another rank's shard render alone.  max(rank 0's frame, another rank's) is the predicted
+N-GPU frame time without the transport.  --root-ratio: rank 0's share relative to the others'
+(weighted partition, bh_partition; 1 = the plain interleave).
 
-    python tools/probe_rank0.py [--n 2,4,8] [--frame 4096x2048] [--D 8] [--rows 16] [--it 12]
-Prints one JSON line per N: render alone, render + unpack, unpack alone (ms per frame)."""
+    python tools/probe_rank0.py [--n 2,4,8] [--frame 4096x2048] [--D 8] [--rows 64] [--root-ratio 1,auto]
+Prints one JSON line per (N, rows, ratio), ms per frame."""
 import argparse
 import json
 import sys
@@ -20,7 +21,8 @@ def main():
     p.add_argument("--n", default="2,4,8")
     p.add_argument("--frame", default="4096x2048")
     p.add_argument("--D", type=int, default=8)
-    p.add_argument("--rows", default="16", help="comma list of tile rows in flight (0 = all)")
+    p.add_argument("--rows", default="64", help="comma list of tile rows in flight (0 = all)")
+    p.add_argument("--root-ratio", default="1", help="comma list: numbers or 'auto'")
     p.add_argument("--it", type=int, default=12)
     a = p.parse_args()
     import torch
@@ -31,53 +33,68 @@ def main():
     fmt = bh.BH_OUT_RGBA16F
     D = a.D
     sky = bh.synthetic_sky(4096, 2048)
-    for n, rows in ((int(v), int(r)) for v in a.n.split(",") for r in a.rows.split(",")):
-        stride = multigpu.packed_stride(W, H, n)
-        tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
-        scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
-        mine = torch.empty((D * stride, tb), dtype=torch.uint8, device=dev)
-        # the gathered launch: every rank's block of D frames (rank 0's own block is rendered for real
-        # once, the others are copies of it: the unpack's cost does not depend on the pixel values)
-        scene.render_frames([mine[f * stride:(f + 1) * stride] for f in range(D)], None, fmt=fmt,
-                            layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=0, shard_count=n)
-        gathered = mine.repeat(n, 1)
-        cols = [torch.empty((H, W, 4), dtype=torch.float16, device=dev) for _ in range(D)]
-        bos = [torch.empty_like(c) for c in cols]
-        rs = torch.cuda.current_stream()
-        ss = torch.cuda.Stream()
+    tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+    for n in (int(v) for v in a.n.split(",")):
+        for rr in a.root_ratio.split(","):
+            ratio = multigpu.auto_root_ratio(n) if rr == "auto" else float(rr)
+            weights = multigpu.root_weights(n, ratio)
+            part = bh.Partition(W, H, weights) if len(set(weights)) > 1 else None
+            counts = part.counts if part else [bh.shard_tile_count(W, H, k, n) for k in range(n)]
+            stride = max(counts)
+            kw = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_count=n, **({"partition": part} if part else {}))
+            for rows in (int(r) for r in a.rows.split(",")):
+                scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
+                bufs = [torch.empty((D * stride, tb), dtype=torch.uint8, device=dev) for _ in range(2)]
+                for k in (0, 1):  # the gathered launch: rank 0's and rank 1's blocks rendered for real
+                    scene.render_frames([bufs[k][f * stride:f * stride + counts[k]] for f in range(D)], None, fmt=fmt,
+                                        shard_index=k, **kw)
+                gathered = torch.cat([bufs[0], bufs[1]] + [bufs[1]] * (n - 2), 0)
+                cols = [torch.empty((H, W, 4), dtype=torch.float16, device=dev) for _ in range(D)]
+                bos = [torch.empty_like(c) for c in cols]
+                rs = torch.cuda.current_stream()
+                ss = torch.cuda.Stream()
 
-        def render():
-            scene.render_frames([mine[f * stride:(f + 1) * stride] for f in range(D)], None, fmt=fmt,
-                                layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=0, shard_count=n, stream=rs)
+                def render(k):
+                    scene.render_frames([bufs[k][f * stride:f * stride + counts[k]] for f in range(D)], None, fmt=fmt,
+                                        shard_index=k, stream=rs, **kw)
 
-        def unpack():
-            for f in range(D):
-                bh.tiles_unpack_rgbm(gathered[f * stride:], cols[f], bos[f], W, H, n, D * stride, fmt,
-                                     stream=ss, rows_in_flight=rows)
+                def unpack():
+                    for f in range(D):
+                        if part:
+                            bh.tiles_unpack_rgbm_partition(gathered[f * stride:], cols[f], bos[f], part, D * stride,
+                                                           fmt, stream=ss, rows_in_flight=rows)
+                        else:
+                            bh.tiles_unpack_rgbm(gathered[f * stride:], cols[f], bos[f], W, H, n, D * stride, fmt,
+                                                 stream=ss, rows_in_flight=rows)
 
-        def run(k, do_render, do_unpack):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            for _ in range(k):
-                if do_render:
-                    render()
-                if do_unpack:
-                    ev = torch.cuda.Event()
-                    ev.record(rs)
-                    ss.wait_event(ev)          # the bench's side stream waits for the receive
-                    unpack()                   # renders never wait for it (double-buffered receive)
-            torch.cuda.synchronize()
-            return (time.perf_counter() - t0) / (k * D) * 1e3
+                def run(k, shard, do_render, do_unpack):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(k):
+                        if do_render:
+                            render(shard)
+                        if do_unpack:
+                            ev = torch.cuda.Event()
+                            ev.record(rs)
+                            ss.wait_event(ev)  # the bench's side stream waits for the receive
+                            unpack()           # renders never wait for it (double-buffered receive)
+                    torch.cuda.synchronize()
+                    return (time.perf_counter() - t0) / (k * D) * 1e3
 
-        for _ in range(3):
-            run(4, True, True)
-        out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
-               "shard_tiles": bh.shard_tile_count(W, H, 0, n),
-               "render_ms": round(run(a.it, True, False), 4),
-               "render_plus_unpack_ms": round(run(a.it, True, True), 4),
-               "unpack_only_ms": round(run(a.it, False, True), 4)}
-        print(json.dumps(out), flush=True)
-        scene.close()
+                for _ in range(3):
+                    run(4, 0, True, True)
+                    run(2, 1, True, False)
+                r0 = run(a.it, 0, True, True)
+                r1 = run(a.it, 1, True, False)
+                out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
+                       "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": counts[:2],
+                       "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
+                       "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),
+                       "predicted_frame_ms": round(max(r0, r1), 4)}
+                print(json.dumps(out), flush=True)
+                scene.close()
+            if part:
+                part.close()
 
 
 if __name__ == "__main__":
