@@ -58,6 +58,10 @@ def parse(argv=None):
     # SURVEY §8d asks for 10 warm-up frames; 300 (0.25 s) let the clocks settle
     p.add_argument("--warmup", type=int, default=300)
     p.add_argument("--workload", choices=["strong", "config4", "weak"], default="strong")
+    p.add_argument("--config", type=int, choices=[1, 2, 3, 4, 5], default=0,
+                   help="BASELINE.json configs[N-1]: 1 = 256x256 cap 64 no surfaces camera A, 2 = 1920x1080 cap 256 "
+                        "camera B, 3 = the headline, 4 = 8192x4096 cap 512 split over the N GPUs, 5 = 4096x2048 cap "
+                        "1000 camera C (sets frame, cap, camera and scene; other flags still apply)")
     p.add_argument("--math", choices=["exact", "fast"], default="exact")
     p.add_argument("--schedule", choices=["tile", "tile-static", "pair", "persistent"], default="tile")
     p.add_argument("--variant", choices=["auto", "issue", "latency"], default="auto",
@@ -240,9 +244,25 @@ def plumbing(args, rank: int, n: int) -> int:
 
 # ---- the measurement ---------------------------------------------------------------------------------
 
+BASELINE_CONFIGS = {  # BASELINE.json configs -> bench flags (SURVEY §8d cameras)
+    1: dict(width=256, height=256, max_iters=64, camera="A", surfaces="off"),
+    2: dict(width=1920, height=1080, max_iters=256, camera="B"),
+    3: dict(max_iters=512, camera="A"),
+    4: dict(workload="config4", max_iters=512, camera="A"),
+    5: dict(max_iters=1000, camera="C"),
+}
+
+
+def apply_config(args):
+    """--config N: BASELINE.json configs[N-1]'s frame, cap, camera and scene."""
+    for k, v in BASELINE_CONFIGS.get(args.config, {}).items():
+        setattr(args, k, v)
+    return args
+
+
 def main() -> int:
     argv = sys.argv[1:]
-    args = parse(argv)
+    args = apply_config(parse(argv))
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -498,6 +518,7 @@ def main() -> int:
                             + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
                                                   "(RGB planes + blackout mask) to rank 0 overlapped with the next "
                                                   "frame, rank 0 unpacks col and blackout_col"),
+                "baseline_config": args.config or None,
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
                 "math": args.math,
                 "schedule": args.schedule, "format": args.fmt, "frames_per_launch": D,

@@ -47,3 +47,14 @@ def test_world_size_mismatch_is_refused():
     rc, lines, err = _bench("--gpus", "2", "--plumbing", env={"WORLD_SIZE": "3", "RANK": "0"})
     assert rc != 0 and not lines
     assert "refusing" in err
+
+
+@pytest.mark.parametrize("cfg,want", [(1, (256, 256, 64, "A", "off", "strong")), (2, (1920, 1080, 256, "B", "on", "strong")),
+                                      (3, (0, 0, 512, "A", "on", "strong")), (4, (0, 0, 512, "A", "on", "config4")),
+                                      (5, (0, 0, 1000, "C", "on", "strong"))])
+def test_config_flag_maps_the_baseline_configs(cfg, want):
+    """bench.py --config N selects BASELINE.json configs[N-1] (frame, cap, camera, scene, workload)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    a = bench.apply_config(bench.parse(["--config", str(cfg)]))
+    assert (a.width, a.height, a.max_iters, a.camera, a.surfaces, a.workload) == want
