@@ -544,11 +544,15 @@ def main() -> int:
                          "valu_busy": pmc.get("valu_busy_est"),
                          "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                          "pmc_source": pmc.get("source"),
+                         "issue_slot_frac": round(achieved_tf / (PEAK_FP32_TFLOPS / 2), 5),
                          "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps x "
                                  "frames_per_launch / avg launch time (HIP events on the render stream); FP32 "
                                  "VALU-bound, no MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU "
                                  "issue cycles / SIMD cycles, from the rocprofv3 PMC passes of this configuration "
-                                 "named in pmc_source (profiles/pmc_traffic.json), null if none"},
+                                 "named in pmc_source (profiles/pmc_traffic.json), null if none. The 157.3 TFLOP/s "
+                                 "peak counts an FMA as 2 flops in every lane-cycle; the WGSL's op sequence has no "
+                                 "FMA to contract (exact mode), so its ceiling is half that: issue_slot_frac = "
+                                 "achieved / 78.65 (DESIGN.md §6)"},
             "roofline_hbm": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": PEAK_HBM_GBS,
                              "unit": "GB/s", "frac": round(achieved_gbs / PEAK_HBM_GBS, 5),
                              "algorithmic_bytes_per_launch": alg_bytes,
