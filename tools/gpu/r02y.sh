@@ -1,5 +1,5 @@
 #!/bin/bash
 # rocprofv3 kernel trace + 4 PMC passes of every single-GPU configuration on the final round-2 build.
 set -u
-timeout -k 10 1500 bash tools/gpu/pmc_configs.sh r02f > gpurun_out/pmc_r02f.log 2>&1 || exit 11
+timeout -k 10 1500 bash tools/gpu/pmc_configs.sh r02g > gpurun_out/pmc_r02g.log 2>&1 || exit 11
 echo done
