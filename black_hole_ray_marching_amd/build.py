@@ -19,6 +19,9 @@ CSRC = PKG / "csrc"
 OBJ = PKG / "_build"
 LIB = PKG / "libbh_render.so"
 ORACLE_SRCS = [ROOT / "oracle" / "bh_oracle.c", ROOT / "oracle" / "bh_bloom_oracle.c"]
+EXAMPLE_SRC = ROOT / "examples" / "render_frame.c"
+EXAMPLE_BIN = ROOT / "examples" / "render_frame"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ORACLE_LIB = ROOT / "oracle" / "libbh_oracle.so"
 
 ARCH = os.environ.get("BH_OFFLOAD_ARCH", "gfx950")
@@ -91,9 +94,22 @@ def build_oracle(force: bool = False) -> Path:
     return ORACLE_LIB
 
 
+def build_example(force: bool = False) -> Path:
+    """examples/render_frame: a plain C11 host of the C ABI (gcc + the HIP runtime's C API, no torch)."""
+    if force or _stale(EXAMPLE_BIN, [EXAMPLE_SRC, ROOT / "include" / "bh_render.h", LIB, Path(__file__)]):
+        tmp = EXAMPLE_BIN.with_suffix(".tmp")
+        _run(["gcc", "-std=c11", "-O2", "-Wall", "-D__HIP_PLATFORM_AMD__", f"-I{ROOT / 'include'}",
+              f"-I{ROCM / 'include'}", str(EXAMPLE_SRC), "-o", str(tmp), f"-L{PKG}", "-lbh_render",
+              f"-L{ROCM / 'lib'}", "-lamdhip64", "-Wl,-rpath,$ORIGIN/../black_hole_ray_marching_amd",
+              f"-Wl,-rpath,{ROCM / 'lib'}", "-lm"])
+        os.replace(tmp, EXAMPLE_BIN)
+    return EXAMPLE_BIN
+
+
 def build_all(force: bool = False) -> None:
     build_product(force)
     build_oracle(force)
+    build_example(force)
 
 
 if __name__ == "__main__":
