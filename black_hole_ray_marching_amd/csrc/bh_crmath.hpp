@@ -97,5 +97,57 @@ constexpr uint32_t KEY_MIN = (0x21800000u << 1) - 1u;  // key(2^-60)
 __device__ __forceinline__ uint32_t key(float n) { return (__float_as_uint(n) << 1) - 1u; }
 __device__ __forceinline__ uint32_t kmin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
 
+
+// ---- atan2 rounded to f32 ----------------------------------------------------------------------
+// The normative shading angle is RN_f32(atan2(y, x)) evaluated in f64 (the oracle calls
+// the C library's f64 atan2, the first kernels ocml's).  atan2_core computes the f64 angle A in fewer
+// and cheaper operations than ocml's general f64 atan2 (whose IEEE division and degree-20 polynomial
+// with 64-bit literal coefficients took ~110 instructions per wave): octant reduction to
+// u = mn / mx, or (mn - mx) / (mn + mx) when mn / mx > tan(pi/8) (both exact in f64 for f32
+// inputs: the exponents are within 2 there), a reciprocal refined twice and one residual correction
+// (RN-accurate quotient), and atan(u) = u + u^3 P(u^2) with an 11-term Chebyshev fit on
+// [0, tan^2(pi/8)] (approximation error 2^-57, f64 evaluation ~2^-53; tools/atan2_coefs.py).  Its
+// relative error is below 2^-50, so RN_f32(A) equals RN_f32 of any f64 atan2 within an ulp of the
+// true angle unless A lies within 2^-45 |A| of an f32 rounding midpoint: atan2_near_mid flags those
+// (and zeros, tiny and non-finite cases) for the caller's fallback to the library call.
+constexpr double ATAN_P[11] = {-0x1.3a31b1c0fd3b7p-6, 0x1.4162c02b1dda3p-5, -0x1.a0999c632b6edp-5,
+                               0x1.dfe6497e96323p-5, -0x1.10fa77b1a6d57p-4, 0x1.3b1263064f6b9p-4,
+                               -0x1.745d0b28a7e37p-4, 0x1.c71c71853d7fap-4, -0x1.2492492436201p-3,
+                               0x1.999999999934cp-3, -0x1.5555555555555p-2};
+constexpr double PI_F64 = 0x1.921fb54442d18p+1, PI_2_F64 = 0x1.921fb54442d18p+0, PI_4_F64 = 0x1.921fb54442d18p-1;
+constexpr double TAN_PI_8 = 0x1.a827999fcef32p-2;
+
+struct Atan2 { float f; bool near; };
+__device__ __forceinline__ Atan2 atan2_core(float yf, float xf) {
+    const double x = (double)xf, y = (double)yf;
+    const double ax = fabs(x), ay = fabs(y);
+    const double mx = fmax(ax, ay), mn = fmin(ax, ay);
+    const bool big = mn > TAN_PI_8 * mx;
+    const double num = big ? mn - mx : mn, den = big ? mn + mx : mx;
+    double r = __builtin_amdgcn_rcp(den);
+    r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+    r = __builtin_fma(__builtin_fma(-den, r, 1.0), r, r);
+    double u = num * r;
+    u = __builtin_fma(__builtin_fma(-den, u, num), r, u);
+    const double s = u * u;
+    double p = ATAN_P[0];
+#pragma unroll
+    for (int k = 1; k < 11; ++k) p = __builtin_fma(p, s, ATAN_P[k]);
+    double a = __builtin_fma(u * s, p, u);
+    a = big ? a + PI_4_F64 : a;
+    a = ay > ax ? PI_2_F64 - a : a;
+    a = __builtin_signbit(x) ? PI_F64 - a : a;
+    a = __builtin_copysign(a, y);
+    const float f = (float)a;
+    // distance of A to the nearest f32 rounding midpoints around f (half an ulp of f; a quarter on the
+    // side below a power of two), exact in f64 (Sterbenz)
+    const double d = fabs(a - (double)f);
+    const double h = __builtin_ldexp(1.0, __builtin_amdgcn_frexp_expf(f) - 25);
+    const double tol = fabs(a) * 0x1p-45;
+    const bool near = (x != x) || (y != y) || !(mx > 0.0 && mx < 0x1p200) || !(fabs(a) >= 0x1p-120) ||
+                      fabs(d - h) <= tol || fabs(d - 0.5 * h) <= tol;
+    return {f, near};
+}
+
 }  // namespace crm
 }  // namespace bh

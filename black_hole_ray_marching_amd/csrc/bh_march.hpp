@@ -741,7 +741,13 @@ __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32
     const float x = (az + ONE_PI) / TWO_PI;                 // :334
 #else
     const v3 n = normalize_x(rd);
-    const float az = (float)atan2((double)n.z, (double)n.x);
+    // RN_f32 of the f64 atan2 (:332): the short f64 core, and the library call for the lanes whose angle
+    // lies too close to an f32 rounding midpoint for the core to decide (about 2^-21 of them)
+    const crm::Atan2 at = crm::atan2_core(n.z, n.x);
+    float az = at.f;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(at.near) != 0ull, 0)) {
+        if (at.near) az = (float)atan2((double)n.z, (double)n.x);
+    }
     // az + pi is +0 or in [2^-22, 7] (az is an f32 in [-RN(pi), RN(pi)]): inside the division core's
     // domain
     const float x = crm::div_core(az + ONE_PI, crm::Rcp{TWO_PI, 1.0f / TWO_PI});  // RN(1/2pi) folded

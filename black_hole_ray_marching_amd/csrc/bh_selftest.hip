@@ -34,6 +34,10 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 4: srgb_encode over every 32-bit pattern in [base, base + count) against a binary search of T
 // op 6: srgb_encode_lut (table form) against srgb_encode over every 32-bit pattern in [base, base + count)
 // op 5: div12 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
+// op 8: atan2_core (+ its library fallback where flagged) against (float)atan2((double)y, (double)x) on
+//       `count` random (y, x) pairs seeded by base: random directions, random magnitudes, and the
+//       special values (+-0, axes, diagonals, tiny); ex[0..3] of a mismatch = y, x, got, want
+// op 9: the unit-vector pairs of op 8 (10 of every 16); counts how many the core hands to the fallback
 // op 7: div_core over EVERY pair of significands (n, d) in [1, 2)^2 with d's 23 fraction bits in
 //       [base, base + count / 2^23): all 2^23 numerators per denominator (the full 2^46 square is
 //       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
@@ -87,6 +91,33 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             const float got = crm::div_core(n, crm::rcp_refined(d)), want = n / d;
             if (__float_as_uint(got) != __float_as_uint(want))
                 record(cnt, ex, __float_as_uint(n), __float_as_uint(d), __float_as_uint(got), __float_as_uint(want));
+        } else if (op == 8 || op == 9) {
+            const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
+            float y, x;
+            const uint32_t kind = (uint32_t)(h1 & 15u);
+            if (kind < 10) {  // a unit vector's (z, x) as the shading sees them
+                const float a = (float)((h2 >> 11) * 0x1p-53) * 6.283185307f, c = (float)((h1 >> 11) * 0x1p-53) * 2.0f - 1.0f;
+                const float r = sqrtf(fmaxf(0.0f, 1.0f - c * c));
+                y = r * sinf(a); x = r * cosf(a);
+            } else if (kind < 13) {
+                y = rnd_float(h1, -126, 10); x = rnd_float(h2, -126, 10);
+                if (op == 9) continue;  // op 9: the rate over unit vectors only
+            } else {
+                if (op == 9) continue;
+                const float sp[8] = {0.0f, -0.0f, 1.0f, -1.0f, 0x1p-130f, -0x1p-149f, 0.70710677f, 3.0f};
+                y = sp[(h2 >> 3) & 7u]; x = sp[(h2 >> 6) & 7u];
+                if ((h2 >> 9) & 1) x = y;       // diagonals
+                if ((h2 >> 10) & 1) x = -x;
+            }
+            const crm::Atan2 at = crm::atan2_core(y, x);
+            if (op == 9) {
+                if (at.near) record(cnt, ex, __float_as_uint(y), __float_as_uint(x), __float_as_uint(at.f), 0u);
+            } else {
+                const float got = at.near ? (float)atan2((double)y, (double)x) : at.f;
+                const float want = (float)atan2((double)y, (double)x);
+                if (__float_as_uint(got) != __float_as_uint(want) && !(got != got && want != want))
+                    record(cnt, ex, __float_as_uint(y), __float_as_uint(x), __float_as_uint(got), __float_as_uint(want));
+            }
         } else if (op == 2 || op == 3) {
             const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
             float d = fabsf(rnd_float(h1, -40, 59));
@@ -112,7 +143,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 7 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 9 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;

@@ -330,7 +330,9 @@ int bh_srgb_encode_table(float* out257);
  * binary search of bh_srgb_encode_table; op 5: x/12 as the bloom chain computes it, over bit
  * patterns [base, base+count); op 6: the bloom chain's table-form sRGB encoder against op 4's; op 7:
  * n/d over all 2^23 numerator significands for the denominator significands (fraction bits)
- * [base, base + count/2^23)).  *out_mismatches = number of differing results;
+ * [base, base + count/2^23); op 8: the shading's f32-rounded atan2 (short f64 core + library fallback)
+ * against (float)atan2((double)y, (double)x) on `count` random (y, x) pairs seeded by base; op 9:
+ * the number of those pairs the core hands to the fallback).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

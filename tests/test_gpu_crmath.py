@@ -75,3 +75,18 @@ def test_srgb_encode_table_form_exhaustive(lib):
     # the bloom chain's log-free encoder (bucket base codes + one threshold) over all 2^32 patterns
     m, ex = run(lib, 6, 0, 1 << 32)
     assert m == 0, ex
+
+
+def test_atan2_core_against_the_library(lib):
+    """The shading's f32-rounded atan2 (bh_crmath.hpp atan2_core + the library fallback where it flags a
+    near-midpoint angle) equals (float)atan2((double)y, (double)x) on 2^29 pairs: unit vectors as the
+    shading sees them, random magnitudes, zeros, axes and diagonals."""
+    m, ex = run(lib, 8, 20261016, 1 << 29)
+    assert m == 0, ex
+
+
+def test_atan2_core_fallback_is_rare(lib):
+    """Unit vectors handed to the library call: ~2e-6 of them (2^28 x 10/16 pairs; profiles/r02b)."""
+    n = 1 << 28
+    m, _ = run(lib, 9, 7, n)
+    assert m < n * 10 // 16 * 1e-5, m
