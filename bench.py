@@ -92,6 +92,10 @@ def parse(argv=None):
     p.add_argument("--plumbing", action="store_true",
                    help="no GPU: the N-rank launch, gather pipeline and RGBM unpack on CPU (gloo) with "
                         "synthetic shards (tests only; prints no measurement)")
+    p.add_argument("--rccl-dry-run", action="store_true",
+                   help="--gpus 1 only: run the N>1 code path with one rank -- an RCCL (nccl backend) process "
+                        "group of world size 1, RGBM shard render, pipelined dist.gather, rank-0 unpack -- to "
+                        "check the collectives on a 1-GPU box (development; not the N=1 measurement)")
     return p.parse_args(argv)
 
 
@@ -273,6 +277,9 @@ def main() -> int:
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure a different N")
     n = world
+    if args.rccl_dry_run and n != 1:
+        raise SystemExit("--rccl-dry-run runs one rank: use --gpus 1")
+    sharded = n > 1 or args.rccl_dry_run  # the N>1 code path (shards, gather, unpack)
     if args.plumbing:
         return plumbing(args, rank, n)
 
@@ -291,7 +298,9 @@ def main() -> int:
         raise SystemExit(f"--gpus {n}: only {torch.cuda.device_count()} GPUs visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if n > 1:
+    if sharded:
+        if args.rccl_dry_run and "MASTER_ADDR" not in os.environ:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
         if rehearsal:
             dist.init_process_group("gloo")
         else:
@@ -318,7 +327,7 @@ def main() -> int:
     sched = {"tile": bh.BH_SCHED_TILE, "tile-static": bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER,
              "pair": bh.BH_SCHED_PAIR, "persistent": bh.BH_SCHED_PERSISTENT}[args.schedule]
     sched |= {"auto": 0, "issue": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}[args.variant]
-    if n > 1 and args.schedule == "persistent":
+    if sharded and args.schedule == "persistent":
         raise SystemExit("N>1 ships BH_LAYOUT_TILES_RGBM shards: tile or pair schedule only")
 
     sky = bh.synthetic_sky(4096, 2048)
@@ -332,7 +341,7 @@ def main() -> int:
     if not 1 <= D <= bh.BH_MAX_FRAMES:
         raise SystemExit(f"--frames-per-launch must be 1..{bh.BH_MAX_FRAMES}")
     weights = None
-    if n == 1:
+    if not sharded:
         cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
         bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
         shard = dict(layout=bh.BH_LAYOUT_ROWMAJOR)
@@ -369,7 +378,8 @@ def main() -> int:
                                          stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
 
         pipe = multigpu.GatherPipeline(lambda: torch.empty((D * stride, tb), dtype=torch.uint8, device=dev),
-                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev))
+                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev),
+                                       collective=True if args.rccl_dry_run else None)
 
     launch_no = [0]
     frame_no = [0]   # frames launched so far (the orbit path's frame index)
@@ -396,7 +406,7 @@ def main() -> int:
         orbit.update({i: orbit_camera(bh, args.camera, i, W, H, args.orbit_deg) for i in range(args.warmup + args.steps + D)})
 
     graph = None
-    if args.graph and n == 1:
+    if args.graph and not sharded:
         # the temporal-order state is per (geometry, shard, stream): render once on the capture stream
         # (allocating that state), then capture on the same stream; replays run there too
         cap_stream = torch.cuda.Stream(dev)
@@ -435,7 +445,7 @@ def main() -> int:
     # the kernel runs on (kernel duration for the roofline)
     plan = sizes(args.steps)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
-    if n > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -447,11 +457,11 @@ def main() -> int:
     if pipe is not None:
         pipe.drain()
     torch.cuda.synchronize(dev)
-    if n > 1:
+    if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     per_rank = [elapsed]
-    if n > 1:
+    if sharded:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         gl = [torch.zeros_like(t) for _ in range(n)]
         dist.all_gather(gl, t)
@@ -464,7 +474,7 @@ def main() -> int:
     kern_avg_s = float(full.mean()) / 1e3                        # a full launch (D frames)
 
     gather_ok = None
-    if args.verify_gather and n > 1 and rank == 0:
+    if args.verify_gather and sharded and rank == 0:
         # every frame of the last launch against a single-GPU render of that frame's camera
         ref_c = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
         ref_b = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
@@ -485,7 +495,7 @@ def main() -> int:
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
     # (lower by the cycle fast-forward of the tile schedule) -- the roofline uses the latter.
-    px_shape = (H, W) if n == 1 else (stride * 64,)  # the layout's pixel index space
+    px_shape = (H, W) if not sharded else (stride * 64,)  # the layout's pixel index space
     nm = 1 if args.camera_path == "fixed" else D  # orbit: every frame of a launch (own cameras), averaged
     frame_no[0] = 0
     nrk_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
@@ -520,18 +530,20 @@ def main() -> int:
                             f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}"
                             + (f" orbiting {args.orbit_deg} deg/frame" if args.camera_path == "orbit" else "") + ", "
                             f"{args.fmt} col+blackout, {args.math} math"
-                            + ("" if n == 1 else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
+                            + ("" if not sharded else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
                                                   "(RGB planes + blackout mask) to rank 0 overlapped with the next "
                                                   "frame, rank 0 unpacks col and blackout_col"),
                 "baseline_config": args.config or None,
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
                 "math": args.math,
                 "schedule": args.schedule, "format": args.fmt, "frames_per_launch": D,
-                "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if n == 1
+                "parallelism": ("single GPU" + (", HIP graph replay" if graph is not None else "")) if not sharded
                                else f"tile-sharded x{n}"
                                + (f", weighted partition {weights} (rank 0 also unpacks)" if n > 1 and weights else "")
-                               + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else ""),
-                **({"partition_weights": weights, "tiles_per_rank_max": stride} if n > 1 else {}),
+                               + (" (REHEARSAL: all ranks on cuda:0, gloo; not a measurement)" if rehearsal else "")
+                               + (" (RCCL DRY RUN: the N>1 path at one rank; not the N=1 measurement)"
+                                  if args.rccl_dry_run else ""),
+                **({"partition_weights": weights, "tiles_per_rank_max": stride} if sharded else {}),
             },
             "kernel": {"name": f"bh::{kernel_ns(args, my_tiles, D, cap, dev)}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
                                + (", 3u>" if args.schedule.startswith("tile") and flags == 3
@@ -564,18 +576,18 @@ def main() -> int:
                              "note": "this rank's outputs (N>1: its RGBM shard, and on rank 0 the two "
                                      "unpacked targets) + the sky texture read once"},
         }
-        if n > 1:
+        if sharded:
             result["world_size"] = dist.get_world_size()
             result["backend"] = dist.get_backend()
             result["per_rank_s"] = [round(x, 6) for x in per_rank]
-        if args.no_cpu or n > 1:
+        if args.no_cpu or sharded:
             result["cpu_baseline"] = None
         else:
             result["cpu_baseline"], result["parity"] = _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched, fmt)
         if gather_ok is not None:
             result["gather_verified_bit_exact"] = gather_ok
         print(json.dumps(result), flush=True)
-    if n > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -211,10 +211,12 @@ class GatherPipeline:
     `side_stream` (rank 0, CUDA), on_frame is issued on that stream -- the unpack (HBM-bound) then
     overlaps the next frame's render (VALU-bound) instead of queueing behind it on the render
     stream; before a receive buffer is gathered into again, the render stream waits for the unpack
-    that read it (and RCCL's stream follows the render stream)."""
+    that read it (and RCCL's stream follows the render stream).  `collective`: gather through
+    torch.distributed even at world size 1 (default: only when world > 1; a one-rank group checks
+    the collective calls on a 1-GPU box)."""
 
     def __init__(self, make_buffer, rank: int, world: int, on_frame=None, depth: int = 2, group=None,
-                 side_stream=None):
+                 side_stream=None, collective=None):
         import torch
         if depth < 1:
             raise ValueError("depth >= 1")
@@ -229,6 +231,7 @@ class GatherPipeline:
         self.pending = []  # (frame, work) in submission order
         self.side = side_stream if rank == 0 else None
         self.consumed = [None] * depth  # per slot: event after the on_frame that read recv[slot]
+        self.collective = world > 1 if collective is None else bool(collective)
 
     def buffer(self, i: int):
         return self.bufs[i % self.depth]
@@ -236,15 +239,15 @@ class GatherPipeline:
     def submit(self, i: int) -> None:
         import torch.distributed as dist
         slot = i % self.depth
-        if self.world == 1:
+        if self.consumed[slot] is not None:  # the unpack that last read recv[slot] (side stream)
+            import torch
+            torch.cuda.current_stream().wait_event(self.consumed[slot])
+            self.consumed[slot] = None
+        if not self.collective:
             work = None
             if self.rank == 0:
                 self.recv[slot].copy_(self.bufs[slot])
         else:
-            if self.consumed[slot] is not None:
-                import torch
-                torch.cuda.current_stream().wait_event(self.consumed[slot])
-                self.consumed[slot] = None
             gl = list(self.recv[slot].view(self.world, *self.bufs[slot].shape).unbind(0)) if self.rank == 0 else None
             work = dist.gather(self.bufs[slot], gl, dst=0, group=self.group, async_op=True)
         self.pending.append((i, work))
@@ -261,9 +264,12 @@ class GatherPipeline:
                 self.on_frame(i, self.recv[slot])
             else:
                 import torch
+                producer = torch.cuda.current_stream()
                 with torch.cuda.stream(self.side):
                     if work is not None:
                         work.wait()  # the side stream: the received frame is complete
+                    else:
+                        self.side.wait_stream(producer)  # the local copy into recv[slot]
                     self.on_frame(i, self.recv[slot])
                     ev = torch.cuda.Event()
                     ev.record(self.side)

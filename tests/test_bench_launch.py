@@ -58,3 +58,24 @@ def test_config_flag_maps_the_baseline_configs(cfg, want):
     import bench
     a = bench.apply_config(bench.parse(["--config", str(cfg)]))
     assert (a.width, a.height, a.max_iters, a.camera, a.surfaces, a.workload) == want
+
+
+def test_rccl_dry_run_needs_one_rank():
+    rc, lines, err = _bench("--gpus", "2", "--rccl-dry-run", env={"WORLD_SIZE": "2"})
+    assert rc != 0 and not lines and "one rank" in err
+
+
+@pytest.mark.gpu
+def test_rccl_dry_run_gathers_bit_exact():
+    """The N>1 code path at one rank over a real RCCL group (nccl backend): RGBM shard render,
+    pipelined dist.gather on the GPU, rank-0 unpack of both targets, barrier and the max-over-ranks
+    all_gather -- the collectives the driver's 8-GPU run makes, checked on a 1-GPU box."""
+    pytest.importorskip("torch")
+    rc, lines, err = _bench("--gpus", "1", "--rccl-dry-run", "--verify-gather", "--steps", "16", "--warmup", "8",
+                            "--width", "1024", "--height", "512", timeout=300)
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    d = lines[0]
+    assert d["backend"] == "nccl" and d["world_size"] == 1 and d["n_gpus"] == 1
+    assert d["gather_verified_bit_exact"] is True
+    assert "RCCL DRY RUN" in d["config"]["parallelism"]
