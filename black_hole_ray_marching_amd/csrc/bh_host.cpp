@@ -64,6 +64,22 @@ int hip_fail(hipError_t e, const char* what) {
     return BH_ERR_HIP;
 }
 
+// Makes `device` current for one ABI call and restores the caller's device on every return path.
+struct DeviceScope {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != device) err = hipSetDevice(device);
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 // ---- glam 0.24 Vec3 subset (scalar f32, left-to-right association as glam writes it) ----------
 struct V3 { float x, y, z; };
 V3 v_add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
@@ -407,9 +423,8 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     hipError_t e = hipGetDeviceCount(&ndev);
     if (e != hipSuccess || ndev <= 0) { g_last_error = "no HIP device"; return BH_ERR_NO_DEVICE; }
     if (device < 0 || device >= ndev) { g_last_error = "device index out of range"; return BH_ERR_NO_DEVICE; }
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if ((e = hipSetDevice(device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    DeviceScope dev(device);
+    if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     bh_ctx* c = new (std::nothrow) bh_ctx();
     if (!c) return BH_ERR_OUT_OF_MEMORY;
     c->device = device;
@@ -441,7 +456,6 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
             c->grid_fast = (uint32_t)(cus * bh_march_blocks_per_cu_fast());
         }
     }
-    (void)hipSetDevice(prev);
     if (st != BH_OK) { bh_destroy(c); return st; }
     *out = c;
     return BH_OK;
@@ -449,9 +463,7 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
 
 int bh_destroy(bh_ctx* c) {
     if (!c) return BH_OK;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(c->device);
+    DeviceScope dev(c->device);
     if (c->sky) (void)hipFree(c->sky);
     if (c->lut) (void)hipFree(c->lut);
     if (c->enc) (void)hipFree(c->enc);
@@ -463,7 +475,6 @@ int bh_destroy(bh_ctx* c) {
         if (o.counters) (void)hipFree(o.counters);
     }
     for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
-    (void)hipSetDevice(prev);
     delete c;
     return BH_OK;
 }
@@ -523,7 +534,8 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     if (!c || !col || !blackout || !out || W == 0 || H == 0 || levels < 1 || levels > 12 || schedule > BH_BLOOM_LITERAL)
         return BH_ERR_INVALID_ARG;
     hipError_t e;
-    if ((e = hipSetDevice(c->device)) != hipSuccess) return hip_fail(e, "hipSetDevice");
+    DeviceScope dev(c->device);
+    if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;
     const BloomPlan P = bloom_plan(W, H, levels);
     const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) &&
@@ -775,26 +787,25 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     }
     if (a.n_tiles == 0) return BH_OK;
 
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    if (prev != c->device) (void)hipSetDevice(c->device);
+    DeviceScope dev(c->device);
+    if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uint32_t sched = d->schedule & 0xFFu;
     bh_ctx::OrderState* os = nullptr;
     if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
         // temporal order of this (geometry, shard, stream): allocated at its first render only
         int st = order_state(c, d, nt, s, &os);
-        if (st != BH_OK) { if (prev != c->device) (void)hipSetDevice(prev); return st; }
+        if (st != BH_OK) return st;
         if (!os->valid) {
             // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent
             hipError_t he = hipMemsetAsync(os->counters, 0, bh::ORDER_WORDS * sizeof(uint32_t), s);
             if (he == hipSuccess) he = hipMemsetAsync(os->tile_cost, 0, nt, s);
-            if (he != hipSuccess) { if (prev != c->device) (void)hipSetDevice(prev); return hip_fail(he, "temporal order reset"); }
+            if (he != hipSuccess) return hip_fail(he, "temporal order reset");
             os->valid = true;
         }
         int oe = bh_launch_build_order(os->tile_cost, a.n_tiles, a.order_block, a.order_centre, os->counters,
                                        os->order, s);
-        if (oe != 0) { os->valid = false; if (prev != c->device) (void)hipSetDevice(prev); return hip_fail((hipError_t)oe, "order kernels"); }
+        if (oe != 0) { os->valid = false; return hip_fail((hipError_t)oe, "order kernels"); }
         a.order = os->order;
         a.tile_cost = os->tile_cost;
         a.order_tot = os->counters;
@@ -803,7 +814,6 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
             : march_variant_issue_order(d, a.n_tiles, a.n_frames, c->cus)
                 ? bh_launch_march_exact(a, sched, c->counters, c->grid_exact, s)
                 : bh_launch_march_exact_lat(a, sched, c->counters, c->grid_exact, s);
-    if (prev != c->device) (void)hipSetDevice(prev);
     if (e != 0) {
         // the costs and their histogram are written together by the march kernel; without it they
         // may disagree, so the next frame of this state starts the temporal order afresh
@@ -925,33 +935,28 @@ int bh_partition_create(uint32_t width, uint32_t height, uint32_t S, const uint3
         list[P->offset[k] + index[t]] = (uint32_t)(t % tx_n) | (uint32_t)(t / tx_n) << 16;
         loc[t] = index[t] | k << 24;
     }
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(device);
-    hipError_t e;
-    if ((e = hipMalloc(&P->tile_list, n * 4)) != hipSuccess || (e = hipMalloc(&P->tile_loc, n * 4)) != hipSuccess ||
+    DeviceScope dev(device);
+    hipError_t e = dev.err;
+    if (e != hipSuccess || (e = hipMalloc(&P->tile_list, n * 4)) != hipSuccess || (e = hipMalloc(&P->tile_loc, n * 4)) != hipSuccess ||
         (e = hipMemcpy(P->tile_list, list.data(), n * 4, hipMemcpyHostToDevice)) != hipSuccess ||
         (e = hipMemcpy(P->tile_loc, loc.data(), n * 4, hipMemcpyHostToDevice)) != hipSuccess) {
         st = e == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "partition tables");
         if (P->tile_list) (void)hipFree(P->tile_list);
         if (P->tile_loc) (void)hipFree(P->tile_loc);
         delete P;
-        (void)hipSetDevice(prev);
         return st;
     }
-    (void)hipSetDevice(prev);
     *out = P;
     return BH_OK;
 }
 
 int bh_partition_destroy(bh_partition* P) {
     if (!P) return BH_OK;
-    int prev = 0;
-    (void)hipGetDevice(&prev);
-    (void)hipSetDevice(P->device);
-    if (P->tile_list) (void)hipFree(P->tile_list);
-    if (P->tile_loc) (void)hipFree(P->tile_loc);
-    (void)hipSetDevice(prev);
+    {
+        DeviceScope dev(P->device);
+        if (P->tile_list) (void)hipFree(P->tile_list);
+        if (P->tile_loc) (void)hipFree(P->tile_loc);
+    }
     delete P;
     return BH_OK;
 }
