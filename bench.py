@@ -390,9 +390,21 @@ def main() -> int:
             return None
         return [orbit[frame_no[0] + f] for f in range(nf)]
 
+    # the timed launches' bh_render_frames calls, prepared once (Scene.prepare_frames): one per pipeline
+    # slot for N > 1 (the slot's packed buffer), else one over cols / bos
+    if pipe is None:
+        batches = [scene.prepare_frames(cols, bos, fmt=fmt, schedule=sched, **shard)]
+    else:
+        batches = [scene.prepare_frames([buf[f * stride:(f + 1) * stride] for f in range(D)], None, fmt=fmt,
+                                        schedule=sched, **shard)
+                   for buf in (pipe.buffer(k) for k in range(pipe.depth))]
+
     def launch(nf, **kw):
-        """One bh_render_frames launch of nf <= D frames (this scene's camera, or the orbit path's)."""
-        if pipe is None:
+        """One bh_render_frames launch of nf <= D frames (this scene's camera, or the orbit path's); with
+        debug outputs (kw) an unprepared call."""
+        if not kw:
+            batches[launch_no[0] % len(batches)].render(n=nf, cameras=cams(nf), stream=stream)
+        elif pipe is None:
             scene.render_frames(cols[:nf], bos[:nf], cameras=cams(nf), fmt=fmt, stream=stream, schedule=sched,
                                 **shard, **kw)
         else:
@@ -470,8 +482,10 @@ def main() -> int:
     kern_ms = np.array([a.elapsed_time(b) for a, b in ev])       # per launch
     frames_in = np.array(plan, dtype=np.float64)
     kern_frame_s = float(kern_ms.sum() / frames_in.sum()) / 1e3   # launch time per frame
-    full = kern_ms[frames_in == D] if (frames_in == D).any() else kern_ms
-    kern_avg_s = float(full.mean()) / 1e3                        # a full launch (D frames)
+    sel = frames_in == D if (frames_in == D).any() else np.ones_like(frames_in, dtype=bool)
+    full = kern_ms[sel]                                          # the full launches (D frames), else all
+    kern_avg_s = float(full.mean()) / 1e3                        # their average duration
+    frames_avg = float(frames_in[sel].mean())                    # frames in each of them (D, or fewer)
 
     gather_ok = None
     if args.verify_gather and sharded and rank == 0:
@@ -508,8 +522,8 @@ def main() -> int:
     if rank == 0:
         value = W * H * args.steps / elapsed / 1e6
         # per launch: D frames' executed steps / the launch's average duration (HIP events)
-        achieved_tf = sum_steps * D * F_STEP[flags] / kern_avg_s / 1e12
-        alg_bytes = my_bytes * D + sky.nbytes
+        achieved_tf = sum_steps * frames_avg * F_STEP[flags] / kern_avg_s / 1e12
+        alg_bytes = int(my_bytes * frames_avg) + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
         pmc = _pmc_entry(W, H, cap, args, n, D)
         result = {
@@ -553,17 +567,20 @@ def main() -> int:
                        "max_ms": round(float(full.max()), 5), "ms_per_frame": round(kern_frame_s * 1e3, 5),
                        "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
                        "mean_n_rk": round(sum_nrk / (my_tiles * 64), 4), "frames_per_s": round(1.0 / kern_frame_s, 2),
-                       "note": "avg/min/max over full launches of frames_per_launch frames; sum_n_rk / sum_steps "
-                               "per frame (this rank's tiles)"},
+                       "frames_per_timed_launch": frames_avg,
+                       "note": "avg/min/max over the full launches of frames_per_launch frames (all launches when "
+                               "the timed frames fill none: frames_per_timed_launch); sum_n_rk / sum_steps per frame "
+                               "(this rank's tiles)"},
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
-                         "traffic": pmc.get("hbm_bytes_per_launch"),
+                         "traffic": (round(pmc["hbm_bytes_per_launch"] * frames_avg / D)
+                                     if pmc.get("hbm_bytes_per_launch") else None),
                          "valu_busy": pmc.get("valu_busy_est"),
                          "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                          "pmc_source": pmc.get("source"),
                          "issue_slot_frac": round(achieved_tf / (PEAK_FP32_TFLOPS / 2), 5),
                          "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps x "
-                                 "frames_per_launch / avg launch time (HIP events on the render stream); FP32 "
+                                 "frames_per_timed_launch / avg launch time (HIP events on the render stream); FP32 "
                                  "VALU-bound, no MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU "
                                  "issue cycles / SIMD cycles, from the rocprofv3 PMC passes of this configuration "
                                  "named in pmc_source (profiles/pmc_traffic.json), null if none. The 157.3 TFLOP/s "
@@ -607,12 +624,21 @@ def kernel_ns(args, tiles: int, D: int, cap: int, dev) -> str:
 
 
 def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
-    """Frames per launch: enough that each frame's serial tail (the few rays that march to the cap, ~0.9
-    us per step alone: DESIGN.md §5) overlaps the other frames' bulk.  Measured (tools/probe_inflight.py,
-    profiles/r02/inflight.log; ms per frame at D = 1/2/4/8): 4096x2048 0.658/0.633/0.621/0.614; its 1/8
-    shard 0.410/0.261/0.121/0.088; 8192x4096's 1/8 shard 0.612/0.334/0.323/0.317.  The most the kernel
-    argument carries (BH_MAX_FRAMES) is the best everywhere measured."""
-    return 8
+    """Frames per launch: enough that each frame's serial tail (the few rays that march to the cap, ~0.8
+    us per step alone: DESIGN.md §5) overlaps the other frames' bulk, and the per-launch cost (the order
+    kernel and the gaps around it, ~16 us) is shared by many frames.  Measured (tools/probe_inflight.py,
+    profiles/r02/inflight.log, profiles/r02b/frames_per_launch/; ms per frame at D = 1/2/4/8/16/32):
+    4096x2048 0.658/0.633/0.621/0.609/0.606/0.602; its 1/8 shard 0.410/0.261/0.121/0.088/0.083/0.080;
+    256x256 cap 64 (D = 8/16/32) 0.0095/0.0073/0.0068.  One GPU: the most the kernel argument carries
+    (BH_MAX_FRAMES = 32), best everywhere measured.  N > 1: 8 -- the last launch's gather and unpack
+    cannot overlap a next render, so the pipeline's drain grows with D (at N = 8 about D x 0.12 ms
+    against ~0.085 ms of render per frame) while the shard's render gains only ~8 % from 8 to 32."""
+    return bh_max_frames() if n == 1 else 8
+
+
+def bh_max_frames() -> int:
+    from black_hole_ray_marching_amd import _abi
+    return _abi.BH_MAX_FRAMES
 
 
 def pmc_key(W, H, cap, camera, math, schedule, fmt, n, D) -> str:

@@ -61,6 +61,9 @@ struct MarchArgs {
     uint32_t n_frames;
     FrameArgs frames[BH_MAX_FRAMES];
 };
+// passed by value: the kernel argument segment holds at most 4 KiB (with the persistent kernel's
+// extra pointer)
+static_assert(sizeof(MarchArgs) + 8 <= 4096, "MarchArgs must fit the kernel argument segment");
 
 // Shard ownership: tile (tx, ty) belongs to shard (tx + 3*ty) % S (SURVEY §8e diagonal interleave).
 // Row ty's first owned column for shard k.

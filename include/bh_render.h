@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 3
+#define BH_ABI_VERSION 4
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
@@ -244,7 +244,7 @@ int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* u
  * expensive tiles first), so the frames' serial tails -- the few rays that march to the cap -- overlap
  * each other's bulk instead of each ending a launch alone; other schedules run n launches.  The
  * temporal order of (geometry, shard, stream) learns from frame 0 of each call. */
-#define BH_MAX_FRAMES 8
+#define BH_MAX_FRAMES 32
 int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* cameras, const bh_uniforms* uniforms,
                      const bh_render_desc* descs, void* hip_stream);
 

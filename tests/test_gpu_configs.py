@@ -215,13 +215,13 @@ def test_renders_on_two_streams_keep_separate_order_state(torch_cuda, sky_small)
 
 
 @pytest.mark.parametrize("layout,S", [(bh.BH_LAYOUT_ROWMAJOR, 1), (bh.BH_LAYOUT_TILES_RGBM, 3)])
-@pytest.mark.parametrize("n", [1, 2, 5, 8])
+@pytest.mark.parametrize("n", [1, 2, 5, 8, bh.BH_MAX_FRAMES])
 def test_render_frames_equals_single_renders(torch_cuda, sky_small, n, layout, S):
     """bh_render_frames: n frames with DIFFERENT cameras in one launch (tiles interleaved across frames),
     each frame's targets and debug counters identical to its own bh_render, and to the oracle."""
     torch = torch_cuda
     W, H, cap = 96, 64, 512
-    names = ["A", "B", "C", "D", "E", "A", "B", "C"][:n]
+    names = (["A", "B", "C", "D", "E"] * 7)[:n]
     scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
     cams = [camera_uniform(c, W, H) for c in names]
     if layout == bh.BH_LAYOUT_ROWMAJOR:
@@ -256,9 +256,9 @@ def test_render_frames_equals_single_renders(torch_cuda, sky_small, n, layout, S
 def test_render_frames_rejects_mixed_descs(torch_cuda, sky_small):
     torch = torch_cuda
     scene = bh.Scene(32, 16, sky=sky_small)
-    a = [torch.zeros((16, 32, 4), device="cuda") for _ in range(9)]
+    a = [torch.zeros((16, 32, 4), device="cuda") for _ in range(bh.BH_MAX_FRAMES + 1)]
     with pytest.raises(bh.BhError):
-        scene.render_frames(a)                       # 9 > BH_MAX_FRAMES
+        scene.render_frames(a)                       # > BH_MAX_FRAMES
     d = (bh._abi.bh_render_desc * 2)()
     for i in range(2):
         d[i] = scene._desc(a[i], None, bh.BH_OUT_RGBA32F, None, None, None, bh.BH_LAYOUT_ROWMAJOR, 0, 1,
@@ -336,4 +336,34 @@ def test_partition_rejects_mismatches(torch_cuda, sky_small):
                      partition=other)
     other.close()
     part.close()
+    scene.close()
+
+
+def test_prepared_frames_equal_render_frames(torch_cuda, sky_small):
+    """Scene.prepare_frames + FrameBatch.render (the bench's launches): the first n of the prepared
+    frames, each camera its own, equal render_frames' bytes; a batch rejects n outside 1..len."""
+    torch = torch_cuda
+    W, H = 96, 64
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=512, math=bh.BH_MATH_EXACT)
+    cams = [camera_uniform(c, W, H) for c in ["A", "B", "C", "D", "E"]]
+    mk = lambda: torch.full((H, W, 4), float("nan"), device="cuda")  # noqa: E731
+    outs, bos = [mk() for _ in cams], [mk() for _ in cams]
+    batch = scene.prepare_frames(outs, bos, fmt=bh.BH_OUT_RGBA32F)
+    for n in (5, 3, 1):
+        for o in outs + bos:
+            o.fill_(float("nan"))
+        batch.render(n=n, cameras=cams[:n])
+        ro, rb = [mk() for _ in range(n)], [mk() for _ in range(n)]
+        scene.render_frames(ro, rb, cameras=cams[:n], fmt=bh.BH_OUT_RGBA32F)
+        torch.cuda.synchronize()
+        for i in range(n):
+            assert torch.equal(outs[i].view(torch.int32), ro[i].view(torch.int32)), (n, i)
+            assert torch.equal(bos[i].view(torch.int32), rb[i].view(torch.int32)), (n, i)
+        for i in range(n, len(cams)):
+            assert torch.isnan(outs[i]).all()  # frames past n are not rendered
+    for bad in (0, 6):
+        with pytest.raises(bh.BhError):
+            batch.render(n=bad)
+    with pytest.raises(bh.BhError):
+        batch.render(n=2, cameras=cams[:3])
     scene.close()
