@@ -298,8 +298,12 @@ def test_partition_shards_unpack_both_targets(torch_cuda, sky_full, weights, fmt
             if part.counts[k] == 0:
                 continue
             blk = packed[k * D * stride:(k + 1) * D * stride]
-            scene.render_frames([blk[f * stride:f * stride + part.counts[k]] for f in range(D)], None, cameras=cams,
-                                fmt=fmt, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=k, shard_count=S, partition=part)
+            frames = [blk[f * stride:f * stride + part.counts[k]] for f in range(D)]
+            kw = dict(fmt=fmt, layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=k, shard_count=S, partition=part)
+            if rep == 0:
+                scene.render_frames(frames, None, cameras=cams, **kw)
+            else:  # the bench's N > 1 launches: a prepared call (Scene.prepare_frames)
+                scene.prepare_frames(frames, None, **kw).render(cameras=cams)
     for f, cu in enumerate(cams):
         scene.camera_uniform = cu
         ref_c = torch.zeros((H, W, 4), dtype=dt, device="cuda")
