@@ -85,7 +85,7 @@ def parse(argv=None):
     p.add_argument("--verify-gather", action="store_true",
                    help="N>1: rank 0 compares both assembled targets with its own full-frame render (bitwise)")
     p.add_argument("--frames-per-launch", type=int, default=0,
-                   help="frames rendered by one bh_render_frames launch (1..8; 0 = auto, DESIGN.md §5 item 9)")
+                   help="frames rendered by one bh_render_frames launch (1..256; 0 = auto, DESIGN.md §5 item 9)")
     p.add_argument("--root-ratio", default="auto",
                    help="N>1: rank 0's tile share relative to each other rank's (it also unpacks every frame): "
                         "'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain (tx + 3ty) %% N interleave")
@@ -560,8 +560,8 @@ def main() -> int:
                 **({"partition_weights": weights, "tiles_per_rank_max": stride} if sharded else {}),
             },
             "kernel": {"name": f"bh::{kernel_ns(args, my_tiles, D, cap, dev)}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
-                               + (", 3u>" if args.schedule.startswith("tile") and flags == 3
-                                  else (", 4294967295u>" if args.schedule.startswith("tile") else ">")),
+                               + ((f", {flags}u>" if flags in (0, 3) else ", 4294967295u>")  # SF: 0/3 folded, else dynamic
+                                  if args.schedule.startswith("tile") else ">"),
                        "launches": len(plan), "frames_per_launch": D, "tiles_per_frame": my_tiles,
                        "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(full.min()), 5),
                        "max_ms": round(float(full.max()), 5), "ms_per_frame": round(kern_frame_s * 1e3, 5),
@@ -629,11 +629,20 @@ def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     kernel and the gaps around it, ~16 us) is shared by many frames.  Measured (tools/probe_inflight.py,
     profiles/r02/inflight.log, profiles/r02b/frames_per_launch/; ms per frame at D = 1/2/4/8/16/32):
     4096x2048 0.658/0.633/0.621/0.609/0.606/0.602; its 1/8 shard 0.410/0.261/0.121/0.088/0.083/0.080;
-    256x256 cap 64 (D = 8/16/32) 0.0095/0.0073/0.0068.  One GPU: the most the kernel argument carries
-    (BH_MAX_FRAMES = 32), best everywhere measured.  N > 1: 8 -- the last launch's gather and unpack
-    cannot overlap a next render, so the pipeline's drain grows with D (at N = 8 about D x 0.12 ms
+    256x256 cap 64 (D = 8/16/32) 0.0095/0.0073/0.0068.  One GPU: 32 (the frames the kernel argument
+    carries), and for frames of fewer than 16384 tiles enough frames for ~2^19 tiles per launch (up to
+    BH_MAX_FRAMES = 256, staged through the device frame table): 256x256 cap 64 at D = 32/64/128/256
+    0.00643/0.00620/0.00608/0.00604, 1920x1080 at D = 32/64/128 0.1500/0.1498/0.1492, the headline at
+    D = 32/64 0.6078/0.6074 (profiles/r02c/frames_table/).  N > 1: 8 -- the last launch's gather and
+    unpack cannot overlap a next render, so the pipeline's drain grows with D (at N = 8 about D x 0.12 ms
     against ~0.085 ms of render per frame) while the shard's render gains only ~8 % from 8 to 32."""
-    return bh_max_frames() if n == 1 else 8
+    if n > 1:
+        return 8
+    tiles = ((W + 7) // 8) * ((H + 7) // 8)
+    D = 32
+    while D < bh_max_frames() and tiles * D < (1 << 19):
+        D *= 2
+    return D
 
 
 def bh_max_frames() -> int:

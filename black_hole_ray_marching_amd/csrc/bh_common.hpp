@@ -7,6 +7,11 @@
 
 namespace bh {
 
+// Frames whose arguments travel inline in the kernel argument; a bh_render_frames call of more
+// (up to BH_MAX_FRAMES) stages them in a device table (bh_host.cpp, FrameTable).
+constexpr uint32_t BH_INLINE_FRAMES = 32;
+static_assert(BH_INLINE_FRAMES <= BH_MAX_FRAMES, "inline frames");
+
 // The per-frame part of a launch that renders several frames (bh_render_frames): camera, the
 // photon-sphere centre derived from its position, and the frame's outputs.
 struct FrameArgs {
@@ -57,9 +62,11 @@ struct MarchArgs {
     uint16_t* dbg_n_rk;
     uint8_t* dbg_fate;
     uint16_t* dbg_steps;
-    // frames of one launch (bh_render_frames): wave slot s marches frame s % n_frames, tile s / n_frames
+    // frames of one launch (bh_render_frames): wave slot s marches frame s % n_frames, tile s / n_frames;
+    // up to BH_INLINE_FRAMES of them inline, more from a device table (frame_table, else null)
     uint32_t n_frames;
-    FrameArgs frames[BH_MAX_FRAMES];
+    const FrameArgs* frame_table;
+    FrameArgs frames[BH_INLINE_FRAMES];
 };
 // passed by value: the kernel argument segment holds at most 4 KiB (with the persistent kernel's
 // extra pointer)

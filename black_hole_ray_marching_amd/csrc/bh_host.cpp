@@ -3,6 +3,7 @@
 // fails with a status code.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -31,7 +32,8 @@ struct bh_ctx {
     // and renders on different streams (frames in flight) never share costs or counters.
     struct OrderState {
         uint32_t width = 0, height = 0, shard_index = 0, shard_count = 0;
-        const void* partition = nullptr;
+        uint64_t partition = 0;              // bh_partition::serial, 0 = none
+        uint64_t n_tiles = 0;                // the buffers' size in tiles
         void* stream = nullptr;
         uint64_t last_use = 0;
         bool valid = false;                  // costs and histogram agree (false: start afresh)
@@ -41,6 +43,19 @@ struct bh_ctx {
     };
     std::vector<OrderState> orders;
     uint64_t order_clock = 0;
+    // per-frame arguments of bh_render_frames calls of more than BH_INLINE_FRAMES frames, one table per
+    // stream: the kernels of one stream run in order, so one device table serves every call on it; the
+    // host writes a pinned slot of a ring and copies it in on the stream (the slot is reused once its
+    // copy has run: its event)
+    static constexpr uint32_t FRAME_RING = 4;
+    struct FrameTable {
+        void* stream = nullptr;
+        bh::FrameArgs* dev = nullptr;                 // BH_MAX_FRAMES entries
+        bh::FrameArgs* host[FRAME_RING] = {};         // pinned, BH_MAX_FRAMES entries each
+        hipEvent_t done[FRAME_RING] = {};             // the slot's copy has executed
+        uint32_t next = 0;
+    };
+    std::vector<FrameTable> frame_tables;
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
     std::vector<uint32_t*> bloom_tex;
     uint64_t bloom_key = ~0ull;
@@ -53,7 +68,11 @@ struct bh_partition {
     std::vector<uint32_t> count, offset;  // per shard: tiles, first entry in tile_list
     uint32_t* tile_list = nullptr;        // device: every shard's tiles in packed order (tx | ty << 16)
     uint32_t* tile_loc = nullptr;         // device: per tile (ty * tiles_x + tx): packed index | shard << 24
+    uint64_t serial = 0;                  // unique per created partition: the temporal-order key (an
+                                          // address can be reused by a later partition)
 };
+static std::atomic<uint64_t> g_partition_serial{0};
+static void free_frame_table(bh_ctx::FrameTable& t);
 
 namespace {
 
@@ -475,6 +494,7 @@ int bh_destroy(bh_ctx* c) {
         if (o.counters) (void)hipFree(o.counters);
     }
     for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
+    for (auto& t : c->frame_tables) free_frame_table(t);
     delete c;
     return BH_OK;
 }
@@ -649,19 +669,72 @@ static bool march_variant_issue_order(const bh_render_desc* d, uint32_t n_tiles,
     return tiles * 512ull >= 384ull * (cus ? cus : 256u) * d->max_iters;
 }
 
+static void free_frame_table(bh_ctx::FrameTable& t) {
+    for (uint32_t k = 0; k < bh_ctx::FRAME_RING; ++k) {
+        if (t.done[k]) { (void)hipEventSynchronize(t.done[k]); (void)hipEventDestroy(t.done[k]); }
+        if (t.host[k]) (void)hipHostFree(t.host[k]);
+    }
+    if (t.dev) (void)hipFree(t.dev);
+    t = bh_ctx::FrameTable{};
+}
+
+// Stage the n frames' arguments in the device table of stream s (created at its first use): a pinned
+// ring slot is filled once its previous copy has executed, then copied in on the stream, ahead of the
+// order and march kernels that read it.  *dev receives the table.
+static int stage_frame_table(bh_ctx* c, hipStream_t s, const bh::FrameArgs* frames, uint32_t n,
+                             const bh::FrameArgs** dev) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        g_last_error = "bh_render_frames: more than 32 frames per call cannot be captured into a graph";
+        return BH_ERR_UNSUPPORTED;
+    }
+    bh_ctx::FrameTable* t = nullptr;
+    for (auto& x : c->frame_tables)
+        if (x.stream == (void*)s) t = &x;
+    if (!t) {
+        bh_ctx::FrameTable n_t;
+        n_t.stream = (void*)s;
+        const size_t bytes = sizeof(bh::FrameArgs) * BH_MAX_FRAMES;
+        hipError_t he = hipMalloc(&n_t.dev, bytes);
+        for (uint32_t k = 0; he == hipSuccess && k < bh_ctx::FRAME_RING; ++k) {
+            he = hipHostMalloc(&n_t.host[k], bytes, hipHostMallocDefault);
+            if (he == hipSuccess) he = hipEventCreateWithFlags(&n_t.done[k], hipEventDisableTiming);
+        }
+        if (he != hipSuccess) {
+            free_frame_table(n_t);
+            return he == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(he, "frame table");
+        }
+        c->frame_tables.push_back(n_t);
+        t = &c->frame_tables.back();
+    }
+    const uint32_t k = t->next;
+    t->next = (k + 1u) % bh_ctx::FRAME_RING;
+    hipError_t he = hipEventSynchronize(t->done[k]);  // a never-recorded event is complete
+    if (he == hipSuccess) {
+        std::memcpy(t->host[k], frames, sizeof(bh::FrameArgs) * n);
+        he = hipMemcpyAsync(t->dev, t->host[k], sizeof(bh::FrameArgs) * n, hipMemcpyHostToDevice, s);
+    }
+    if (he == hipSuccess) he = hipEventRecord(t->done[k], s);
+    if (he != hipSuccess) return hip_fail(he, "frame table upload");
+    *dev = t->dev;
+    return BH_OK;
+}
+
 // The temporal-order state of (geometry, shard, stream): found, or created (allocating; the LRU state
 // is evicted beyond BH_ORDER_STATES).  New states start with all costs 0 and an empty histogram.
 static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStream_t s, bh_ctx::OrderState** out) {
+    const uint64_t pser = d->partition ? d->partition->serial : 0u;
     for (auto& o : c->orders)
         if (o.width == d->width && o.height == d->height && o.shard_index == d->shard_index &&
-            o.shard_count == d->shard_count && o.partition == (const void*)d->partition && o.stream == (void*)s) {
+            o.shard_count == d->shard_count && o.partition == pser && o.n_tiles == nt && o.stream == (void*)s) {
             o.last_use = ++c->order_clock;
             *out = &o;
             return BH_OK;
         }
     bh_ctx::OrderState n;
     n.width = d->width; n.height = d->height; n.shard_index = d->shard_index; n.shard_count = d->shard_count;
-    n.partition = d->partition;
+    n.partition = pser;
+    n.n_tiles = nt;
     n.stream = (void*)s;
     const size_t cw = bh::ORDER_WORDS * sizeof(uint32_t);
     hipError_t he;
@@ -776,9 +849,12 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     // k = (DP * RS) * -1.5 (:126); the per-frame fields (camera, c_ps, outputs)
     a.kfac = (a.dp * a.rs) * -1.5f;
     a.n_frames = n_frames;
-    for (uint32_t i = 0; i < n_frames; ++i) frame_args(&cams[i], a.rs, &descs[i], &a.frames[i]);
+    std::vector<bh::FrameArgs> table;  // n_frames > BH_INLINE_FRAMES: staged in the stream's device table
+    if (n_frames > bh::BH_INLINE_FRAMES) table.resize(n_frames);
+    bh::FrameArgs* fa = table.empty() ? a.frames : table.data();
+    for (uint32_t i = 0; i < n_frames; ++i) frame_args(&cams[i], a.rs, &descs[i], &fa[i]);
     {
-        const bh::FrameArgs& F = a.frames[0];
+        const bh::FrameArgs& F = fa[0];
         for (int k = 0; k < 3; ++k) {
             a.pos[k] = F.pos[k]; a.c0[k] = F.c0[k]; a.c1[k] = F.c1[k]; a.c2[k] = F.c2[k]; a.cps[k] = F.cps[k];
         }
@@ -791,6 +867,10 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const uint32_t sched = d->schedule & 0xFFu;
+    if (!table.empty()) {
+        const int st = stage_frame_table(c, s, table.data(), n_frames, &a.frame_table);
+        if (st != BH_OK) return st;
+    }
     bh_ctx::OrderState* os = nullptr;
     if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
         // temporal order of this (geometry, shard, stream): allocated at its first render only
@@ -925,6 +1005,7 @@ int bh_partition_create(uint32_t width, uint32_t height, uint32_t S, const uint3
     if (!P) return BH_ERR_OUT_OF_MEMORY;
     P->width = width; P->height = height; P->shard_count = S; P->tiles_x = tx_n; P->tiles_y = ty_n;
     P->device = device;
+    P->serial = ++g_partition_serial;
     P->count.assign(S, 0);
     for (size_t t = 0; t < n; ++t) ++P->count[owner[t]];
     P->offset.assign(S, 0);

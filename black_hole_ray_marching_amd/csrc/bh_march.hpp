@@ -424,7 +424,11 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
     float rho2, qm;
     const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
-    X.sq_args(rho2, qm);
+    // the root guards of the enabled terms (a disabled term's value is discarded; a kernel built for
+    // one flag set drops its arithmetic entirely)
+    if constexpr (SF == SF_DYN || SF == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
+    else if constexpr (SF == BH_SCENE_DISC) X.sq_arg(rho2);
+    else if constexpr (SF == BH_SCENE_MARKERS) X.sq_arg(qm);
     const bool surface = ds < MIN_DIST;                                // :286-288
     if constexpr (BRANCHY) {
         if (blackout | surface) {
@@ -588,7 +592,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const float m = crm::sqrt_core(qm) - 0.5f;
     const float ds = fminf((scene_flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
                            (scene_flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
-    G.bad |= crm::sqrt_bad2(rho2, qm);
+    if constexpr (SF == SF_DYN || SF == BH_SCENE_DEFAULT) G.bad |= crm::sqrt_bad2(rho2, qm);
+    else if constexpr (SF == BH_SCENE_DISC) G.bad |= crm::sqrt_bad(rho2);
+    else if constexpr (SF == BH_SCENE_MARKERS) G.bad |= crm::sqrt_bad(qm);
     const bool surface = ds < MIN_DIST;
     if (blackout | surface) {
         fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
@@ -967,7 +973,10 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         fi = slot - j * nf;
     }
     MarchArgs a = A;
-    select_camera(a, A.frames[fi]);  // frames[0] == the top-level fields for a one-frame launch
+    // frames[0] == the top-level fields for a one-frame launch; launches of more than
+    // BH_INLINE_FRAMES frames read them from the device table (wave-uniform index: one load per wave)
+    if (A.frame_table) select_camera(a, A.frame_table[fi]);
+    else select_camera(a, A.frames[fi]);
     if (fi != 0u) a.tile_cost = nullptr;
     const uint32_t t = a.order ? a.order[j] : centre_out(j, a.n_tiles, a.order_block, a.order_centre);
     if (t >= a.n_tiles) return;  // defensive: a corrupt order must not address outside the shard
@@ -1033,7 +1042,8 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         // workgroups per CU resident (MI355X_MICROARCH.md, Residency)
         uint32_t fo = fi;
         asm volatile("" : "+s"(fo));
-        select_outputs(a, A.frames[fo]);
+        if (A.frame_table) select_outputs(a, A.frame_table[fo]);
+        else select_outputs(a, A.frames[fo]);
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
     }
     if (a.tile_cost) {

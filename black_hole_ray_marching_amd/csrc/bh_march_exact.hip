@@ -22,6 +22,8 @@ int launch(const bh::MarchArgs& a, uint32_t schedule, uint32_t* counters, uint32
     if (schedule == BH_SCHED_TILE) {
         if (a.scene_flags == BH_SCENE_DEFAULT)  // the reference's scene: flags folded at compile time
             bh::BH_NS::launch_tile_schedule<FMT, BH_SCENE_DEFAULT>(a, s);
+        else if (a.scene_flags == 0u)  // no surfaces (BASELINE config 1): the sdf folds to +inf
+            bh::BH_NS::launch_tile_schedule<FMT, 0u>(a, s);
         else
             bh::BH_NS::launch_tile_schedule<FMT, bh::BH_NS::SF_DYN>(a, s);
     } else if (schedule == BH_SCHED_PAIR) {

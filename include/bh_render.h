@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 4
+#define BH_ABI_VERSION 5
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
@@ -243,8 +243,11 @@ int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* u
  * schedule the frames' tiles are interleaved in one grid (slot s = tile s / n of frame s % n, most
  * expensive tiles first), so the frames' serial tails -- the few rays that march to the cap -- overlap
  * each other's bulk instead of each ending a launch alone; other schedules run n launches.  The
- * temporal order of (geometry, shard, stream) learns from frame 0 of each call. */
-#define BH_MAX_FRAMES 32
+ * temporal order of (geometry, shard, stream) learns from frame 0 of each call.  Up to 32 frames travel
+ * in the kernel argument; a call of more stages the frames' arguments through a pinned host ring into a
+ * device table of the stream (allocated at the first such call, never captured into a HIP graph: a
+ * capturing stream gets BH_ERR_UNSUPPORTED for n_frames > 32). */
+#define BH_MAX_FRAMES 256
 int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* cameras, const bh_uniforms* uniforms,
                      const bh_render_desc* descs, void* hip_stream);
 

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     lib = bh.load()
-    assert lib.bh_abi_version() == _abi.ABI_VERSION == 4
+    assert lib.bh_abi_version() == _abi.ABI_VERSION == 5
     assert lib.bh_status_string(0) == b"ok"
     assert lib.bh_status_string(-1) == b"invalid argument"
 

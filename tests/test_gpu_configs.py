@@ -215,13 +215,14 @@ def test_renders_on_two_streams_keep_separate_order_state(torch_cuda, sky_small)
 
 
 @pytest.mark.parametrize("layout,S", [(bh.BH_LAYOUT_ROWMAJOR, 1), (bh.BH_LAYOUT_TILES_RGBM, 3)])
-@pytest.mark.parametrize("n", [1, 2, 5, 8, bh.BH_MAX_FRAMES])
+@pytest.mark.parametrize("n", [1, 2, 5, 8, 32, 33, 100, bh.BH_MAX_FRAMES])
 def test_render_frames_equals_single_renders(torch_cuda, sky_small, n, layout, S):
     """bh_render_frames: n frames with DIFFERENT cameras in one launch (tiles interleaved across frames),
-    each frame's targets and debug counters identical to its own bh_render, and to the oracle."""
+    each frame's targets and debug counters identical to its own bh_render, and to the oracle.  Up to
+    32 frames travel in the kernel argument, more through the stream's device frame table."""
     torch = torch_cuda
     W, H, cap = 96, 64, 512
-    names = (["A", "B", "C", "D", "E"] * 7)[:n]
+    names = [["A", "B", "C", "D", "E"][i % 5] for i in range(n)]
     scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
     cams = [camera_uniform(c, W, H) for c in names]
     if layout == bh.BH_LAYOUT_ROWMAJOR:
@@ -247,7 +248,7 @@ def test_render_frames_equals_single_renders(torch_cuda, sky_small, n, layout, S
             assert torch.equal(outs[i].view(torch.uint8), o1.view(torch.uint8)), (rep, i, names[i])
             assert torch.equal(bos[i].view(torch.uint8), b1.view(torch.uint8)), (rep, i, names[i])
             assert torch.equal(nrk[i], n1), (rep, i)
-            if layout == bh.BH_LAYOUT_ROWMAJOR:
+            if layout == bh.BH_LAYOUT_ROWMAJOR and (i < 5 or i == n - 1):
                 o = oracle.render_rows(cu.to_bytes(), bytes(uniforms().to_c()), sky_small, W, H, cap, 3)
                 assert np.array_equal(o1.cpu().numpy().view(np.uint32), o[0].view(np.uint32))
     scene.close()
@@ -316,6 +317,36 @@ def test_partition_shards_unpack_both_targets(torch_cuda, sky_full, weights, fmt
         assert torch.equal(out_c.view(torch.uint8), ref_c.view(torch.uint8)), (weights, f)
         assert torch.equal(out_b.view(torch.uint8), ref_b.view(torch.uint8)), (weights, f)
     part.close()
+    scene.close()
+
+
+def test_partition_replaced_keeps_its_own_order_state(torch_cuda, sky_small):
+    """A partition destroyed and another created in its place (the allocator may hand out the same
+    address) never inherits the first one's temporal-order state: the state is keyed by the
+    partition's serial and the shard's tile count, so a larger shard gets buffers of its own size."""
+    torch = torch_cuda
+    W, H = 96, 64
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=512, math=bh.BH_MATH_EXACT)
+    fmt = bh.BH_OUT_RGBA16F
+    tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+    ref_c = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
+    ref_b = torch.zeros_like(ref_c)
+    scene.render(ref_c, ref_b, fmt=fmt)
+    for weights in ([5, 1], [1, 5], [1, 1], [1, 7]):  # shard 1 grows from the first partition to the next
+        part = bh.Partition(W, H, weights)
+        stride = max(part.counts)
+        packed = torch.zeros((2 * stride, tb), dtype=torch.uint8, device="cuda")
+        for rep in range(2):  # the second render runs the learned order
+            for k in range(2):
+                scene.render(packed[k * stride:k * stride + part.counts[k]], None, fmt=fmt,
+                             layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=k, shard_count=2, partition=part)
+        out_c = torch.full_like(ref_c, 7)
+        out_b = torch.full_like(ref_c, 7)
+        bh.tiles_unpack_rgbm_partition(packed, out_c, out_b, part, stride, fmt)
+        torch.cuda.synchronize()
+        assert torch.equal(out_c.view(torch.uint8), ref_c.view(torch.uint8)), weights
+        assert torch.equal(out_b.view(torch.uint8), ref_b.view(torch.uint8)), weights
+        part.close()
     scene.close()
 
 
