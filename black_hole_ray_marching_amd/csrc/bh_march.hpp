@@ -1001,15 +1001,19 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
         // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
-        // writes its input, so no per-step register copies); `in_b` records which one holds the
-        // lane's final state: the output of its last iteration, or its input for the fates decided
-        // before the RK update.  The trip condition is wave-uniform and each lane's iteration is
+        // writes its input, so no per-step register copies).  The lane's final state is the output
+        // of its last iteration, or its input for the fates decided before the RK update: the one of
+        // st / sb with the larger n_rk, once a lane leaving before the RK update has zeroed the
+        // other's n_rk (it may hold a discarded output of the guarded first pass).  The input of
+        // iteration i holds n_rk = i and the other register i - 1 or (i = 0) the same state, so no
+        // per-step flag records where the state is (-6 VALU per step: headline -0.5 %, A/B r02,
+        // profiles/r02c/ab_inb/).  The trip condition is wave-uniform and each lane's iteration is
         // predicated: with a divergent loop exit the state would be live out of the loop at a
         // different iteration per lane, which costs a register copy of every state value per
         // iteration.  (390 -> 370 VALU per step; with the flag template and the guard pooling
         // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
         RayState sb = st;
-        bool in_b = false, alive = true;
+        bool alive = true;
         // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
         // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
         constexpr uint32_t TRIP_PAIRS = 3;
@@ -1018,14 +1022,14 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
 #pragma unroll
             for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
                 if (alive) {
-                    if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; in_b = !fate_before_rk(fate); }
+                    if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; if (fate_before_rk(fate)) sb.n_rk = 0u; }
                 }
                 if (alive) {
-                    if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; in_b = fate_before_rk(fate); }
+                    if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; if (fate_before_rk(fate)) st.n_rk = 0u; }
                 }
             }
         }
-        if (in_b) st = sb;
+        if (sb.n_rk > st.n_rk) st = sb;
         steps = st.n_rk;
         if (alive) {
             // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
