@@ -396,9 +396,11 @@ constexpr float R2_GT1 = 0x1.000002p0f;
 
 __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
 
-template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN>
+// UNI: every active lane of the wave is at loop iteration `it` (n_rk == it: the ping-pong loop), so the
+// cap test is a wave-uniform (scalar) compare.
+template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
-                                        uint32_t& fate) {
+                                        uint32_t& fate, uint32_t it = 0u) {
     const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
     const v3 ro = in.ro, rd = in.rd;
     const float travelled = in.travelled, s = in.s;
@@ -470,7 +472,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     out.s = s;
     out.outside = not_out ? in.outside : 1u;                           // only read when bo_on
     const bool escape = ntr > a.max_dist;                              // :325-327
-    const bool capped = n_rk + 1u >= a.max_iters;                      // loop end (:266)
+    const bool capped = (UNI ? it : n_rk) + 1u >= a.max_iters;         // loop end (:266)
     if constexpr (BRANCHY) {
         out.ro = nro;
         out.rd = nrd;
@@ -637,15 +639,15 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
 
 // One iteration for one ray from `in` into `out` (step_bf<true> contract: `out` is not written for
 // fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
-template <uint32_t SF = SF_DYN>
+template <uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
-                                              uint32_t& fate) {
+                                              uint32_t& fate, uint32_t it = 0u) {
 #if BH_FAST
     FOps X;
-    return step_bf<true, FOps, SF>(a, f, in, out, X, fate);
+    return step_bf<true, FOps, SF, UNI>(a, f, in, out, X, fate, it);
 #else
     XOps<true> X;
-    bool done = step_bf<true, XOps<true>, SF>(a, f, in, out, X, fate);
+    bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it);
 #ifdef BH_DIAG_SLOW
     const uint64_t badm = __builtin_amdgcn_ballot_w64(X.bad);
     if (badm != 0ull && (threadIdx.x & 63u) == 0u) {
@@ -657,7 +659,7 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
     // ballot here costs a v_cndmask + v_cmp per step to materialise the mask)
     if (__builtin_expect(X.bad, 0)) {
         XOps<false> Y;
-        done = step_bf<true, XOps<false>, SF>(a, f, in, out, Y, fate);
+        done = step_bf<true, XOps<false>, SF, UNI>(a, f, in, out, Y, fate, it);
     }
     return done;
 #endif
@@ -1022,10 +1024,16 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
 #pragma unroll
             for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
                 if (alive) {
-                    if (march_step_io<SF>(a, f, st, sb, fate)) { alive = false; if (fate_before_rk(fate)) sb.n_rk = 0u; }
+                    if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j)) {
+                        alive = false;
+                        if (fate_before_rk(fate)) sb.n_rk = 0u;
+                    }
                 }
                 if (alive) {
-                    if (march_step_io<SF>(a, f, sb, st, fate)) { alive = false; if (fate_before_rk(fate)) st.n_rk = 0u; }
+                    if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u)) {
+                        alive = false;
+                        if (fate_before_rk(fate)) st.n_rk = 0u;
+                    }
                 }
             }
         }
