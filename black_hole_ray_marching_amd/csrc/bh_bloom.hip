@@ -18,6 +18,9 @@
 // coalesced 4-byte stores; the 256-entry decode table and the 257 encode thresholds in LDS.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include "bh_common.hpp"
 #include "bh_crmath.hpp"
 #include "bh_srgb.hpp"
@@ -157,6 +160,35 @@ struct Taps {
     __device__ __forceinline__ float dv_min() const { return dv(6); }
     __device__ __forceinline__ float dv_max() const { return dv(2); }
 };
+// The structured form of an 8-tap pass, proven by the host for every pixel of a launch
+// (bh_bloom_tap_plan): along each axis tap i's unclamped texel coordinate u*n - 0.5 equals x + o_i + f_i
+// exactly, with an integer offset o_i and a weight f_i of 0 (point) or 1/2 (half).  The bilinear sample
+// then reads texels clamp(x + o_i) and clamp(x + o_i + 1) at constant offsets, and its lerps reduce
+// exactly: with weights 1/2 (products by 1/2 exact for the decoded texels, which are 0 or >= 2^-12)
+//   (t0 * 0.5 + t1 * 0.5) == (t0 + t1) * 0.5,   both axes: ((t00 + t10) + (t01 + t11)) * 0.25,
+// and with weight 0 the lerp returns t0 (t * 1 + t' * 0 == t).  Clamping agrees at the edges: a
+// coordinate clamped to -1 or n has weight 0 and selects the edge texel, which both reads of a half
+// tap then clamp to (t + t) * 0.5 == t).
+struct TapPlan {
+    int32_t ox[8], oy[8];
+    uint32_t hx, hy;                 // bit i: tap i's weight along x (y) is 1/2, else 0
+    int32_t lo_x, hi_x, lo_y, hi_y;  // the footprint's offsets: min o_i, max (o_i + half_i)
+    uint32_t valid;
+};
+// A block's staged footprint for a TapPlan: tile[(y - y0) * FP + (x - x0)] holds the decoded texel
+// (clamp(x), clamp(y)) for the logical coordinates [x0, x0 + FP) x [y0, y0 + FP).
+template <int FP>
+struct PlanSrc {
+    CTex t;
+    const float4* tile;
+    int32_t x0, y0;
+    const TapPlan* P;
+    __device__ __forceinline__ F4 at(int32_t x, int32_t y) const {
+        const float4 v = tile[(y - y0) * FP + (x - x0)];
+        return {v.x, v.y, v.z, v.w};
+    }
+};
+
 // `point`: bit i set = tap i's weights are exactly 0 for every pixel of this launch
 template <class Src>
 __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float v, uint32_t point) {
@@ -173,6 +205,36 @@ __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float 
     }
     return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
 }
+// up8 over a TapPlan-staged footprint: the same sums, each tap 1, 2 or 4 LDS reads at constant offsets
+template <int FP>
+__device__ __forceinline__ F4 up8(const PlanSrc<FP>& src, const Taps&, float, float, uint32_t) {
+    const TapPlan& P = *src.P;
+    const uint32_t lx = blockIdx.x * 16u + (threadIdx.x & 15u), ly = blockIdx.y * 16u + (threadIdx.x >> 4);
+    const int32_t base = ((int32_t)ly - src.y0) * FP + ((int32_t)lx - src.x0);
+    F4 s{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float4* p = src.tile + (base + P.oy[i] * FP + P.ox[i]);
+        float4 q = p[0];
+        const bool hx = (P.hx >> i) & 1u, hy = (P.hy >> i) & 1u;
+        if (hx && hy) {
+            const float4 a = p[1], b = p[FP], c = p[FP + 1];
+            q = make_float4(((q.x + a.x) + (b.x + c.x)) * 0.25f, ((q.y + a.y) + (b.y + c.y)) * 0.25f,
+                            ((q.z + a.z) + (b.z + c.z)) * 0.25f, ((q.w + a.w) + (b.w + c.w)) * 0.25f);
+        } else if (hx || hy) {
+            const float4 a = p[hx ? 1 : FP];
+            q = make_float4((q.x + a.x) * 0.5f, (q.y + a.y) * 0.5f, (q.z + a.z) * 0.5f, (q.w + a.w) * 0.5f);
+        }
+        if (i == 0) {
+            s = {q.x, q.y, q.z, q.w};
+        } else {
+            const float w = (i & 1) ? 2.0f : 1.0f;
+            s.r = s.r + q.x * w; s.g = s.g + q.y * w; s.b = s.b + q.z * w; s.a = s.a + q.w * w;
+        }
+    }
+    return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
+}
+
 // remix.wgsl:22-24
 __device__ __forceinline__ F4 remix(F4 c0, F4 c1) {
     return {c0.r + c1.r * 0.5f, c0.g + c1.g * 0.5f, c0.b + c1.b * 0.5f, c0.a + c1.a * 0.5f};
@@ -196,8 +258,40 @@ __device__ __forceinline__ Span tap_span(uint32_t first, uint32_t last, const cr
 // else straight from global memory; both give identical values.  Called by every thread.
 template <int FP, class Body>
 __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, const Taps& k, uint32_t ow,
-                                            uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, Body body) {
+                                            uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, const TapPlan& P,
+                                            Body body) {
     const uint32_t bx = blockIdx.x * 16u, by = blockIdx.y * 16u;
+    if (P.valid && P.hi_x - P.lo_x + 16 <= FP && P.hi_y - P.lo_y + 16 <= FP) {  // launch-uniform
+        // the footprint with clamp-to-edge addressing: row r of the tile is texel row clamp(y0 + r);
+        // every load of this thread first, then the decodes
+        const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;
+        const int32_t nx = P.hi_x - P.lo_x + 16, ny = P.hi_y - P.lo_y + 16;
+        const int32_t tx = (int32_t)(threadIdx.x & 15u), ty = (int32_t)(threadIdx.x >> 4);
+        constexpr int R = (FP + 15) / 16;
+        const int32_t wm = (int32_t)t.w - 1, hm = (int32_t)t.h - 1;
+        uint32_t raw[R][R];
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < R; ++b) {
+                const int32_t ly = ty + 16 * a, lx = tx + 16 * b;
+                if (ly < ny && lx < nx)
+                    raw[a][b] = t.px[(size_t)clampi(y0 + ly, 0, hm) * t.w + clampi(x0 + lx, 0, wm)];
+            }
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < R; ++b) {
+                const int32_t ly = ty + 16 * a, lx = tx + 16 * b;
+                if (ly < ny && lx < nx) {
+                    const F4 d = dec(L, raw[a][b]);
+                    tile[ly * FP + lx] = make_float4(d.r, d.g, d.b, d.a);
+                }
+            }
+        __syncthreads();
+        body(PlanSrc<FP>{t, tile, x0, y0, &P});
+        return;
+    }
     const Span sx = tap_span(bx, min(bx + 15u, ow - 1u), Rw, k.du_min(), k.du_max(), t.w);
     const Span sy = tap_span(by, min(by + 15u, oh - 1u), Rh, k.dv_min(), k.dv_max(), t.h);
     if (sx.n <= FP && sy.n <= FP) {  // block-uniform
@@ -240,7 +334,8 @@ constexpr int FP_FINAL = 44;  // the last up pass at res / 4: taps within +-12 t
 
 // One render pass of the reference (literal schedule): 16x16 pixels per 256-thread block.
 template <uint32_t SH>
-__global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx, uint32_t ry, uint32_t point, Tex out) {
+__global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx, uint32_t ry, uint32_t point, TapPlan P,
+                                        Tex out) {
     __shared__ Lds L;
     __shared__ float4 tile[SH == SH_UP ? FP_UP * FP_UP : 1];
     load_tables(tb, L);
@@ -248,7 +343,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     if constexpr (SH == SH_UP) {
         const Taps k(rx, ry);
-        with_source<FP_UP>(a, L, tile, k, out.w, out.h, Rw, Rh, [&](const auto& src) {
+        with_source<FP_UP>(a, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
             if (x >= out.w || y >= out.h) return;
             out.px[(size_t)y * out.w + x] = enc(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         });
@@ -264,14 +359,14 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
 }
 
 // Fused stage 1 (same-size sampling exact): Y = X + 0.5 * q(blur1(X)), blur1 = up8(X, res (W, H)).
-__global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, Tex Y) {
+__global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, TapPlan P, Tex Y) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_Y * FP_Y];
     load_tables(tb, L);
     const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)Y.w), Rh = crm::rcp_refined((float)Y.h);
     const Taps k(X.w, X.h);
-    with_source<FP_Y>(X, L, tile, k, Y.w, Y.h, Rw, Rh, [&](const auto& src) {
+    with_source<FP_Y>(X, L, tile, k, Y.w, Y.h, Rw, Rh, P, [&](const auto& src) {
         if (x >= Y.w || y >= Y.h) return;
         const F4 b1 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         Y.px[(size_t)y * Y.w + x] = enc(L, remix(src.at((int32_t)x, (int32_t)y), b1));
@@ -280,14 +375,14 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
 
 // Fused last stage: out = col + 0.5 * q(Z), Z = Y + 0.5 * q(up8(U0, res (rx, ry))).
 __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTex U0, uint32_t rx,
-                                                   uint32_t ry, uint32_t point, Tex out) {
+                                                   uint32_t ry, uint32_t point, TapPlan P, Tex out) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_FINAL * FP_FINAL];
     load_tables(tb, L);
     const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
-    with_source<FP_FINAL>(U0, L, tile, k, out.w, out.h, Rw, Rh, [&](const auto& src) {
+    with_source<FP_FINAL>(U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
         if (x >= out.w || y >= out.h) return;
         const size_t i = (size_t)y * out.w + x;
         const F4 b3 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
@@ -321,6 +416,57 @@ bool axis_point(uint32_t on, uint32_t tn, float d) {
 }
 }  // namespace
 
+// One axis of tap i (offset d in texcoord units) over an on-pixel pass of an tn-texel texture: the
+// integer offset o and half flag f with u*tn - 0.5 == x + o + f/2 exactly for every x, else false.
+bool axis_plan(uint32_t on, uint32_t tn, float d, int32_t* o, bool* half) {
+    const float t0 = ((0.5f / (float)on) + d) * (float)tn - 0.5f;
+    const float f0 = floorf(t0);
+    if (!(t0 - f0 == 0.0f || t0 - f0 == 0.5f) || !(fabsf(f0) < 4096.0f)) return false;
+    *o = (int32_t)f0;
+    *half = t0 != f0;
+    const float fr = t0 - f0;
+    for (uint32_t x = 0; x < on; ++x) {
+        const float t = (((float)x + 0.5f) / (float)on + d) * (float)tn - 0.5f;
+        if (t != (float)((int32_t)x + *o) + fr) return false;
+    }
+    return true;
+}
+struct PlanKey { uint32_t ow, oh, tw, th, rx, ry; };
+// The TapPlan of an 8-tap pass (see TapPlan), cached per shape (a few per bloom chain).
+TapPlan tap_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry) {
+    static thread_local PlanKey keys[16];
+    static thread_local TapPlan plans[16];
+    static thread_local uint32_t n = 0, next = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (keys[i].ow == ow && keys[i].oh == oh && keys[i].tw == tw && keys[i].th == th && keys[i].rx == rx &&
+            keys[i].ry == ry)
+            return plans[i];
+    TapPlan P{};
+    P.valid = 1u;
+    P.lo_x = P.lo_y = 1 << 20;
+    P.hi_x = P.hi_y = -(1 << 20);
+    const float hx = 0.5f / (float)rx, hy = 0.5f / (float)ry;
+    for (int i = 0; i < 8 && P.valid; ++i) {
+        const float du = (hx * (float)((int)((0x12343210u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        const float dv = (hy * (float)((int)((0x10123432u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        bool fx, fy;
+        if (!axis_plan(ow, tw, du, &P.ox[i], &fx) || !axis_plan(oh, th, dv, &P.oy[i], &fy)) {
+            P.valid = 0u;
+            break;
+        }
+        P.hx |= (uint32_t)fx << i;
+        P.hy |= (uint32_t)fy << i;
+        P.lo_x = std::min(P.lo_x, P.ox[i]); P.hi_x = std::max(P.hi_x, P.ox[i] + (int32_t)fx);
+        P.lo_y = std::min(P.lo_y, P.oy[i]); P.hi_y = std::max(P.hi_y, P.oy[i] + (int32_t)fy);
+    }
+    if (!P.valid) P = TapPlan{};
+    keys[next] = {ow, oh, tw, th, rx, ry};
+    plans[next] = P;
+    next = (next + 1u) % 16u;
+    n = n < 16u ? n + 1u : 16u;
+    return P;
+}
+
 // bit i: tap i of kawase_upsample.wgsl samples texel centres exactly for every pixel of an
 // ow x oh pass over a tw x th texture with resolution uniform (rx, ry)
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(uint32_t ow, uint32_t oh, uint32_t tw,
@@ -344,12 +490,13 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     const Tables tb{lut, enc, buckets};
     const CTex A{a, aw, ah}, B{b ? b : a, aw, ah};
     const Tex O{out, ow, oh};
-    const uint32_t pm = shader == SH_UP ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
+    const TapPlan P = shader == SH_UP ? tap_plan(ow, oh, aw, ah, rx, ry) : TapPlan{};
+    const uint32_t pm = shader == SH_UP && !P.valid ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
     switch (shader) {
-        case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, O); break;
-        case SH_DOWN: hipLaunchKernelGGL(pass_kernel<SH_DOWN>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, O); break;
-        case SH_UP: hipLaunchKernelGGL(pass_kernel<SH_UP>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, O); break;
-        default: hipLaunchKernelGGL(pass_kernel<SH_REMIX>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, O); break;
+        case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
+        case SH_DOWN: hipLaunchKernelGGL(pass_kernel<SH_DOWN>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
+        case SH_UP: hipLaunchKernelGGL(pass_kernel<SH_UP>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
+        default: hipLaunchKernelGGL(pass_kernel<SH_REMIX>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
     }
     return (int)hipGetLastError();
 }
@@ -357,8 +504,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
                                                                       const uint8_t* buckets, const uint32_t* X, uint32_t* Y, uint32_t w,
                                                                       uint32_t h, hipStream_t s) {
-    const uint32_t pm = bh_bloom_point_mask(w, h, w, h, w, h);
-    hipLaunchKernelGGL(bloom_y_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{X, w, h}, pm, Tex{Y, w, h});
+    const TapPlan P = tap_plan(w, h, w, h, w, h);
+    const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, w, h);
+    hipLaunchKernelGGL(bloom_y_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{X, w, h}, pm, P,
+                       Tex{Y, w, h});
     return (int)hipGetLastError();
 }
 
@@ -367,8 +516,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
                                                                           const uint32_t* U0, uint32_t rx, uint32_t ry,
                                                                           uint32_t* out, uint32_t w, uint32_t h,
                                                                           hipStream_t s) {
-    const uint32_t pm = bh_bloom_point_mask(w, h, w, h, rx, ry);
+    const TapPlan P = tap_plan(w, h, w, h, rx, ry);
+    const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, rx, ry);
     hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{col, w, h},
-                       CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, Tex{out, w, h});
+                       CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
     return (int)hipGetLastError();
 }

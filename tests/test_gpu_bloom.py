@@ -37,10 +37,12 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
 
 @pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
 @pytest.mark.parametrize("H,W,levels", [(128, 256, 3), (64, 64, 1), (64, 128, 2), (120, 200, 3), (37, 53, 3),
-                                        (256, 512, 5)])
+                                        (256, 512, 5), (512, 1024, 4), (2048, 4096, 3)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     """AUTO fuses passes for sizes whose same-size sampling is exact (powers of two) and runs the
-    literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes."""
+    literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes.  Power-of-two
+    sizes also take the 8-tap passes' TapPlan form (constant-offset taps), up to the full
+    4096x2048 frame."""
     rng = np.random.default_rng(W * 7 + H + levels)
     col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
     scene = bh.Scene(16, 16, sky=sky_small)
