@@ -402,3 +402,36 @@ def test_prepared_frames_equal_render_frames(torch_cuda, sky_small):
     with pytest.raises(bh.BhError):
         batch.render(n=2, cameras=cams[:3])
     scene.close()
+
+
+def test_graph_capture_of_render_frames(torch_cuda, sky_small):
+    """bh_render_frames inside a HIP graph: after a first call of the (geometry, stream) key, a launch of
+    up to 32 frames (kernel-argument frames) captures and replays to the same bytes; a launch of more
+    (the device frame table, staged from a host ring) is refused on a capturing stream with a status
+    and launches nothing, so the capture stays valid."""
+    torch = torch_cuda
+    W, H = 64, 32
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=512, math=bh.BH_MATH_EXACT)
+    cams = [camera_uniform(c, W, H) for c in ("A", "B")]
+    mk = lambda: torch.full((H, W, 4), float("nan"), device="cuda")  # noqa: E731
+    outs = [mk() for _ in cams]
+    many = [mk() for _ in range(33)]
+    s = torch.cuda.Stream()
+    scene.render_frames(outs, None, cameras=cams, stream=s)  # allocates this stream's order state
+    torch.cuda.synchronize()
+    for o in outs:
+        o.fill_(float("nan"))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        with pytest.raises(bh.BhError):
+            scene.render_frames(many, None, stream=s)
+        scene.render_frames(outs, None, cameras=cams, stream=s)
+    g.replay()
+    torch.cuda.synchronize()
+    for o, cu in zip(outs, cams):
+        scene.camera_uniform = cu
+        ref = mk()
+        scene.render(ref, None)
+        torch.cuda.synchronize()
+        assert torch.equal(o.view(torch.int32), ref.view(torch.int32))
+    scene.close()
