@@ -57,6 +57,9 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=100)   # SURVEY §8d timing protocol: 100 timed frames
     # SURVEY §8d asks for 10 warm-up frames; 300 (0.25 s) let the clocks settle
     p.add_argument("--warmup", type=int, default=300)
+    p.add_argument("--settle-ms", type=float, default=100.0,
+                   help="untimed power-state settle before the warm-up: full launches of the workload for this "
+                        "many ms (the GPU clock ramps for ~30 ms under load after idle; DESIGN.md §6); 0 = none")
     p.add_argument("--workload", choices=["strong", "config4", "weak"], default="strong")
     p.add_argument("--config", type=int, choices=[1, 2, 3, 4, 5], default=0,
                    help="BASELINE.json configs[N-1]: 1 = 256x256 cap 64 no surfaces camera A, 2 = 1920x1080 cap 256 "
@@ -446,6 +449,18 @@ def main() -> int:
     def sizes(k):  # frames per launch covering k frames
         return [min(D, k - i) for i in range(0, k, D)]
 
+    # power-state settle (DESIGN.md §6 "Warm-up"): after an idle period the shader clock under this load
+    # starts at 1.77-1.95 GHz and reaches its sustained 2.17 GHz only after ~30 ms of work, so a short
+    # --warmup would time the power manager's ramp, not the kernel.  Full launches of the same workload
+    # (render only: nothing is exchanged, no frame index advances) until settle_ms of GPU-busy wall time
+    # has passed; reported in the line ("clock_settle").  Untimed, like the W warm-up steps after it.
+    settle_frames, t_settle = 0, time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        render(D)
+        torch.cuda.synchronize(dev)
+        settle_frames += D
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
+
     for nf in sizes(args.warmup):
         render(nf)
         exchange(nf)
@@ -533,6 +548,7 @@ def main() -> int:
             "n_gpus": n,
             "steps": args.steps,
             "warmup": args.warmup,
+            "clock_settle": {"ms": round(settle_ms, 1), "frames": settle_frames},
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
             "higher_is_better": True,
             "scaling": scaling,
