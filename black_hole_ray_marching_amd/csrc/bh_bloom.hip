@@ -19,7 +19,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 #include "bh_common.hpp"
 #include "bh_crmath.hpp"
@@ -391,6 +395,78 @@ __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTe
     });
 }
 
+// The 2:1 form of an 8-tap pass: an up pass from a texture of n texels to 2n pixels along each axis
+// (at 4096x2048 the full-size up pass from 2048x1024 and the one before it).  Its taps' texel
+// coordinates are t = (x >> 1) + o + f with an integer o and a weight f in [0, 1) that depend only on
+// the pixel's parity and the tap (the host proves it for every pixel: bh_bloom_up2_plan).  Where no tap
+// is clamped and both texels of every tap lie inside the texture (the interior: every block but the
+// outermost ring), the bilinear sample reads texels (x>>1) + o and + 1 with weights f, 1 - f -- the
+// general sampler's own arithmetic, without its texcoord, floor and clamp work.  The kernel gives each
+// wave of a block one parity class (wave w: x parity w & 1, y parity w >> 1; lane l: pixel (2 (l & 7),
+// 2 (l >> 3)) of the class), so a tap's offsets and weights are wave-uniform scalars.
+struct Up2Plan {
+    int32_t ox[2][8], oy[2][8];      // [pixel parity][tap]: floor(t) - (x >> 1)
+    float fx[2][8], fy[2][8];        // t - floor(t)
+    int32_t x_lo, x_hi, y_lo, y_hi;  // the interior's output pixels (inclusive; empty when lo > hi)
+    uint32_t valid;
+};
+
+template <int FP>
+__device__ __forceinline__ F4 up8_2(const TileSrc<FP>& src, const Up2Plan& P, uint32_t cx, uint32_t cy, uint32_t x,
+                                    uint32_t y) {
+    const int32_t base = ((int32_t)(y >> 1) - src.y0) * FP + ((int32_t)(x >> 1) - src.x0);
+    F4 s{0.0f, 0.0f, 0.0f, 0.0f};
+    // rolled: unrolled (even with a sched barrier per tap) the 8 taps' constant-offset LDS reads are
+    // hoisted together, 164 VGPRs (3 waves per SIMD); rolled 59, the plan read by scalar loads
+#pragma unroll 1
+    for (int i = 0; i < 8; i++) {
+        const int32_t ox = cx ? P.ox[1][i] : P.ox[0][i], oy = cy ? P.oy[1][i] : P.oy[0][i];
+        const float fa = cx ? P.fx[1][i] : P.fx[0][i], fb = cy ? P.fy[1][i] : P.fy[0][i];
+        const float4* p = src.tile + (base + oy * FP + ox);
+        const float4 t00 = p[0], t10 = p[1], t01 = p[FP], t11 = p[FP + 1];
+        const float ia = 1.0f - fa, ib = 1.0f - fb;
+        F4 q;  // sample(): the same operations in the same order
+        q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+        q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+        q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+        q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+        if (i == 0) {
+            s = q;
+        } else {
+            const float w = (i & 1) ? 2.0f : 1.0f;
+            s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
+        }
+    }
+    return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
+}
+
+// A 2:1 up pass (kawase_upsample.wgsl), 16x16 pixels per block in parity-class waves (see Up2Plan);
+// the outermost blocks take the general sampler over the same staged footprint.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_WPE))) up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P, Tex out) {
+    __shared__ Lds L;
+    __shared__ float4 tile[FP_UP * FP_UP];
+    load_tables(tb, L);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
+    const uint32_t cx = w & 1u, cy = w >> 1;
+    const uint32_t bx = blockIdx.x * 16u, by = blockIdx.y * 16u;
+    const uint32_t x = bx + 2u * (l & 7u) + cx, y = by + 2u * (l >> 3) + cy;
+    const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
+    const Taps k(rx, ry);
+    const bool inner = (int32_t)bx >= P.x_lo && (int32_t)bx + 15 <= P.x_hi && (int32_t)by >= P.y_lo &&
+                       (int32_t)by + 15 <= P.y_hi;  // block-uniform
+    with_source<FP_UP>(a, L, tile, k, out.w, out.h, Rw, Rh, TapPlan{}, [&](const auto& src) {
+        if (x >= out.w || y >= out.h) return;
+        F4 r;
+        if constexpr (std::is_same_v<std::decay_t<decltype(src)>, TileSrc<FP_UP>>) {
+            if (inner) r = up8_2(src, P, cx, cy, x, y);
+            else r = up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point);
+        } else {
+            r = up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point);
+        }
+        out.px[(size_t)y * out.w + x] = enc(L, r);
+    });
+}
+
 }  // namespace bloom
 }  // namespace bh
 
@@ -467,6 +543,79 @@ TapPlan tap_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx
     return P;
 }
 
+// One axis of tap i (offset d in texcoord units) of a 2:1 pass (on == 2 tn): per pixel parity p the
+// integer o[p] and weight f[p] with floor(t) == (x >> 1) + o[p] and t - floor(t) == f[p] for every x,
+// t = u*tn - 0.5 the sampler's unclamped coordinate; [lo, hi] = the pixels whose two texels floor(t),
+// floor(t) + 1 both lie in [0, tn) (there the sampler's clamps change nothing).  False if not so.
+bool axis_plan2(uint32_t on, uint32_t tn, float d, int32_t o[2], float f[2], int32_t* lo, int32_t* hi) {
+    if (on != 2u * tn || tn < 2u) return false;
+    bool seen[2] = {false, false};
+    int32_t ilo = INT_MAX, ihi = -1, count = 0;
+    for (uint32_t x = 0; x < on; ++x) {
+        const float t = (((float)x + 0.5f) / (float)on + d) * (float)tn - 0.5f;
+        const float fl = floorf(t);
+        if (!(fabsf(fl) < 16777216.0f)) return false;
+        const uint32_t p = x & 1u;
+        const int32_t oo = (int32_t)fl - (int32_t)(x >> 1);
+        const float ff = t - fl;
+        if (!seen[p]) {
+            o[p] = oo;
+            f[p] = ff;
+            seen[p] = true;
+        } else if (oo != o[p] || std::memcmp(&ff, &f[p], sizeof ff) != 0) {
+            return false;
+        }
+        if (fl >= 0.0f && fl + 1.0f <= (float)tn - 1.0f) {
+            ilo = std::min(ilo, (int32_t)x);
+            ihi = std::max(ihi, (int32_t)x);
+            ++count;
+        }
+    }
+    if (count != 0 && count != ihi - ilo + 1) return false;  // t is monotone: an interval
+    *lo = count ? ilo : 0;
+    *hi = count ? ihi : -1;
+    return true;
+}
+// The Up2Plan of an up pass (see Up2Plan), cached per shape; valid == 0 when the pass is not 2:1 or a
+// tap's offset or weight varies within a parity class.
+Up2Plan up2_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry) {
+    static thread_local PlanKey keys[16];
+    static thread_local Up2Plan plans[16];
+    static thread_local uint32_t n = 0, next = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        if (keys[i].ow == ow && keys[i].oh == oh && keys[i].tw == tw && keys[i].th == th && keys[i].rx == rx &&
+            keys[i].ry == ry)
+            return plans[i];
+    Up2Plan P{};
+    P.valid = 1u;
+    P.x_lo = P.y_lo = 0;
+    P.x_hi = (int32_t)ow - 1;
+    P.y_hi = (int32_t)oh - 1;
+    const float hx = 0.5f / (float)rx, hy = 0.5f / (float)ry;
+    for (int i = 0; i < 8; ++i) {
+        const float du = (hx * (float)((int)((0x12343210u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        const float dv = (hy * (float)((int)((0x10123432u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        int32_t ox[2], oy[2], xl, xh, yl, yh;
+        float fx[2], fy[2];
+        if (!axis_plan2(ow, tw, du, ox, fx, &xl, &xh) || !axis_plan2(oh, th, dv, oy, fy, &yl, &yh)) {
+            P.valid = 0u;
+            break;
+        }
+        for (int p = 0; p < 2; ++p) {
+            P.ox[p][i] = ox[p]; P.fx[p][i] = fx[p];
+            P.oy[p][i] = oy[p]; P.fy[p][i] = fy[p];
+        }
+        P.x_lo = std::max(P.x_lo, xl); P.x_hi = std::min(P.x_hi, xh);
+        P.y_lo = std::max(P.y_lo, yl); P.y_hi = std::min(P.y_hi, yh);
+    }
+    if (!P.valid) P = Up2Plan{};
+    keys[next] = {ow, oh, tw, th, rx, ry};
+    plans[next] = P;
+    next = (next + 1u) % 16u;
+    n = n < 16u ? n + 1u : 16u;
+    return P;
+}
+
 // bit i: tap i of kawase_upsample.wgsl samples texel centres exactly for every pixel of an
 // ow x oh pass over a tw x th texture with resolution uniform (rx, ry)
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(uint32_t ow, uint32_t oh, uint32_t tw,
@@ -492,6 +641,14 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     const Tex O{out, ow, oh};
     const TapPlan P = shader == SH_UP ? tap_plan(ow, oh, aw, ah, rx, ry) : TapPlan{};
     const uint32_t pm = shader == SH_UP && !P.valid ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
+    static const bool no_up2 = std::getenv("BH_BLOOM_NO_UP2") != nullptr;  // A/B: the general up pass
+    if (shader == SH_UP && !P.valid && !no_up2) {
+        const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
+        if (Q.valid) {
+            hipLaunchKernelGGL(up2_kernel, grid_for(ow, oh), dim3(256), 0, s, tb, A, rx, ry, pm, Q, O);
+            return (int)hipGetLastError();
+        }
+    }
     switch (shader) {
         case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
         case SH_DOWN: hipLaunchKernelGGL(pass_kernel<SH_DOWN>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
