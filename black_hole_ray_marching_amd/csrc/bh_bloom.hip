@@ -179,16 +179,27 @@ struct TapPlan {
     int32_t lo_x, hi_x, lo_y, hi_y;  // the footprint's offsets: min o_i, max (o_i + half_i)
     uint32_t valid;
 };
-// A block's staged footprint for a TapPlan: tile[(y - y0) * FP + (x - x0)] holds the decoded texel
-// (clamp(x), clamp(y)) for the logical coordinates [x0, x0 + FP) x [y0, y0 + FP).
-template <int FP>
+// A block's staged footprint for a TapPlan: entry (y - y0) * FP + (x - x0) of the tile holds texel
+// (clamp(x), clamp(y)) for the logical coordinates [x0, x0 + FP) x [y0, y0 + FP): decoded (float4), or
+// with RAW the BGRA8 word (4 B instead of 16: the final pass's 44 x 44 footprint then takes 7.6 KiB of
+// LDS instead of 30 KiB, so twice as many blocks fit a CU), decoded when a tap reads it.
+template <int FP, bool RAW = false>
 struct PlanSrc {
     CTex t;
-    const float4* tile;
+    const void* tile;
     int32_t x0, y0;
     const TapPlan* P;
+    const Lds* L;
+    __device__ __forceinline__ float4 fetch(int32_t i) const {
+        if constexpr (RAW) {
+            const F4 d = dec(*L, static_cast<const uint32_t*>(tile)[i]);
+            return make_float4(d.r, d.g, d.b, d.a);
+        } else {
+            return static_cast<const float4*>(tile)[i];
+        }
+    }
     __device__ __forceinline__ F4 at(int32_t x, int32_t y) const {
-        const float4 v = tile[(y - y0) * FP + (x - x0)];
+        const float4 v = fetch((y - y0) * FP + (x - x0));
         return {v.x, v.y, v.z, v.w};
     }
 };
@@ -210,23 +221,23 @@ __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float 
     return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
 }
 // up8 over a TapPlan-staged footprint: the same sums, each tap 1, 2 or 4 LDS reads at constant offsets
-template <int FP>
-__device__ __forceinline__ F4 up8(const PlanSrc<FP>& src, const Taps&, float, float, uint32_t) {
+template <int FP, bool RAW>
+__device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW>& src, const Taps&, float, float, uint32_t) {
     const TapPlan& P = *src.P;
     const uint32_t lx = blockIdx.x * 16u + (threadIdx.x & 15u), ly = blockIdx.y * 16u + (threadIdx.x >> 4);
     const int32_t base = ((int32_t)ly - src.y0) * FP + ((int32_t)lx - src.x0);
     F4 s{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        const float4* p = src.tile + (base + P.oy[i] * FP + P.ox[i]);
-        float4 q = p[0];
+        const int32_t o = base + P.oy[i] * FP + P.ox[i];
+        float4 q = src.fetch(o);
         const bool hx = (P.hx >> i) & 1u, hy = (P.hy >> i) & 1u;
         if (hx && hy) {
-            const float4 a = p[1], b = p[FP], c = p[FP + 1];
+            const float4 a = src.fetch(o + 1), b = src.fetch(o + FP), c = src.fetch(o + FP + 1);
             q = make_float4(((q.x + a.x) + (b.x + c.x)) * 0.25f, ((q.y + a.y) + (b.y + c.y)) * 0.25f,
                             ((q.z + a.z) + (b.z + c.z)) * 0.25f, ((q.w + a.w) + (b.w + c.w)) * 0.25f);
         } else if (hx || hy) {
-            const float4 a = p[hx ? 1 : FP];
+            const float4 a = src.fetch(o + (hx ? 1 : FP));
             q = make_float4((q.x + a.x) * 0.5f, (q.y + a.y) * 0.5f, (q.z + a.z) * 0.5f, (q.w + a.w) * 0.5f);
         }
         if (i == 0) {
@@ -259,8 +270,10 @@ __device__ __forceinline__ Span tap_span(uint32_t first, uint32_t last, const cr
 }
 
 // Run `body(src)` with the block's input footprint staged in LDS (decoded) when it fits FP x FP,
-// else straight from global memory; both give identical values.  Called by every thread.
-template <int FP, class Body>
+// else straight from global memory; both give identical values.  Called by every thread.  RAW: a
+// TapPlan footprint is staged as BGRA8 words (PlanSrc<FP, true>; `tile` then needs FP*FP*4 bytes,
+// else FP*FP*16).
+template <int FP, bool RAW = false, class Body>
 __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, const Taps& k, uint32_t ow,
                                             uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, const TapPlan& P,
                                             Body body) {
@@ -288,12 +301,16 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
             for (int b = 0; b < R; ++b) {
                 const int32_t ly = ty + 16 * a, lx = tx + 16 * b;
                 if (ly < ny && lx < nx) {
-                    const F4 d = dec(L, raw[a][b]);
-                    tile[ly * FP + lx] = make_float4(d.r, d.g, d.b, d.a);
+                    if constexpr (RAW) {
+                        reinterpret_cast<uint32_t*>(tile)[ly * FP + lx] = raw[a][b];
+                    } else {
+                        const F4 d = dec(L, raw[a][b]);
+                        tile[ly * FP + lx] = make_float4(d.r, d.g, d.b, d.a);
+                    }
                 }
             }
         __syncthreads();
-        body(PlanSrc<FP>{t, tile, x0, y0, &P});
+        body(PlanSrc<FP, RAW>{t, tile, x0, y0, &P, &L});
         return;
     }
     const Span sx = tap_span(bx, min(bx + 15u, ow - 1u), Rw, k.du_min(), k.du_max(), t.w);
@@ -381,12 +398,14 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
 __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTex U0, uint32_t rx,
                                                    uint32_t ry, uint32_t point, TapPlan P, Tex out) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_FINAL * FP_FINAL];
+    // dynamic: FP_FINAL^2 BGRA8 words for the TapPlan form (7.6 KiB: ~2x the resident blocks of the
+    // decoded form, for a pass that mostly waits on its staging loads), else FP_FINAL^2 float4
+    extern __shared__ float4 tile[];
     load_tables(tb, L);
     const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
-    with_source<FP_FINAL>(U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
+    with_source<FP_FINAL, true>(U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
         if (x >= out.w || y >= out.h) return;
         const size_t i = (size_t)y * out.w + x;
         const F4 b3 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
@@ -675,7 +694,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
                                                                           hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, rx, ry);
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, rx, ry);
-    hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{col, w, h},
+    // the kernel's with_source takes the TapPlan form exactly when this holds (raw words staged)
+    const bool plan = P.valid && P.hi_x - P.lo_x + 16 <= FP_FINAL && P.hi_y - P.lo_y + 16 <= FP_FINAL;
+    const size_t lds = (size_t)FP_FINAL * FP_FINAL * (plan ? sizeof(uint32_t) : sizeof(float4));
+    hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets}, CTex{col, w, h},
                        CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
     return (int)hipGetLastError();
 }
