@@ -417,12 +417,12 @@ __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTe
 // The 2:1 form of an 8-tap pass: an up pass from a texture of n texels to 2n pixels along each axis
 // (at 4096x2048 the full-size up pass from 2048x1024 and the one before it).  Its taps' texel
 // coordinates are t = (x >> 1) + o + f with an integer o and a weight f in [0, 1) that depend only on
-// the pixel's parity and the tap (the host proves it for every pixel: bh_bloom_up2_plan).  Where no tap
-// is clamped and both texels of every tap lie inside the texture (the interior: every block but the
-// outermost ring), the bilinear sample reads texels (x>>1) + o and + 1 with weights f, 1 - f -- the
-// general sampler's own arithmetic, without its texcoord, floor and clamp work.  The kernel gives each
-// wave of a block one parity class (wave w: x parity w & 1, y parity w >> 1; lane l: pixel (2 (l & 7),
-// 2 (l >> 3)) of the class), so a tap's offsets and weights are wave-uniform scalars.
+// the pixel's parity and the tap (the host proves it for every pixel: up2_plan), and o of an odd
+// pixel is o of an even one or one more.  Where no tap is clamped and both texels of every tap lie
+// inside the texture (the interior: every block but the outermost ring), the bilinear sample reads
+// texels (x>>1) + o and + 1 with weights f, 1 - f -- the general sampler's own arithmetic, without its
+// texcoord, floor and clamp work.  One lane computes a 2x2 pixel quad: per tap the four pixels' texels
+// lie in a 3x3 (2x2 when both parities share o) neighbourhood of (x>>1, y>>1), read once for all four.
 struct Up2Plan {
     int32_t ox[2][8], oy[2][8];      // [pixel parity][tap]: floor(t) - (x >> 1)
     float fx[2][8], fy[2][8];        // t - floor(t)
@@ -430,60 +430,118 @@ struct Up2Plan {
     uint32_t valid;
 };
 
-template <int FP>
-__device__ __forceinline__ F4 up8_2(const TileSrc<FP>& src, const Up2Plan& P, uint32_t cx, uint32_t cy, uint32_t x,
-                                    uint32_t y) {
-    const int32_t base = ((int32_t)(y >> 1) - src.y0) * FP + ((int32_t)(x >> 1) - src.x0);
-    F4 s{0.0f, 0.0f, 0.0f, 0.0f};
-    // rolled: unrolled (even with a sched barrier per tap) the 8 taps' constant-offset LDS reads are
-    // hoisted together, 164 VGPRs (3 waves per SIMD); rolled 59, the plan read by scalar loads
-#pragma unroll 1
-    for (int i = 0; i < 8; i++) {
-        const int32_t ox = cx ? P.ox[1][i] : P.ox[0][i], oy = cy ? P.oy[1][i] : P.oy[0][i];
-        const float fa = cx ? P.fx[1][i] : P.fx[0][i], fb = cy ? P.fy[1][i] : P.fy[0][i];
-        const float4* p = src.tile + (base + oy * FP + ox);
-        const float4 t00 = p[0], t10 = p[1], t01 = p[FP], t11 = p[FP + 1];
-        const float ia = 1.0f - fa, ib = 1.0f - fb;
-        F4 q;  // sample(): the same operations in the same order
-        q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
-        q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
-        q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
-        q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
-        if (i == 0) {
-            s = q;
-        } else {
-            const float w = (i & 1) ? 2.0f : 1.0f;
-            s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
-        }
+// bilinear of texels (t00, t10, t01, t11) with weights (fa, fb): sample()'s operations in its order
+__device__ __forceinline__ F4 lerp2(const float4& t00, const float4& t10, const float4& t01, const float4& t11, float fa,
+                                    float fb) {
+    const float ia = 1.0f - fa, ib = 1.0f - fb;
+    F4 q;
+    q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+    q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+    q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+    q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+    return q;
+}
+__device__ __forceinline__ void acc(F4& s, const F4& q, int i) {
+    if (i == 0) {
+        s = q;
+    } else {
+        const float w = (i & 1) ? 2.0f : 1.0f;  // up8's sums, tap by tap
+        s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
     }
-    return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
+}
+// One tap for the quad: DX / DY = o(odd) - o(even) along x / y; T = the (2 + DY) x (2 + DX) texels from
+// (x>>1) + o(even), row stride FP.  s[b][a]: the pixel of y parity b, x parity a.
+template <int FP, int DX, int DY>
+__device__ __forceinline__ void quad_tap(const float4* T, const Up2Plan& P, int i, F4 (&s)[2][2]) {
+    float4 t[2 + DY][2 + DX];
+#pragma unroll
+    for (int r = 0; r < 2 + DY; ++r)
+#pragma unroll
+        for (int c = 0; c < 2 + DX; ++c) t[r][c] = T[r * FP + c];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int c = a ? DX : 0, r = b ? DY : 0;
+            acc(s[b][a], lerp2(t[r][c], t[r][c + 1], t[r + 1][c], t[r + 1][c + 1], P.fx[a][i], P.fy[b][i]), i);
+        }
 }
 
-// A 2:1 up pass (kawase_upsample.wgsl), 16x16 pixels per block in parity-class waves (see Up2Plan);
-// the outermost blocks take the general sampler over the same staged footprint.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_WPE))) up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P, Tex out) {
+// A 2:1 up pass (kawase_upsample.wgsl): 32x32 pixels per 256-thread block, one 2x2 quad per lane; the
+// outermost blocks (and footprints over FP) take the general sampler per pixel.
+constexpr int FP_UPQ = 28;  // footprint of 16 texels + the taps' reach (24 at 4096x2048)
+__global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P,
+                                        Tex out) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_UP * FP_UP];
+    __shared__ float4 tile[FP_UPQ * FP_UPQ];
     load_tables(tb, L);
-    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l = threadIdx.x & 63u;
-    const uint32_t cx = w & 1u, cy = w >> 1;
-    const uint32_t bx = blockIdx.x * 16u, by = blockIdx.y * 16u;
-    const uint32_t x = bx + 2u * (l & 7u) + cx, y = by + 2u * (l >> 3) + cy;
+    const uint32_t bx = blockIdx.x * 32u, by = blockIdx.y * 32u;
+    const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
-    const bool inner = (int32_t)bx >= P.x_lo && (int32_t)bx + 15 <= P.x_hi && (int32_t)by >= P.y_lo &&
-                       (int32_t)by + 15 <= P.y_hi;  // block-uniform
-    with_source<FP_UP>(a, L, tile, k, out.w, out.h, Rw, Rh, TapPlan{}, [&](const auto& src) {
-        if (x >= out.w || y >= out.h) return;
-        F4 r;
-        if constexpr (std::is_same_v<std::decay_t<decltype(src)>, TileSrc<FP_UP>>) {
-            if (inner) r = up8_2(src, P, cx, cy, x, y);
-            else r = up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point);
-        } else {
-            r = up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point);
+    const Span sx = tap_span(bx, min(bx + 31u, out.w - 1u), Rw, k.du_min(), k.du_max(), a.w);
+    const Span sy = tap_span(by, min(by + 31u, out.h - 1u), Rh, k.dv_min(), k.dv_max(), a.h);
+    const bool staged = sx.n <= FP_UPQ && sy.n <= FP_UPQ;  // block-uniform
+    if (staged) {
+        // every load of this thread first, then the decodes (as with_source)
+        constexpr int R = (FP_UPQ * FP_UPQ + 255) / 256;
+        uint32_t raw[R];
+        const int32_t n = sx.n * sy.n;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                raw[r] = a.px[(size_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
+            }
         }
-        out.px[(size_t)y * out.w + x] = enc(L, r);
-    });
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FP_UPQ + lx] = make_float4(d.r, d.g, d.b, d.a);
+            }
+        }
+        __syncthreads();
+    }
+    if (x >= out.w || y >= out.h) return;  // out.w, out.h are even (2n): the whole quad is outside
+    const bool inner = staged && (int32_t)bx >= P.x_lo && (int32_t)bx + 31 <= P.x_hi && (int32_t)by >= P.y_lo &&
+                       (int32_t)by + 31 <= P.y_hi;  // block-uniform
+    if (!inner) {
+        // the general sampler per pixel (rolled: four unrolled 8-tap samples need 120 VGPRs)
+#pragma unroll 1
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t px = x + (j & 1), py = y + (j >> 1);
+            const float u = texcoord(px, Rw), v = texcoord(py, Rh);
+            const F4 r = staged ? up8(TileSrc<FP_UPQ>{a, tile, sx.lo, sy.lo}, k, u, v, point)
+                                : up8(GlobalSrc{a, &L}, k, u, v, point);
+            out.px[(size_t)py * out.w + px] = enc(L, r);
+        }
+        return;
+    }
+    F4 s[2][2];
+    const int32_t base = ((int32_t)(y >> 1) - sy.lo) * FP_UPQ + ((int32_t)(x >> 1) - sx.lo);
+    // rolled (the plan read by scalar loads; unrolled, the taps' LDS reads are hoisted together)
+#pragma unroll 1
+    for (int i = 0; i < 8; i++) {
+        const float4* T = tile + (base + P.oy[0][i] * FP_UPQ + P.ox[0][i]);
+        const uint32_t d = (uint32_t)(P.ox[1][i] - P.ox[0][i]) | (uint32_t)(P.oy[1][i] - P.oy[0][i]) << 1;
+        switch (d) {  // wave-uniform
+            case 0: quad_tap<FP_UPQ, 0, 0>(T, P, i, s); break;
+            case 1: quad_tap<FP_UPQ, 1, 0>(T, P, i, s); break;
+            case 2: quad_tap<FP_UPQ, 0, 1>(T, P, i, s); break;
+            default: quad_tap<FP_UPQ, 1, 1>(T, P, i, s); break;
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        uint2 w;
+        w.x = enc(L, {div12(s[b][0].r), div12(s[b][0].g), div12(s[b][0].b), div12(s[b][0].a)});
+        w.y = enc(L, {div12(s[b][1].r), div12(s[b][1].g), div12(s[b][1].b), div12(s[b][1].a)});
+        *reinterpret_cast<uint2*>(out.px + (size_t)(y + b) * out.w + x) = w;  // x even: 8-byte aligned
+    }
 }
 
 }  // namespace bloom
@@ -624,6 +682,10 @@ Up2Plan up2_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx
             P.ox[p][i] = ox[p]; P.fx[p][i] = fx[p];
             P.oy[p][i] = oy[p]; P.fy[p][i] = fy[p];
         }
+        if (ox[1] - ox[0] < 0 || ox[1] - ox[0] > 1 || oy[1] - oy[0] < 0 || oy[1] - oy[0] > 1) {  // the quad's 3x3
+            P.valid = 0u;
+            break;
+        }
         P.x_lo = std::max(P.x_lo, xl); P.x_hi = std::min(P.x_hi, xh);
         P.y_lo = std::max(P.y_lo, yl); P.y_hi = std::min(P.y_hi, yh);
     }
@@ -664,7 +726,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     if (shader == SH_UP && !P.valid && !no_up2) {
         const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
         if (Q.valid) {
-            hipLaunchKernelGGL(up2_kernel, grid_for(ow, oh), dim3(256), 0, s, tb, A, rx, ry, pm, Q, O);
+            hipLaunchKernelGGL(up2_kernel, dim3((ow + 31u) / 32u, (oh + 31u) / 32u), dim3(256), 0, s, tb, A, rx, ry, pm, Q, O);
             return (int)hipGetLastError();
         }
     }

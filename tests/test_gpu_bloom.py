@@ -37,12 +37,15 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
 
 @pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
 @pytest.mark.parametrize("H,W,levels", [(128, 256, 3), (64, 64, 1), (64, 128, 2), (120, 200, 3), (37, 53, 3),
-                                        (256, 512, 5), (512, 1024, 4), (2048, 4096, 3)])
+                                        (256, 512, 5), (512, 1024, 4), (2048, 4096, 3),
+                                        # 2:1 up form (Up2Plan) on thin / narrow power-of-two frames: the
+                                        # general sampler's outer ring covers whole axes at the small levels
+                                        (32, 2048, 3), (1024, 64, 4), (8, 1024, 2), (64, 16, 3)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     """AUTO fuses passes for sizes whose same-size sampling is exact (powers of two) and runs the
     literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes.  Power-of-two
-    sizes also take the 8-tap passes' TapPlan form (constant-offset taps), up to the full
-    4096x2048 frame."""
+    sizes also take the 8-tap passes' TapPlan form (constant-offset taps) and the 2:1 up passes'
+    Up2Plan form (per-parity offsets and weights), up to the full 4096x2048 frame."""
     rng = np.random.default_rng(W * 7 + H + levels)
     col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
     scene = bh.Scene(16, 16, sky=sky_small)
