@@ -792,16 +792,18 @@ __device__ __forceinline__ void store_px(void* base, size_t idx, v3 c, const flo
 }
 
 // LDS tables of a workgroup: [0, 256) the sRGB decode of sky texels, then for BGRA8 output the
-// encoder's 257 thresholds.  Needs blockDim.x >= 256.
+// encoder's 257 thresholds.  NT = the workgroup's threads (a divisor or multiple of 256).
 template <uint32_t FMT>
 constexpr int lds_tables() { return FMT == BH_OUT_BGRA8_SRGB ? 256 + SRGB_TABLE : 256; }
-template <uint32_t FMT>
+template <uint32_t FMT, uint32_t NT = 256>
 __device__ __forceinline__ void load_tables(const MarchArgs& a, float* tab) {
-    tab[threadIdx.x] = a.srgb_lut[threadIdx.x];
-    if constexpr (FMT == BH_OUT_BGRA8_SRGB) {
-        tab[256 + threadIdx.x] = a.srgb_enc[threadIdx.x];
-        if (threadIdx.x == 0) tab[256 + 256] = a.srgb_enc[256];
+#pragma unroll
+    for (uint32_t i = threadIdx.x; i < 256u; i += NT) {
+        tab[i] = a.srgb_lut[i];
+        if constexpr (FMT == BH_OUT_BGRA8_SRGB) tab[256 + i] = a.srgb_enc[i];
     }
+    if constexpr (FMT == BH_OUT_BGRA8_SRGB)
+        if (threadIdx.x == 0) tab[256 + 256] = a.srgb_enc[256];
 }
 
 // BH_LAYOUT_TILES_RGB(M) store: pixel idx = tile * 64 + lane goes to three channel planes of its tile
@@ -873,6 +875,15 @@ __device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint
 // +34 % of kernel time at cap 512 vs cap 64 without it) and the tile schedule starts checking for
 // cycles (march_cycles).
 constexpr uint32_t PRIO_ITERS = 48;
+
+// Waves per workgroup of the tile schedule.  One: a workgroup's LDS (1 KiB decode table + 4 KiB
+// cycle history) is released when its one wave ends, and a new wave needs no three other free
+// slots on the CU; no workgroup barrier beyond the wave's own table load.  1 vs 4 waves (interleaved
+// A/B, profiles/r02d/ab_wg/): headline -0.6 %, 1920x1080 -0.8 %, cap 1000 -1.0 %, one frame per
+// launch -1.4 %, 256x256 cap 64 +0.6 % (noise level).  32 such workgroups per CU fill its 160 KiB.
+#ifndef BH_WG_WAVES
+#define BH_WG_WAVES 1u
+#endif
 
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
 // Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
@@ -1044,7 +1055,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
             // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
             // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
             __builtin_amdgcn_s_setprio(2);
-            __shared__ HistLds hist[4];  // 16 KiB per workgroup: 8 workgroups per CU still fit
+            __shared__ HistLds hist[BH_WG_WAVES];  // 4 KiB per wave: 8 waves per SIMD still fit (5 KiB x 32)
             fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
         }
     }
@@ -1071,13 +1082,13 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     }
 }
 
-// One wave per dispatch slot (the grid covers every slot).
+// One wave per dispatch slot (the grid covers every slot), BH_WG_WAVES waves per workgroup.
 template <uint32_t FMT, uint32_t SF>
-__global__ void __launch_bounds__(256) march_tile_kernel(MarchArgs A) {
+__global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs A) {
     __shared__ float lut[lds_tables<FMT>()];
-    load_tables<FMT>(A, lut);
+    load_tables<FMT, 64u * BH_WG_WAVES>(A, lut);
     __syncthreads();
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
     if (slot >= A.n_tiles * A.n_frames) return;  // wave-uniform
     march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
 }
@@ -1265,8 +1276,8 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
 // atomic on one word is serialised across the 8 XCDs at ~85 M claims/s)
 template <uint32_t FMT, uint32_t SF>
 inline void launch_tile_schedule(const MarchArgs& a, hipStream_t s) {
-    const uint32_t blocks = (a.n_tiles * a.n_frames + 3u) / 4u;
-    hipLaunchKernelGGL((march_tile_kernel<FMT, SF>), dim3(blocks), dim3(256), 0, s, a);
+    const uint32_t blocks = (a.n_tiles * a.n_frames + (BH_WG_WAVES - 1u)) / BH_WG_WAVES;
+    hipLaunchKernelGGL((march_tile_kernel<FMT, SF>), dim3(blocks), dim3(64u * BH_WG_WAVES), 0, s, a);
 }
 
 }  // namespace BH_NS
