@@ -14,8 +14,9 @@
 //     second loop iteration recomputes the same Y from the same input), two 2:1 downsamples, two
 //     upsamples at 1/2 and full size, and out = col + 0.5 (Y + 0.5 up(U0)) (one pass).  Each fused
 //     stage still quantises through the sRGB encode exactly where the reference stores a texture.
-// HBM-bound byte work: one lane per output pixel, 4-byte texel gathers (L2-resident neighbourhoods),
-// coalesced 4-byte stores; the 256-entry decode table and the 257 encode thresholds in LDS.
+// Byte work bound by the exact filter arithmetic and its LDS reads, not by HBM: one lane per output
+// pixel (a 2x2 quad in the 2:1 up passes), each block's input footprint decoded into LDS once,
+// coalesced stores; the 256-entry decode table and the 257 encode thresholds in LDS.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
