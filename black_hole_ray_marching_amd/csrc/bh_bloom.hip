@@ -251,6 +251,15 @@ __device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW>& src, const Taps&, floa
     return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
 }
 
+__device__ __forceinline__ void acc(F4& s, const F4& q, int i) {
+    if (i == 0) {
+        s = q;
+    } else {
+        const float w = (i & 1) ? 2.0f : 1.0f;  // up8's sums, tap by tap
+        s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
+    }
+}
+
 // remix.wgsl:22-24
 __device__ __forceinline__ F4 remix(F4 c0, F4 c1) {
     return {c0.r + c1.r * 0.5f, c0.g + c1.g * 0.5f, c0.b + c1.b * 0.5f, c0.a + c1.a * 0.5f};
@@ -395,6 +404,94 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
     });
 }
 
+// Y in the TapPlan form with one 2x2 pixel quad per lane (32x32 pixels per block): per tap the quad's
+// texels lie in a (2 + hx) x (2 + hy) neighbourhood at the plan's constant offset, read once for the
+// four pixels (14 LDS reads per pixel instead of 21 at 4096x2048), each pixel reduced exactly as
+// up8(PlanSrc) does.  HX / HY: the tap's half flags.
+constexpr int FP_YQ = 40;  // 32 + the taps' reach (38 at 4096x2048)
+template <int HX, int HY>
+__device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2]) {
+    float4 t[2 + HY][2 + HX];
+#pragma unroll
+    for (int r = 0; r < 2 + HY; ++r)
+#pragma unroll
+        for (int c = 0; c < 2 + HX; ++c) t[r][c] = T[r * FP_YQ + c];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            float4 q = t[b][a];
+            if constexpr (HX && HY) {
+                const float4 u = t[b][a + 1], v = t[b + 1][a], w = t[b + 1][a + 1];
+                q = make_float4(((q.x + u.x) + (v.x + w.x)) * 0.25f, ((q.y + u.y) + (v.y + w.y)) * 0.25f,
+                                ((q.z + u.z) + (v.z + w.z)) * 0.25f, ((q.w + u.w) + (v.w + w.w)) * 0.25f);
+            } else if constexpr (HX || HY) {
+                const float4 u = HX ? t[b][a + 1] : t[b + 1][a];
+                q = make_float4((q.x + u.x) * 0.5f, (q.y + u.y) * 0.5f, (q.z + u.z) * 0.5f, (q.w + u.w) * 0.5f);
+            }
+            acc(s[b][a], {q.x, q.y, q.z, q.w}, i);
+        }
+}
+__global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y) {
+    __shared__ Lds L;
+    __shared__ float4 tile[FP_YQ * FP_YQ];
+    load_tables(tb, L);
+    const uint32_t bx = blockIdx.x * 32u, by = blockIdx.y * 32u;
+    const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;  // the footprint, clamp-to-edge
+    {
+        const int32_t nx = P.hi_x - P.lo_x + 32, ny = P.hi_y - P.lo_y + 32;
+        const int32_t wm = (int32_t)X.w - 1, hm = (int32_t)X.h - 1;
+        constexpr int R = (FP_YQ * FP_YQ + 255) / 256;
+        uint32_t raw[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
+            if (ly < ny) raw[r] = X.px[(size_t)clampi(y0 + ly, 0, hm) * X.w + clampi(x0 + lx, 0, wm)];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
+            if (ly < ny) {
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FP_YQ + lx] = make_float4(d.r, d.g, d.b, d.a);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
+    if (x >= Y.w || y >= Y.h) return;
+    const int32_t base = ((int32_t)y - y0) * FP_YQ + ((int32_t)x - x0);
+    F4 s[2][2];
+#pragma unroll 1
+    for (int i = 0; i < 8; i++) {
+        const float4* T = tile + (base + P.oy[i] * FP_YQ + P.ox[i]);
+        switch (((P.hx >> i) & 1u) | ((P.hy >> i) & 1u) << 1) {  // launch-uniform
+            case 0: yquad_tap<0, 0>(T, i, s); break;
+            case 1: yquad_tap<1, 0>(T, i, s); break;
+            case 2: yquad_tap<0, 1>(T, i, s); break;
+            default: yquad_tap<1, 1>(T, i, s); break;
+        }
+    }
+    const bool full = x + 1u < Y.w && y + 1u < Y.h;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        uint32_t c[2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const F4 b1 = quant(L, {div12(s[b][a].r), div12(s[b][a].g), div12(s[b][a].b), div12(s[b][a].a)});
+            const float4 v = tile[base + b * FP_YQ + a];  // the pixel's own texel
+            c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
+        }
+        if (full) {
+            *reinterpret_cast<uint2*>(Y.px + (size_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
+        } else {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+                if (x + a < Y.w && y + b < Y.h) Y.px[(size_t)(y + b) * Y.w + x + a] = c[a];
+        }
+    }
+}
+
 // Fused last stage: out = col + 0.5 * q(Z), Z = Y + 0.5 * q(up8(U0, res (rx, ry))).
 __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTex U0, uint32_t rx,
                                                    uint32_t ry, uint32_t point, TapPlan P, Tex out) {
@@ -441,14 +538,6 @@ __device__ __forceinline__ F4 lerp2(const float4& t00, const float4& t10, const 
     q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
     q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
     return q;
-}
-__device__ __forceinline__ void acc(F4& s, const F4& q, int i) {
-    if (i == 0) {
-        s = q;
-    } else {
-        const float w = (i & 1) ? 2.0f : 1.0f;  // up8's sums, tap by tap
-        s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
-    }
 }
 // One tap for the quad: DX / DY = o(odd) - o(even) along x / y; T = the (2 + DY) x (2 + DX) texels from
 // (x>>1) + o(even), row stride FP.  s[b][a]: the pixel of y parity b, x parity a.
@@ -744,6 +833,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const flo
                                                                       const uint8_t* buckets, const uint32_t* X, uint32_t* Y, uint32_t w,
                                                                       uint32_t h, hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, w, h);
+    static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
+    if (P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ) {
+        hipLaunchKernelGGL(bloom_yq_kernel, dim3((w + 31u) / 32u, (h + 31u) / 32u), dim3(256), 0, s,
+                           Tables{lut, enc, buckets}, CTex{X, w, h}, P, Tex{Y, w, h});
+        return (int)hipGetLastError();
+    }
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, w, h);
     hipLaunchKernelGGL(bloom_y_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{X, w, h}, pm, P,
                        Tex{Y, w, h});
