@@ -79,3 +79,13 @@ def test_rccl_dry_run_gathers_bit_exact():
     assert d["backend"] == "nccl" and d["world_size"] == 1 and d["n_gpus"] == 1
     assert d["gather_verified_bit_exact"] is True
     assert "RCCL DRY RUN" in d["config"]["parallelism"]
+
+
+def test_power_state_settle_defaults_outside_the_timed_region():
+    """The untimed power-state settle (DESIGN.md §6 "Warm-up") runs by default for 100 ms, whatever
+    --warmup is, and can be switched off; it never changes --steps / --warmup."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    a = bench.parse(["--warmup", "5", "--steps", "20"])
+    assert a.settle_ms == 100.0 and a.warmup == 5 and a.steps == 20
+    assert bench.parse(["--settle-ms", "0"]).settle_ms == 0.0
