@@ -3,10 +3,15 @@
 (BASELINE.json configs[2]) and the max |delta pixel| against the CPU oracle (the normative WGSL
 restatement, oracle/bh_oracle.c).
 
-A "step" is one frame: one pass of the hot path (Scene::render -> the HIP march kernel) over the
-synthetic frame, the sky already resident in HBM.  Default arithmetic: BH_MATH_EXACT, the bit-exact
-path (the only one that can meet |delta| < 1e-4); RGBA16F col + blackout targets as
-north_star asks.
+A "step" is one batch of the offline renderer: ONE bh_render_frames launch of D frames of the
+camera path (D = --frames-per-launch, 32 at N = 1 for the headline; every frame is a full pass of the
+hot path, Scene::render -> the HIP march kernel, over the synthetic frame, the sky already resident in
+HBM).  `value` = frames x W x H / the timed region's wall time; `ms_per_step` is per batch and
+`ms_per_frame` per frame.  Default arithmetic: BH_MATH_EXACT, the bit-exact path (the only one that can
+meet |delta| < 1e-4); RGBA16F col + blackout targets as north_star asks.  Besides the
+headline the line carries `single_frame` (one bh_render per frame, the reference's one Scene::render
+per redraw, src/state.rs:270-279) and `orbit` (every frame its own camera), untimed for `value`, and
+`clock`: the shader clock measured inside the timed launches (bh_set_clock_probe).
 
 Workloads (--workload):
   strong   (default) north_star's fixed 4096x2048 frame, split over the N GPUs (strong scaling; at
@@ -14,10 +19,10 @@ Workloads (--workload):
   config4  BASELINE configs[3]: the fixed 8192x4096 frame split over the N GPUs (8 in the config);
   weak     ~8.4 Mpix per GPU at aspect 2:1 (the frame grows with N).
 N>1: one process per GPU (torch.distributed, RCCL).  Each rank renders its (tx + 3*ty) % N share of
-8x8 tiles in BH_LAYOUT_TILES_RGBM (RGB planes + the blackout mask word: 6.125 B per RGBA16F pixel),
-the shards are gathered to rank 0 (one collective per frame, overlapped with the next frame's
-render), and rank 0 unpacks BOTH targets, col and blackout_col, row-major.  Every timed step
-includes render, gather and unpack.
+8x8 tiles of the batch's D frames in BH_LAYOUT_TILES_RGBM (RGB planes + the blackout mask word: 6.125 B
+per RGBA16F pixel), the batch's shards are gathered to rank 0 (one collective per batch, overlapped with
+the next batch's render), and rank 0 unpacks BOTH targets, col and blackout_col, row-major.  Every timed
+step includes render, gather and unpack; the line carries a per-rank breakdown (`ranks`).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload strong|config4|weak]
 
@@ -54,12 +59,15 @@ WORKLOADS = {"strong": (4096, 2048), "config4": (8192, 4096)}
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=100)   # SURVEY §8d timing protocol: 100 timed frames
-    # SURVEY §8d asks for 10 warm-up frames; 300 (0.25 s) let the clocks settle
-    p.add_argument("--warmup", type=int, default=300)
-    p.add_argument("--settle-ms", type=float, default=100.0,
-                   help="untimed power-state settle before the warm-up: full launches of the workload for this "
-                        "many ms (the GPU clock ramps for ~30 ms under load after idle; DESIGN.md §6); 0 = none")
+    # a step is one batch (one launch of D frames): 20 x 32 = 640 timed frames at the headline
+    p.add_argument("--steps", type=int, default=20)
+    # 10 warm-up batches (320 frames, ~0.2 s): past the GPU clock's ~30 ms ramp under load
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--settle-ms", type=float, default=0.0,
+                   help="optional untimed power-state settle before the warm-up: full launches of the workload "
+                        "for this many ms (DESIGN.md §6); 0 = none (the warm-up batches cover the clock ramp)")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the single_frame / orbit legs (N = 1) that follow the timed region")
     p.add_argument("--workload", choices=["strong", "config4", "weak"], default="strong")
     p.add_argument("--config", type=int, choices=[1, 2, 3, 4, 5], default=0,
                    help="BASELINE.json configs[N-1]: 1 = 256x256 cap 64 no surfaces camera A, 2 = 1920x1080 cap 256 "
@@ -382,14 +390,14 @@ def main() -> int:
 
         pipe = multigpu.GatherPipeline(lambda: torch.empty((D * stride, tb), dtype=torch.uint8, device=dev),
                                        rank, n, on_frame, side_stream=torch.cuda.Stream(dev),
-                                       collective=True if args.rccl_dry_run else None)
+                                       collective=True if args.rccl_dry_run else None, timing=True)
 
     launch_no = [0]
     frame_no = [0]   # frames launched so far (the orbit path's frame index)
     orbit = {}       # frame index -> CameraUniform, built outside the timed region
 
-    def cams(nf):
-        if args.camera_path == "fixed":
+    def cams(nf, path=None):
+        if (path or args.camera_path) == "fixed":
             return None
         return [orbit[frame_no[0] + f] for f in range(nf)]
 
@@ -402,23 +410,27 @@ def main() -> int:
                                         schedule=sched, **shard)
                    for buf in (pipe.buffer(k) for k in range(pipe.depth))]
 
-    def launch(nf, **kw):
+    def launch(nf, path=None, **kw):
         """One bh_render_frames launch of nf <= D frames (this scene's camera, or the orbit path's); with
         debug outputs (kw) an unprepared call."""
         if not kw:
-            batches[launch_no[0] % len(batches)].render(n=nf, cameras=cams(nf), stream=stream)
+            batches[launch_no[0] % len(batches)].render(n=nf, cameras=cams(nf, path), stream=stream)
         elif pipe is None:
-            scene.render_frames(cols[:nf], bos[:nf], cameras=cams(nf), fmt=fmt, stream=stream, schedule=sched,
+            scene.render_frames(cols[:nf], bos[:nf], cameras=cams(nf, path), fmt=fmt, stream=stream, schedule=sched,
                                 **shard, **kw)
         else:
             buf = pipe.buffer(launch_no[0])
-            scene.render_frames([buf[f * stride:(f + 1) * stride] for f in range(nf)], None, cameras=cams(nf), fmt=fmt,
-                                stream=stream, schedule=sched, **shard, **kw)
+            scene.render_frames([buf[f * stride:(f + 1) * stride] for f in range(nf)], None, cameras=cams(nf, path),
+                                fmt=fmt, stream=stream, schedule=sched, **shard, **kw)
 
-    if args.camera_path == "orbit":
+    extra = not (args.no_extra or sharded or args.graph)
+    n_orbit_frames = (args.warmup + args.steps) * D if args.camera_path == "orbit" else 0
+    if extra:
+        n_orbit_frames = max(n_orbit_frames, EXTRA_ORBIT_LAUNCHES * D + D)
+    if n_orbit_frames:
         if args.graph:
             raise SystemExit("--graph replays one launch's cameras: use --camera-path fixed")
-        orbit.update({i: orbit_camera(bh, args.camera, i, W, H, args.orbit_deg) for i in range(args.warmup + args.steps + D)})
+        orbit.update({i: orbit_camera(bh, args.camera, i, W, H, args.orbit_deg) for i in range(n_orbit_frames)})
 
     graph = None
     if args.graph and not sharded:
@@ -446,14 +458,9 @@ def main() -> int:
         launch_no[0] += 1
         frame_no[0] += nf
 
-    def sizes(k):  # frames per launch covering k frames
-        return [min(D, k - i) for i in range(0, k, D)]
-
-    # power-state settle (DESIGN.md §6 "Warm-up"): after an idle period the shader clock under this load
-    # starts at 1.77-1.95 GHz and reaches its sustained 2.17 GHz only after ~30 ms of work, so a short
-    # --warmup would time the power manager's ramp, not the kernel.  Full launches of the same workload
-    # (render only: nothing is exchanged, no frame index advances) until settle_ms of GPU-busy wall time
-    # has passed; reported in the line ("clock_settle").  Untimed, like the W warm-up steps after it.
+    # optional power-state settle (DESIGN.md §6 "Warm-up"; off by default: the W warm-up batches cover
+    # the clock's ~30 ms ramp under load): full launches of the same workload (render only, nothing
+    # exchanged, no frame index advances) until settle_ms of GPU-busy wall time has passed.
     settle_frames, t_settle = 0, time.perf_counter()
     while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
         render(D)
@@ -461,32 +468,39 @@ def main() -> int:
         settle_frames += D
     settle_ms = (time.perf_counter() - t_settle) * 1e3
 
-    for nf in sizes(args.warmup):
-        render(nf)
-        exchange(nf)
+    for _ in range(args.warmup):
+        render(D)
+        exchange(D)
     if pipe is not None:
         pipe.drain()
     torch.cuda.synchronize(dev)
 
-    # timed region: barrier + synchronize on both sides; HIP events around every launch on the stream
-    # the kernel runs on (kernel duration for the roofline)
-    plan = sizes(args.steps)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in plan]
+    # shader clock inside the timed launches (bh_set_clock_probe; rows: timed region, extra legs)
+    clk = torch.zeros((3, 128), dtype=torch.int64, device=dev)
+    if graph is None:
+        scene.set_clock_probe(clk[0], CLOCK_STRIDE)
+
+    # timed region: K steps = K batches of D frames; barrier + synchronize on both sides; HIP events
+    # around every launch on the stream the kernel runs on (kernel duration for the roofline)
+    K = args.steps
+    first_timed = launch_no[0]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if sharded:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i, nf in enumerate(plan):
+    for i in range(K):
         ev[i][0].record(stream)
-        render(nf)
+        render(D)
         ev[i][1].record(stream)
-        exchange(nf)
+        exchange(D)
     if pipe is not None:
         pipe.drain()
     torch.cuda.synchronize(dev)
     if sharded:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    scene.set_clock_probe(None)
     per_rank = [elapsed]
     if sharded:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -495,22 +509,40 @@ def main() -> int:
         per_rank = [float(x.item()) for x in gl]
         elapsed = max(per_rank)
     kern_ms = np.array([a.elapsed_time(b) for a, b in ev])       # per launch
-    frames_in = np.array(plan, dtype=np.float64)
-    kern_frame_s = float(kern_ms.sum() / frames_in.sum()) / 1e3   # launch time per frame
-    sel = frames_in == D if (frames_in == D).any() else np.ones_like(frames_in, dtype=bool)
-    full = kern_ms[sel]                                          # the full launches (D frames), else all
-    kern_avg_s = float(full.mean()) / 1e3                        # their average duration
-    frames_avg = float(frames_in[sel].mean())                    # frames in each of them (D, or fewer)
+    kern_avg_s = float(kern_ms.mean()) / 1e3                     # a launch's average duration
+    kern_frame_s = kern_avg_s / D                                # launch time per frame
+    clock = bh.clock_mhz(clk[0].cpu().numpy()) if graph is None else None
+
+    ranks = None
+    if sharded:
+        # per-rank breakdown of the timed steps (HIP events): render = the launch on the render stream;
+        # gaps = render-stream idle between consecutive launches (waiting for a gather slot / the host);
+        # gather = render end -> the batch's collective complete (rank 0: every shard received);
+        # unpack = rank 0's two-target unpack of the batch; drain = rank 0, last render end -> last unpack end
+        tl = pipe.timeline(range(first_timed, first_timed + K))
+        gaps = [ev[i][1].elapsed_time(ev[i + 1][0]) for i in range(K - 1)]
+        mine = {"rank": rank, "render_ms": round(float(kern_ms.mean()), 4),
+                "render_ms_min_max": [round(float(kern_ms.min()), 4), round(float(kern_ms.max()), 4)],
+                "render_gap_ms": round(float(np.mean(gaps)) if gaps else 0.0, 4),
+                "gather_ms": round(float(np.mean(tl["gather_ms"])), 4) if tl["gather_ms"] else None,
+                "unpack_ms": round(float(np.mean(tl["unpack_ms"])), 4) if tl["unpack_ms"] else None,
+                "wall_s": round(per_rank[rank] if len(per_rank) > rank else elapsed, 6),
+                "clock_mhz": clock["mhz"] if clock else None}
+        if rank == 0 and tl["unpack_ms"]:
+            last = pipe.events.get(first_timed + K - 1, {})
+            if "unpacked" in last:
+                mine["drain_ms"] = round(ev[K - 1][1].elapsed_time(last["unpacked"]), 4)
+        ranks = [None] * n
+        dist.all_gather_object(ranks, mine)
 
     gather_ok = None
     if args.verify_gather and sharded and rank == 0:
-        # every frame of the last launch against a single-GPU render of that frame's camera
+        # every frame of the last batch against a single-GPU render of that frame's camera
         ref_c = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
         ref_b = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
-        last = plan[-1]
-        first = frame_no[0] - last  # frame index of the last launch's first frame
+        first = frame_no[0] - D  # frame index of the last batch's first frame
         gather_ok = True
-        for f in range(last):
+        for f in range(D):
             if args.camera_path == "orbit":
                 scene.render_frames([ref_c], [ref_b], cameras=[orbit[first + f]], fmt=fmt, stream=stream,
                                     schedule=sched)
@@ -520,6 +552,27 @@ def main() -> int:
             gather_ok = gather_ok and bool(torch.equal(ref_c.view(torch.uint8), frame_cols[f].view(torch.uint8))
                                            and torch.equal(ref_b.view(torch.uint8), frame_bos[f].view(torch.uint8)))
         del ref_c, ref_b
+
+    # the unfavourable cases beside the headline (N = 1, not part of `value`): one bh_render per frame
+    # (the reference's one Scene::render per redraw), and an orbiting camera path (every frame its own
+    # camera, so the learned dispatch order is a launch stale)
+    legs = {}
+    if extra:
+        legs["single_frame"] = _leg(lambda: launch(1, path="fixed"), EXTRA_SINGLE_FRAMES, 1, scene, clk[1], stream, dev, W, H, torch, bh)
+        frame_no[0] = 0
+        launch(D, path="orbit")  # untimed: the order learns the path's start
+        frame_no[0] = D
+
+        def orbit_launch():
+            launch(D, path="orbit")
+            frame_no[0] += D
+        legs["orbit"] = _leg(orbit_launch, EXTRA_ORBIT_LAUNCHES, D, scene, clk[2], stream, dev, W, H, torch, bh)
+        legs["single_frame"]["note"] = ("one bh_render_frames(n=1) per frame, fixed camera, back to back: the "
+                                        "reference's one Scene::render per redraw (src/state.rs:270-279)")
+        legs["orbit"].update(deg_per_frame=args.orbit_deg, frames_per_launch=D,
+                             note=f"camera {args.camera} orbiting the hole at {args.orbit_deg} deg/frame, {D} "
+                                  "frames per launch each with its own camera (the dispatch order learned from "
+                                  "the previous launch's frame 0)")
 
     # algorithmic work of one launch: RK steps over this rank's pixels (deterministic).  sum_n_rk is
     # the loop's own count (what the reference iterates); sum_steps the updates actually executed
@@ -535,21 +588,25 @@ def main() -> int:
     sum_steps = sum(int(b.cpu().numpy().view(np.uint16).astype(np.int64).sum()) for b in steps_bufs) // nm
 
     if rank == 0:
-        value = W * H * args.steps / elapsed / 1e6
+        frames = K * D
+        value = W * H * frames / elapsed / 1e6
         # per launch: D frames' executed steps / the launch's average duration (HIP events)
-        achieved_tf = sum_steps * frames_avg * F_STEP[flags] / kern_avg_s / 1e12
-        alg_bytes = int(my_bytes * frames_avg) + sky.nbytes
+        achieved_tf = sum_steps * D * F_STEP[flags] / kern_avg_s / 1e12
+        alg_bytes = int(my_bytes * D) + sky.nbytes
         achieved_gbs = alg_bytes / kern_avg_s / 1e9
         pmc = _pmc_entry(W, H, cap, args, n, D)
+        mhz = clock["mhz"] if clock else None
         result = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mpix/s",
             "n_gpus": n,
-            "steps": args.steps,
+            "steps": K,
             "warmup": args.warmup,
-            "clock_settle": {"ms": round(settle_ms, 1), "frames": settle_frames},
-            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "ms_per_step": round(elapsed / K * 1e3, 5),
+            "ms_per_frame": round(elapsed / frames * 1e3, 5),
+            "frames_per_s": round(frames / elapsed, 2),
+            "step": f"one batch: one bh_render_frames launch of {D} frames (ms_per_step is per batch)",
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
@@ -559,10 +616,10 @@ def main() -> int:
                 "workload": f"{workload}: {W}x{H} frame, cap {cap} RK steps, "
                             f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}"
                             + (f" orbiting {args.orbit_deg} deg/frame" if args.camera_path == "orbit" else "") + ", "
-                            f"{args.fmt} col+blackout, {args.math} math"
+                            f"{args.fmt} col+blackout, {args.math} math, {D} frames per step"
                             + ("" if not sharded else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
                                                   "(RGB planes + blackout mask) to rank 0 overlapped with the next "
-                                                  "frame, rank 0 unpacks col and blackout_col"),
+                                                  "batch, rank 0 unpacks col and blackout_col"),
                 "baseline_config": args.config or None,
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
                 "math": args.math,
@@ -578,26 +635,34 @@ def main() -> int:
             "kernel": {"name": f"bh::{kernel_ns(args, my_tiles, D, cap, dev)}::march_{args.schedule.split('-')[0]}_kernel<{fmt}u"
                                + ((f", {flags}u>" if flags in (0, 3) else ", 4294967295u>")  # SF: 0/3 folded, else dynamic
                                   if args.schedule.startswith("tile") else ">"),
-                       "launches": len(plan), "frames_per_launch": D, "tiles_per_frame": my_tiles,
-                       "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(full.min()), 5),
-                       "max_ms": round(float(full.max()), 5), "ms_per_frame": round(kern_frame_s * 1e3, 5),
+                       "launches": K, "frames_per_launch": D, "tiles_per_frame": my_tiles,
+                       "avg_ms": round(kern_avg_s * 1e3, 5), "min_ms": round(float(kern_ms.min()), 5),
+                       "max_ms": round(float(kern_ms.max()), 5), "ms_per_frame": round(kern_frame_s * 1e3, 5),
                        "sum_n_rk": sum_nrk, "sum_steps": sum_steps,
                        "mean_n_rk": round(sum_nrk / (my_tiles * 64), 4), "frames_per_s": round(1.0 / kern_frame_s, 2),
-                       "frames_per_timed_launch": frames_avg,
-                       "note": "avg/min/max over the full launches of frames_per_launch frames (all launches when "
-                               "the timed frames fill none: frames_per_timed_launch); sum_n_rk / sum_steps per frame "
-                               "(this rank's tiles)"},
+                       "note": "avg/min/max over the K timed launches (HIP events on the render stream, the order "
+                               "kernel included); sum_n_rk / sum_steps per frame (this rank's tiles)"},
+            "clock": (dict(clock, stride=CLOCK_STRIDE,
+                           note="shader clock during the timed launches: every "
+                                f"{CLOCK_STRIDE}th wave of the march kernel reads s_memtime (shader clock) and "
+                                "s_memrealtime (100 MHz) at its start and end (bh_set_clock_probe); mhz = 100 x "
+                                "sum(shader ticks) / sum(100 MHz ticks) over those waves; peak_mhz is the clock "
+                                "the 157.3 TFLOP/s peak assumes") | {"peak_mhz": PEAK_MHZ}) if clock else None,
+            "clock_settle": {"ms": round(settle_ms, 1), "frames": settle_frames} if args.settle_ms > 0 else None,
             "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 5),
-                         "traffic": (round(pmc["hbm_bytes_per_launch"] * frames_avg / D)
-                                     if pmc.get("hbm_bytes_per_launch") else None),
+                         "frac_at_measured_clock": (round(achieved_tf / (PEAK_FP32_TFLOPS * mhz / PEAK_MHZ), 5)
+                                                    if mhz else None),
+                         "traffic": (round(pmc["hbm_bytes_per_launch"]) if pmc.get("hbm_bytes_per_launch") else None),
                          "valu_busy": pmc.get("valu_busy_est"),
                          "valu_lane_utilization": pmc.get("valu_lane_utilization"),
                          "pmc_source": pmc.get("source"),
                          "issue_slot_frac": round(achieved_tf / (PEAK_FP32_TFLOPS / 2), 5),
                          "note": f"{F_STEP[flags]} flop-eq per executed RK step (SURVEY §8d) x sum_steps x "
-                                 "frames_per_timed_launch / avg launch time (HIP events on the render stream); FP32 "
-                                 "VALU-bound, no MFMA-shaped work; traffic = HBM bytes/launch and valu_busy = VALU "
+                                 "frames_per_launch / avg launch time (HIP events on the render stream); FP32 "
+                                 "VALU-bound, no MFMA-shaped work; frac_at_measured_clock = achieved over the "
+                                 "peak scaled to the clock measured in the timed launches (clock.mhz / "
+                                 "clock.peak_mhz); traffic = HBM bytes/launch and valu_busy = VALU "
                                  "issue cycles / SIMD cycles, from the rocprofv3 PMC passes of this configuration "
                                  "named in pmc_source (profiles/pmc_traffic.json), null if none. The 157.3 TFLOP/s "
                                  "peak counts an FMA as 2 flops in every lane-cycle; the WGSL's op sequence has no "
@@ -608,11 +673,13 @@ def main() -> int:
                              "algorithmic_bytes_per_launch": alg_bytes,
                              "note": "this rank's outputs (N>1: its RGBM shard, and on rank 0 the two "
                                      "unpacked targets) + the sky texture read once"},
+            **legs,
         }
         if sharded:
             result["world_size"] = dist.get_world_size()
             result["backend"] = dist.get_backend()
             result["per_rank_s"] = [round(x, 6) for x in per_rank]
+            result["ranks"] = ranks
         if args.no_cpu or sharded:
             result["cpu_baseline"] = None
         else:
@@ -624,6 +691,35 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+# extra legs after the timed region (N = 1): single-frame launches, orbit-path launches
+EXTRA_SINGLE_FRAMES = 24
+EXTRA_ORBIT_LAUNCHES = 4
+CLOCK_STRIDE = 256   # every 256th wave of a march launch samples the shader clock
+PEAK_MHZ = 2400.0    # the shader clock behind the 157.3 TFLOP/s FP32 peak (1024 SIMDs x 32 lanes x 2 x 2.4 GHz)
+
+
+def _leg(fn, launches: int, frames_per_launch: int, scene, clk_row, stream, dev, W, H, torch, bh) -> dict:
+    """Time `launches` calls of fn (each one launch of frames_per_launch frames) back to back: wall time
+    between synchronises, HIP events around each launch, and the shader clock inside them."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(launches)]
+    scene.set_clock_probe(clk_row, CLOCK_STRIDE)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    scene.set_clock_probe(None)
+    k = np.array([a.elapsed_time(b) for a, b in ev])
+    frames = launches * frames_per_launch
+    return {"frames": frames, "ms_per_frame": round(wall / frames * 1e3, 5),
+            "kernel_ms_per_frame": round(float(k.sum()) / frames, 5),
+            "mpix_s": round(W * H * frames / wall / 1e6, 3),
+            "clock_mhz": bh.clock_mhz(clk_row.cpu().numpy())["mhz"]}
 
 
 def kernel_ns(args, tiles: int, D: int, cap: int, dev) -> str:
@@ -649,11 +745,13 @@ def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     carries), and for frames of fewer than 16384 tiles enough frames for ~2^19 tiles per launch (up to
     BH_MAX_FRAMES = 256, staged through the device frame table): 256x256 cap 64 at D = 32/64/128/256
     0.00643/0.00620/0.00608/0.00604, 1920x1080 at D = 32/64/128 0.1500/0.1498/0.1492, the headline at
-    D = 32/64 0.6078/0.6074 (profiles/r02c/frames_table/).  N > 1: 8 -- the last launch's gather and
-    unpack cannot overlap a next render, so the pipeline's drain grows with D (at N = 8 about D x 0.12 ms
-    against ~0.085 ms of render per frame) while the shard's render gains only ~8 % from 8 to 32."""
+    D = 32/64 0.6078/0.6074 (profiles/r02c/frames_table/).  N > 1: 16 -- the last batch's gather and
+    unpack cannot overlap a next render, so the pipeline drains one batch at the end of the timed region
+    (at N = 8 about D x 0.12 ms against ~0.085 ms of render per frame): with a step = one batch that is
+    ~1/(K+1) of K steps whatever D is, while the shard's render gains ~6 % from 8 to 16 frames per launch
+    and the receive buffers grow with D."""
     if n > 1:
-        return 8
+        return 16
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
     D = 32
     while D < bh_max_frames() and tiles * D < (1 << 19):

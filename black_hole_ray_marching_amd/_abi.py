@@ -29,7 +29,7 @@ BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled bu
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
 
@@ -111,6 +111,7 @@ SIGNATURES = {
     "bh_bloom": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_void_p, C.c_void_p]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
+    "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
 }
 
 _lib = None

@@ -472,7 +472,9 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             default: yquad_tap<1, 1>(T, i, s); break;
         }
     }
-    const bool full = x + 1u < Y.w && y + 1u < Y.h;
+    // both pixels of each quad row in one 8-byte store: inside the frame, and rows 8-byte aligned (even
+    // width; x is even); else one word per pixel
+    const bool full = x + 1u < Y.w && y + 1u < Y.h && (Y.w & 1u) == 0u;
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         uint32_t c[2];

@@ -66,6 +66,9 @@ struct MarchArgs {
     // up to BH_INLINE_FRAMES of them inline, more from a device table (frame_table, else null)
     uint32_t n_frames;
     const FrameArgs* frame_table;
+    // shader-clock probe (bh_set_clock_probe): per-XCD accumulators, sampled slots = slot & clk_mask == 0
+    unsigned long long* clk;
+    uint32_t clk_mask;
     FrameArgs frames[BH_INLINE_FRAMES];
 };
 // passed by value: the kernel argument segment holds at most 4 KiB (with the persistent kernel's

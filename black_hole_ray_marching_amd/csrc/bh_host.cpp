@@ -37,6 +37,7 @@ struct bh_ctx {
         void* stream = nullptr;
         uint64_t last_use = 0;
         bool valid = false;                  // costs and histogram agree (false: start afresh)
+        bool captured = false;               // used by a launch captured into a graph: never evicted
         uint8_t* tile_cost = nullptr;
         uint32_t* order = nullptr;
         uint32_t* counters = nullptr;        // ORDER_WORDS words (bh_common.hpp)
@@ -60,6 +61,9 @@ struct bh_ctx {
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
     std::vector<uint32_t*> bloom_tex;
     uint64_t bloom_key = ~0ull;
+    // shader-clock probe of the march launches (bh_set_clock_probe): device accumulators or null
+    unsigned long long* clk = nullptr;
+    uint32_t clk_mask = 0;
 };
 
 // A weighted tile partition (include/bh_render.h, bh_partition_create).
@@ -730,15 +734,32 @@ static int stage_frame_table(bh_ctx* c, hipStream_t s, const bh::FrameArgs* fram
 
 // The temporal-order state of (geometry, shard, stream): found, or created (allocating; the LRU state
 // is evicted beyond BH_ORDER_STATES).  New states start with all costs 0 and an empty histogram.
-static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStream_t s, bh_ctx::OrderState** out) {
+// Graph contract (include/bh_render.h): a state used by a launch captured into a graph is marked and
+// never evicted (its buffers are what the graph's kernels read and write); when every state is marked
+// the ctx keeps more than BH_ORDER_STATES instead of evicting one.  A capturing stream cannot create a
+// state (the allocation and the reset are not capturable work): BH_ERR_UNSUPPORTED.
+static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStream_t s, bool capturing,
+                       bh_ctx::OrderState** out) {
     const uint64_t pser = d->partition ? d->partition->serial : 0u;
     for (auto& o : c->orders)
         if (o.width == d->width && o.height == d->height && o.shard_index == d->shard_index &&
             o.shard_count == d->shard_count && o.partition == pser && o.n_tiles == nt && o.stream == (void*)s) {
             o.last_use = ++c->order_clock;
+            if (capturing) {
+                if (!o.valid) {
+                    g_last_error = "bh_render: this (geometry, shard, stream) must be rendered once outside graph capture";
+                    return BH_ERR_UNSUPPORTED;
+                }
+                o.captured = true;
+            }
             *out = &o;
             return BH_OK;
         }
+    if (capturing) {
+        g_last_error = "bh_render: the first render of a (geometry, shard, stream) allocates; render it once "
+                       "before capturing it into a graph";
+        return BH_ERR_UNSUPPORTED;
+    }
     bh_ctx::OrderState n;
     n.width = d->width; n.height = d->height; n.shard_index = d->shard_index; n.shard_count = d->shard_count;
     n.partition = pser;
@@ -752,13 +773,15 @@ static int order_state(bh_ctx* c, const bh_render_desc* d, uint64_t nt, hipStrea
         if (n.order) (void)hipFree(n.order);
         return he == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(he, "hipMalloc(temporal order)");
     }
-    if (c->orders.size() >= BH_ORDER_STATES) {  // evict the least recently used
-        size_t v = 0;
-        for (size_t i = 1; i < c->orders.size(); ++i)
-            if (c->orders[i].last_use < c->orders[v].last_use) v = i;
-        auto& o = c->orders[v];
-        (void)hipFree(o.tile_cost); (void)hipFree(o.order); (void)hipFree(o.counters);
-        c->orders.erase(c->orders.begin() + (long)v);
+    if (c->orders.size() >= BH_ORDER_STATES) {  // evict the least recently used state no graph holds
+        size_t v = c->orders.size();
+        for (size_t i = 0; i < c->orders.size(); ++i)
+            if (!c->orders[i].captured && (v == c->orders.size() || c->orders[i].last_use < c->orders[v].last_use)) v = i;
+        if (v < c->orders.size()) {
+            auto& o = c->orders[v];
+            (void)hipFree(o.tile_cost); (void)hipFree(o.order); (void)hipFree(o.counters);
+            c->orders.erase(c->orders.begin() + (long)v);
+        }
     }
     n.last_use = ++c->order_clock;
     c->orders.push_back(n);
@@ -857,6 +880,8 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     // k = (DP * RS) * -1.5 (:126); the per-frame fields (camera, c_ps, outputs)
     a.kfac = (a.dp * a.rs) * -1.5f;
     a.n_frames = n_frames;
+    a.clk = c->clk;
+    a.clk_mask = c->clk_mask;
     std::vector<bh::FrameArgs> table;  // n_frames > BH_INLINE_FRAMES: staged in the stream's device table
     if (n_frames > bh::BH_INLINE_FRAMES) table.resize(n_frames);
     bh::FrameArgs* fa = table.empty() ? a.frames : table.data();
@@ -882,7 +907,9 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     bh_ctx::OrderState* os = nullptr;
     if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
         // temporal order of this (geometry, shard, stream): allocated at its first render only
-        int st = order_state(c, d, nt, s, &os);
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+        int st = order_state(c, d, nt, s, capturing, &os);
         if (st != BH_OK) return st;
         if (!os->valid) {
             // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent
@@ -908,6 +935,13 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
         if (os) os->valid = false;
         return hip_fail((hipError_t)e, "march kernel launch");
     }
+    return BH_OK;
+}
+
+int bh_set_clock_probe(bh_ctx* c, uint64_t* acc, uint32_t stride) {
+    if (!c || (acc && (stride == 0u || (stride & (stride - 1u)) != 0u))) return BH_ERR_INVALID_ARG;
+    c->clk = reinterpret_cast<unsigned long long*>(acc);
+    c->clk_mask = acc ? stride - 1u : 0u;
     return BH_OK;
 }
 

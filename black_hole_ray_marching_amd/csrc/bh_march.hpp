@@ -1082,6 +1082,26 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     }
 }
 
+// Shader-clock probe (bh_set_clock_probe): a sampled wave reads both counters when it starts and adds
+// the differences at its end to its XCD's accumulators (vector atomics from lane 0, no return).  (A
+// divergent lane-0 branch before the march trips an "illegal VGPR to SGPR copy" in this compiler, so
+// the start values are held in 4 SGPRs instead: 68 of the 80 that keep 8 waves per SIMD.)
+struct ClockStart { unsigned long long t, r; };
+__device__ __forceinline__ ClockStart clock_start() {
+    return {__builtin_amdgcn_s_memtime(), __builtin_amdgcn_s_memrealtime()};
+}
+__device__ __forceinline__ void clock_end(unsigned long long* acc, const ClockStart& c0) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime() - c0.t;      // shader clock
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime() - c0.r;  // constant 100 MHz
+    const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;  // HW_REG_XCC_ID[2:0]
+    if ((threadIdx.x & 63u) == 0u) {
+        unsigned long long* p = acc + 16u * x;
+        __hip_atomic_fetch_add(p, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p + 1, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(p + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // One wave per dispatch slot (the grid covers every slot), BH_WG_WAVES waves per workgroup.
 template <uint32_t FMT, uint32_t SF>
 __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs A) {
@@ -1090,7 +1110,11 @@ __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs 
     __syncthreads();
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
     if (slot >= A.n_tiles * A.n_frames) return;  // wave-uniform
+    const bool probe = A.clk && (slot & A.clk_mask) == 0u;
+    ClockStart c0{0ull, 0ull};
+    if (probe) c0 = clock_start();
     march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
+    if (probe) clock_end(A.clk, c0);
 }
 
 // ---- schedule BH_SCHED_PERSISTENT: persistent waves with per-lane refill (A/B option) ------------

@@ -213,10 +213,15 @@ class GatherPipeline:
     stream; before a receive buffer is gathered into again, the render stream waits for the unpack
     that read it (and RCCL's stream follows the render stream).  `collective`: gather through
     torch.distributed even at world size 1 (default: only when world > 1; a one-rank group checks
-    the collective calls on a 1-GPU box)."""
+    the collective calls on a 1-GPU box).
+
+    `timing` (CUDA): HIP events per frame for the bench's per-rank breakdown (timeline()): `submitted`
+    on the producer stream when the gather is issued (the end of the render), `gathered` when the
+    frame's collective is complete as seen by rank 0's side stream (every rank's shard received), or by
+    another rank's producer stream (its send buffer released), `unpacked` after rank 0's on_frame."""
 
     def __init__(self, make_buffer, rank: int, world: int, on_frame=None, depth: int = 2, group=None,
-                 side_stream=None, collective=None):
+                 side_stream=None, collective=None, timing=False):
         import torch
         if depth < 1:
             raise ValueError("depth >= 1")
@@ -232,6 +237,27 @@ class GatherPipeline:
         self.side = side_stream if rank == 0 else None
         self.consumed = [None] * depth  # per slot: event after the on_frame that read recv[slot]
         self.collective = world > 1 if collective is None else bool(collective)
+        self.timing = bool(timing)
+        self.events = {}  # frame -> {"submitted" | "gathered" | "unpacked": torch.cuda.Event}
+
+    def _mark(self, i: int, what: str, stream=None) -> None:
+        if self.timing:
+            import torch
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream if stream is not None else torch.cuda.current_stream())
+            self.events.setdefault(i, {})[what] = ev
+
+    def timeline(self, frames) -> dict:
+        """Per-frame ms between the timing events of `frames` (synchronise first): gather = submitted ->
+        gathered, unpack = gathered -> unpacked (rank 0 with a side stream)."""
+        out = {"gather_ms": [], "unpack_ms": []}
+        for i in frames:
+            e = self.events.get(i, {})
+            if "submitted" in e and "gathered" in e:
+                out["gather_ms"].append(e["submitted"].elapsed_time(e["gathered"]))
+            if "gathered" in e and "unpacked" in e:
+                out["unpack_ms"].append(e["gathered"].elapsed_time(e["unpacked"]))
+        return out
 
     def buffer(self, i: int):
         return self.bufs[i % self.depth]
@@ -243,6 +269,7 @@ class GatherPipeline:
             import torch
             torch.cuda.current_stream().wait_event(self.consumed[slot])
             self.consumed[slot] = None
+        self._mark(i, "submitted")
         if not self.collective:
             work = None
             if self.rank == 0:
@@ -259,6 +286,8 @@ class GatherPipeline:
         slot = i % self.depth
         if work is not None:
             work.wait()  # the current stream: the send buffer may be rendered into again
+        if self.side is None:
+            self._mark(i, "gathered")
         if self.rank == 0 and self.on_frame is not None:
             if self.side is None:
                 self.on_frame(i, self.recv[slot])
@@ -270,7 +299,9 @@ class GatherPipeline:
                         work.wait()  # the side stream: the received frame is complete
                     else:
                         self.side.wait_stream(producer)  # the local copy into recv[slot]
+                    self._mark(i, "gathered", self.side)
                     self.on_frame(i, self.recv[slot])
+                    self._mark(i, "unpacked", self.side)
                     ev = torch.cuda.Event()
                     ev.record(self.side)
                     self.consumed[slot] = ev

@@ -370,6 +370,13 @@ class Scene:
                                             for i in range(n)])
         return FrameBatch(self, descs, (outputs, blackout_outputs, dbg_n_rk, dbg_fate, dbg_steps, partition))
 
+    def set_clock_probe(self, acc, stride: int = 256) -> None:
+        """bh_set_clock_probe: arm (acc = a zeroed device buffer of 128 u64) or disarm (acc = None) the
+        shader-clock sampling of this scene's march launches; clock_mhz() reads the result."""
+        if acc is not None:
+            _check_size(acc, 128 * 8, "acc", "set_clock_probe")
+        check(self.lib.bh_set_clock_probe(self._ctx, _ptr(acc), stride), "bh_set_clock_probe")
+
     def bloom(self, col, blackout, out, *, levels: int = 3, schedule: int = 0, width: int | None = None,
               height: int | None = None, stream=None) -> None:
         """Bloom::render (src/bloom.rs:53-71): the Kawase bloom + remix chain over this scene's two
@@ -382,6 +389,18 @@ class Scene:
             _check_size(t, need, name, "bloom")
         check(self.lib.bh_bloom(self._ctx, _ptr(col), _ptr(blackout), width or self.width, height or self.height,
                                 levels, schedule, _ptr(out), _stream_handle(stream)), "bh_bloom")
+
+
+def clock_mhz(acc) -> dict:
+    """The shader clock sampled by set_clock_probe: acc (128 u64 as an int64 array) -> per-XCD MHz and
+    the clock over all sampled waves (100 MHz * shader ticks / reference ticks)."""
+    a = np.asarray(acc, dtype=np.int64).view(np.uint64).reshape(8, 16)
+    ticks, ref, waves = a[:, 0].astype(np.float64), a[:, 1].astype(np.float64), a[:, 2].astype(np.int64)
+    per = [round(100.0 * t / r, 1) if r > 0 else None for t, r in zip(ticks, ref)]
+    tot = float(ref.sum())
+    return {"mhz": round(100.0 * float(ticks.sum()) / tot, 1) if tot > 0 else None,
+            "per_xcd_mhz": per, "waves": int(waves.sum()),
+            "wave_ms": round(tot / 1e5 / max(1, int(waves.sum())), 5)}
 
 
 def _stream_handle(stream) -> int | None:

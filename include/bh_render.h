@@ -28,15 +28,20 @@
  * Conventions: every function returns BH_OK (0) or a negative bh_status; nothing aborts or throws
  * across the ABI.  Output pointers are caller-owned DEVICE pointers (the reference's consumer, Bloom,
  * owns its textures and lends views: src/bloom.rs:31-37).  bh_render is asynchronous on the given
- * HIP stream (NULL = the legacy default stream) and never synchronises the host.  The tile
- * schedule's temporal dispatch order keeps small per-(frame geometry, shard, stream) device buffers
- * in the ctx: the FIRST bh_render of such a key allocates them (hipMalloc, not capturable); every
- * later call with that key allocates nothing and may be captured into a hipGraph.  Those buffers
- * are never freed or moved before bh_destroy (a captured graph keeps valid pointers), except that a
- * ctx holds at most BH_ORDER_STATES keys and evicts the least recently used beyond that (re-capture
- * graphs after rendering more keys than that).  Renders of one ctx on different streams use
- * different order state, so they may run concurrently (frames in flight).  One bh_ctx per device; a
- * ctx is not thread-safe, distinct ctx objects may be used from distinct threads (one per rank).
+ * HIP stream (NULL = the legacy default stream).  It never synchronises the host, with one exception:
+ * a bh_render_frames call of more than 32 frames may wait for the copy of the call four before it on
+ * the same stream (its pinned staging ring, see bh_render_frames).  The tile schedule's temporal
+ * dispatch order keeps small per-(frame geometry, shard, stream) device buffers in the ctx: the FIRST
+ * bh_render of such a key allocates them (hipMalloc) and must not be captured -- on a capturing stream
+ * it returns BH_ERR_UNSUPPORTED and launches nothing; every later call with that key allocates nothing
+ * and may be captured into a hipGraph.  Those buffers are never freed or moved before bh_destroy
+ * while a graph may use them: a key rendered under stream capture is never evicted.  Other keys are
+ * evicted least-recently-used beyond BH_ORDER_STATES (when every key has been captured the ctx keeps
+ * more instead).  Renders of one ctx on different streams with the TILE or PAIR schedule use
+ * different order state and no other shared scratch, so they may run concurrently (frames in flight);
+ * the PERSISTENT schedule (shared work counters) and bh_bloom (shared scratch textures) must not run
+ * concurrently with themselves on one ctx.  One bh_ctx per device; a ctx is not thread-safe, distinct
+ * ctx objects may be used from distinct threads (one per rank).
  */
 #ifndef BH_RENDER_H
 #define BH_RENDER_H
@@ -48,7 +53,7 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 5
+#define BH_ABI_VERSION 6
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
@@ -246,7 +251,8 @@ int bh_render(bh_ctx* ctx, const bh_camera_uniform* camera, const bh_uniforms* u
  * temporal order of (geometry, shard, stream) learns from frame 0 of each call.  Up to 32 frames travel
  * in the kernel argument; a call of more stages the frames' arguments through a pinned host ring into a
  * device table of the stream (allocated at the first such call, never captured into a HIP graph: a
- * capturing stream gets BH_ERR_UNSUPPORTED for n_frames > 32). */
+ * capturing stream gets BH_ERR_UNSUPPORTED for n_frames > 32).  The ring has 4 slots: such a call
+ * blocks the host until the copy of the 4th such call before it on the stream has executed. */
 #define BH_MAX_FRAMES 256
 int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* cameras, const bh_uniforms* uniforms,
                      const bh_render_desc* descs, void* hip_stream);
@@ -339,6 +345,16 @@ int bh_srgb_encode_table(float* out257);
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);
+
+/* Diagnostics: the shader clock DURING march launches (the bench's "clock" block).  While armed
+ * (acc != NULL), every wave of the tile schedule's march kernels of this ctx whose dispatch slot is a
+ * multiple of `stride` (a power of two) reads the shader-clock counter (s_memtime) and the constant
+ * 100 MHz counter (s_memrealtime) when it starts and when it ends, and adds the differences to its
+ * XCD's slot: acc[16*x + 0] += shader ticks, acc[16*x + 1] += 100 MHz ticks, acc[16*x + 2] += 1 (x =
+ * the XCD, 0..7; acc = 128 u64 of device memory, zeroed by the caller, 128 B per XCD).  The clock of
+ * XCD x over the sampled waves' lifetimes is 100 MHz * acc[16x] / acc[16x+1].  Takes effect from the
+ * next bh_render* call; never changes a result.  acc = NULL disarms. */
+int bh_set_clock_probe(bh_ctx* ctx, uint64_t* acc, uint32_t stride);
 
 #ifdef __cplusplus
 }

@@ -81,11 +81,26 @@ def test_rccl_dry_run_gathers_bit_exact():
     assert "RCCL DRY RUN" in d["config"]["parallelism"]
 
 
-def test_power_state_settle_defaults_outside_the_timed_region():
-    """The untimed power-state settle (DESIGN.md §6 "Warm-up") runs by default for 100 ms, whatever
-    --warmup is, and can be switched off; it never changes --steps / --warmup."""
+def test_steps_are_batches_and_the_settle_is_optional():
+    """A step is one batch (one bh_render_frames launch of D frames, VERDICT/ADVICE r02): the driver's
+    --steps / --warmup count batches and are never changed; the power-state settle of round 2 is off
+    by default (the warm-up batches cover the clock ramp) and can still be asked for."""
     sys.path.insert(0, str(ROOT))
     import bench
     a = bench.parse(["--warmup", "5", "--steps", "20"])
-    assert a.settle_ms == 100.0 and a.warmup == 5 and a.steps == 20
-    assert bench.parse(["--settle-ms", "0"]).settle_ms == 0.0
+    assert a.settle_ms == 0.0 and a.warmup == 5 and a.steps == 20
+    assert bench.parse(["--settle-ms", "100"]).settle_ms == 100.0
+    assert bench.auto_frames_per_launch(1, 4096, 2048, 512) == 32
+    assert bench.auto_frames_per_launch(8, 4096, 2048, 512) == 16
+
+
+def test_clock_accumulators_to_mhz():
+    """bh_set_clock_probe's per-XCD accumulators (shader ticks, 100 MHz ticks, waves) -> MHz."""
+    import numpy as np
+    import black_hole_ray_marching_amd as bh
+    acc = np.zeros(128, np.int64)
+    acc[0:3] = (2_100_000, 100_000, 10)       # XCD 0: 2100 MHz
+    acc[16:19] = (2_300_000, 100_000, 10)     # XCD 1: 2300 MHz
+    c = bh.clock_mhz(acc)
+    assert c["mhz"] == 2200.0 and c["per_xcd_mhz"][:2] == [2100.0, 2300.0] and c["per_xcd_mhz"][2] is None
+    assert c["waves"] == 20 and c["wave_ms"] == 0.1  # 1 ms of 100 MHz ticks per 10 waves

@@ -435,3 +435,60 @@ def test_graph_capture_of_render_frames(torch_cuda, sky_small):
         torch.cuda.synchronize()
         assert torch.equal(o.view(torch.int32), ref.view(torch.int32))
     scene.close()
+
+
+def test_graph_keeps_its_order_state_past_eviction(torch_cuda, sky_small):
+    """Graph contract (include/bh_render.h): a (geometry, shard, stream) key rendered
+    under stream capture is never evicted, however many other keys are rendered after it (beyond
+    BH_ORDER_STATES), so a replay never touches a freed buffer and renders the same bytes; a key seen for
+    the first time on a capturing stream is refused with a status (it would allocate)."""
+    torch = torch_cuda
+    W, H = 64, 32
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=512, math=bh.BH_MATH_EXACT)
+    out = torch.full((H, W, 4), float("nan"), device="cuda")
+    s = torch.cuda.Stream()
+    scene.render(out, None, stream=s)  # allocates this key's order state
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    other = torch.empty((2 * H, 2 * W, 4), device="cuda")
+    with torch.cuda.graph(g, stream=s):
+        with pytest.raises(bh.BhError):  # a new key under capture: refused, nothing launched
+            scene.render(other, None, stream=s, width=2 * W, height=2 * H)
+        scene.render(out, None, stream=s)
+    # 33 other keys (frame widths) on the same stream: more than BH_ORDER_STATES
+    big = torch.empty((H, W + 8 * (bh.BH_ORDER_STATES + 2), 4), device="cuda")
+    for k in range(bh.BH_ORDER_STATES + 1):
+        w = W + 8 * (k + 1)
+        scene.render(big, None, stream=s, width=w, height=H)
+    torch.cuda.synchronize()
+    out.fill_(float("nan"))
+    g.replay()
+    torch.cuda.synchronize()
+    ref = torch.empty_like(out)
+    scene.render(ref, None)
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    scene.close()
+
+
+def test_clock_probe_samples_the_march_without_changing_it(torch_cuda, sky_small):
+    """bh_set_clock_probe: the sampled waves report a plausible shader clock (MHz from s_memtime /
+    s_memrealtime), on at least one XCD, and the frame's bytes are those of an unprobed render."""
+    torch = torch_cuda
+    W, H = 512, 256
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=512, math=bh.BH_MATH_EXACT)
+    a = torch.empty((H, W, 4), device="cuda")
+    b = torch.empty((H, W, 4), device="cuda")
+    scene.render(a, a.clone())
+    acc = torch.zeros(128, dtype=torch.int64, device="cuda")
+    scene.set_clock_probe(acc, 16)
+    scene.render(b, b.clone())
+    scene.set_clock_probe(None)
+    torch.cuda.synchronize()
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    c = bh.clock_mhz(acc.cpu().numpy())
+    assert c["waves"] == (W // 8) * (H // 8) // 16, c
+    assert 300.0 < c["mhz"] < 3500.0, c
+    with pytest.raises(bh.BhError):
+        scene.set_clock_probe(acc, 3)  # stride must be a power of two
+    scene.close()
