@@ -501,11 +501,6 @@ __device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
 #ifndef BH_TAIL_PACKED
 #define BH_TAIL_PACKED 0
 #endif
-// The tail loop (waves still marching after PRIO_ITERS iterations): 1 = the lane-spread form
-// (march_spread, exact mode), 0 = one lane per ray (march_cycles; the fast build, and A/B variants).
-#ifndef BH_TAIL_SPREAD
-#define BH_TAIL_SPREAD (!BH_FAST)
-#endif
 #if !BH_FAST && BH_TAIL_PACKED
 // ---- the tail's step, in packed FP32 (exact mode) ---------------------------------------------------
 // The same arithmetic as step_bf<true, XOps<true>> -- every rounding identical, in the same order, the
@@ -964,250 +959,6 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
     }
 }
 
-#if !BH_FAST
-// ---- the tail in lane-spread form (exact mode) ------------------------------------------------------
-// A wave still marching after PRIO_ITERS iterations typically holds one to a few photon-sphere rays
-// among 64 lanes, and its time is the serial chain of its slowest ray (up to max_iters steps): a lone
-// wave issues one instruction every ~4.6 cycles however many of its lanes are live, so
-// the tail costs instructions per step, not lanes.  So each ray left is moved to one lane quad (16
-// quads, refilled as rays end: march_spread): lane c = 0, 1, 2 of the quad holds component c of ro and rd (lane 3 mirrors
-// x), the per-ray scalars (travelled, s, n_rk, outside and the whole scalar chain: r, the SDFs, dt, the
-// four denominators and their reciprocals) are computed identically in all four lanes, and every vec3
-// operation becomes ONE instruction.  Dot products read the quad's other lanes through DPP
-// (quad_perm broadcasts fold into the adds: v_add_f32_dpp), in the oracle's order (x*x + y*y) + z*z.
-// Every rounding is the scalar step's (step_bf<true, XOps<CR>>): same IEEE operations on the same
-// operands, so the bits are the same; ~190 instead of ~300 instructions per step.
-constexpr uint32_t SPREAD_MAX = 16;  // quads of a wave
-
-template <int K>
-__device__ __forceinline__ float qb(float v) {  // lane K of the quad, broadcast to the quad
-    // every lane reads a lane of its own quad (all rows and banks enabled): no `old` value is needed
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), K * 0x55, 0xF, 0xF, true));
-}
-// dot(a, b) = (a.x*b.x + a.y*b.y) + a.z*b.z of the quad's vectors, in every lane of the quad
-__device__ __forceinline__ float qdot(float a, float b) {
-    const float m = a * b;
-    return (qb<0>(m) + qb<1>(m)) + qb<2>(m);
-}
-
-// Per lane: its component of ro and rd, and the ray's scalars (equal in the four lanes of the quad).
-struct SpreadRay {
-    float ro, rd, tr, s;
-    uint32_t n_rk, outside;
-};
-
-// One iteration (step_bf<true> contract: `out` is not written for the fates decided before the RK
-// update).  CR: the correctly rounded cores with their domain guards (`bad`, per lane: the caller
-// re-runs the iteration with CR = false when any lane of the wave raised it), else plain IEEE ops.
-template <bool CR, uint32_t SF>
-__device__ __forceinline__ bool step_spread(const MarchArgs& a, float cps_c, const SpreadRay& in, SpreadRay& out,
-                                            bool& bad, uint32_t& fate) {
-    const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
-    auto SQRT = [](float x) { if constexpr (CR) return crm::sqrt_core(x); else return __builtin_sqrtf(x); };
-    const float x = qb<0>(in.ro), y = qb<1>(in.ro), z = qb<2>(in.ro);
-    const float xx = x * x, yy = y * y, zz0 = z * z;
-    const float r2 = (xx + yy) + zz0;                                  // dot(ro, ro)
-    const float r = SQRT(r2);
-    const bool bo_on = a.blackout_eh != 0u;
-    const bool not_out = !(r2 > R2_GT1);
-    bool ingoing = false;
-    if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = qdot(in.rd, in.ro) < 0.0f;
-    const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
-    // sdf (XOps::sdf): the disc from rho^2 = x*x + z*z, the markers from the near sphere of each pair
-    const float rho2 = xx + zz0;
-    const float rho = SQRT(rho2);
-    const float disc = fmaxf(fmaxf(rho - 6.0f * a.rs, -(rho - 3.0f * a.rs)), fabsf(y - 0.0f) - 0.02f);
-    const float dz = -10.0f - z, zz = dz * dz;
-    const float ty = 10.0f - fabsf(y), tx = 10.0f - fabsf(x);
-    const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
-    const float qm = fminf(qy, qx);
-    const float m = SQRT(qm) - 0.5f;
-    const float ds = fminf((scene_flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
-                           (scene_flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
-    if constexpr (CR) {
-        if constexpr (SF == SF_DYN || SF == BH_SCENE_DEFAULT) bad |= crm::sqrt_bad2(rho2, qm);
-        else if constexpr (SF == BH_SCENE_DISC) bad |= crm::sqrt_bad(rho2);
-        else if constexpr (SF == BH_SCENE_MARKERS) bad |= crm::sqrt_bad(qm);
-    }
-    const bool surface = ds < MIN_DIST;
-    if (blackout | surface) {
-        fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
-        return true;
-    }
-    const float dc = cps_c - in.ro;                                    // sub(f.cps, ro)
-    const float qps = qdot(dc, dc);
-    const float dps = SQRT(qps) - 0.075f;
-    if constexpr (CR) bad |= crm::sqrt_bad(qps);
-    const float dist = fminf(ds, dps);
-    const float dt = fminf(dist * 0.9f, a.dtm * r);
-    const float s = in.s;
-    // rd_derivative (:125-127) at p with q = dot(p, p), sq = sqrt(q): (s * p) / ((q*q)*sq)
-    auto accel = [&](float p, float q, float sq, int K) {
-        const float Q = (q * q) * sq;
-        const float n = s * p;
-        if constexpr (CR) {
-            bad |= crm::div_d_bad(Q);
-            bad |= (K == 1) ? (crm::key(n) < crm::KEY_MIN) : !(fabsf(n) >= crm::DIV_N_MIN);
-            return crm::div_core(n, crm::rcp_refined(Q));
-        } else {
-            return n / Q;
-        }
-    };
-    const float ro_k1 = dt * in.rd;
-    const float rd_k1 = dt * accel(in.ro, r2, r, 1);
-    const float ro_k2 = dt * (in.rd + 0.5f * rd_k1);
-    const float p2 = in.ro + 0.5f * ro_k1;
-    const float q2 = qdot(p2, p2);
-    const float rd_k2 = dt * accel(p2, q2, SQRT(q2), 2);
-    const float ro_k3 = dt * (in.rd + 0.5f * rd_k2);
-    const float p3 = in.ro + 0.5f * ro_k2;
-    const float q3 = qdot(p3, p3);
-    const float rd_k3 = dt * accel(p3, q3, SQRT(q3), 3);
-    const float ro_k4 = dt * (in.rd + rd_k3);
-    const float p4 = in.ro + ro_k3;
-    const float q4 = qdot(p4, p4);
-    const float rd_k4 = dt * accel(p4, q4, SQRT(q4), 4);
-    float dro, drd;
-    if constexpr (CR) {
-        const float sro = __builtin_fmaf(2.0f, ro_k3, __builtin_fmaf(2.0f, ro_k2, ro_k1)) + ro_k4;
-        const float srd = __builtin_fmaf(2.0f, rd_k3, __builtin_fmaf(2.0f, rd_k2, rd_k1)) + rd_k4;
-        bad |= (!(fabsf(sro) >= crm::DIV_N_MIN) | !(fabsf(srd) >= crm::DIV_N_MIN)) & (dt != 0.0f);
-        bad |= !(fabsf(s) <= 0x1p30f);
-        dro = crm::div6(sro);
-        drd = crm::div6(srd);
-    } else {
-        dro = (((ro_k1 + 2.0f * ro_k2) + 2.0f * ro_k3) + ro_k4) / 6.0f;
-        drd = (((rd_k1 + 2.0f * rd_k2) + 2.0f * rd_k3) + rd_k4) / 6.0f;
-    }
-    const float ntr = in.tr + dt;
-    out.s = s;
-    out.outside = not_out ? in.outside : 1u;
-    out.ro = in.ro + dro;
-    out.rd = in.rd + drd;
-    out.tr = ntr;
-    out.n_rk = in.n_rk + 1u;
-    const bool escape = ntr > a.max_dist;
-    fate = escape ? (uint32_t)BH_FATE_ESCAPE : (uint32_t)BH_FATE_CAP;
-    return escape | (in.n_rk + 1u >= a.max_iters);
-}
-
-__device__ __forceinline__ bool same_f(float x, float y) { return __float_as_uint(x) == __float_as_uint(y); }
-
-// quad-wise AND of a lane mask: the lanes of every quad whose four lanes are all set
-__device__ __forceinline__ uint64_t quad_all(uint64_t e) {
-    e &= (e >> 1) & (e >> 2) & (e >> 3) & 0x1111111111111111ull;
-    return e | (e << 1) | (e << 2) | (e << 3);
-}
-
-// The tail of the wave's alive rays (bit i of `am`: lane i) in lane-spread form with march_cycles'
-// fast-forward; every lane of the wave must execute this (full exec).  The 16 quads march the first 16
-// rays; a quad whose ray ends takes the next one (in lane order), so any number of alive rays is
-// handled and the wave ends with its longest ray.  On return every lane holds its ray's final rd, n_rk,
-// `fate` and `steps` (what the shading and the outputs read; the other lanes' values pass through), as
-// march_cycles leaves them.  The wave's 4 KiB `H` (as 1024 floats) carries the rays to their quads and
-// back, so that no register holds the lanes' own state across the loop: [0, 640) per lane, 10 floats =
-// ro, rd, travelled, s, n_rk, outside (alive lanes; overwritten by the ray's final rd, n_rk, fate,
-// steps when it ends) or the final values (other lanes); [640, 704) ray k -> its lane; [704, 707) the
-// photon-sphere centre.  The cycle test keeps the states one and two iterations back in registers
-// (4 per lane: ro_c, rd_c, travelled, outside).
-template <uint32_t SF>
-__device__ __forceinline__ void march_spread(const MarchArgs& a, uint64_t am, RayState& st, uint32_t& fate,
-                                             uint32_t& steps, HistLds& H, uint32_t lane, const Frame& f) {
-    float* pl = reinterpret_cast<float*>(&H);
-    uint32_t* ray_lane = reinterpret_cast<uint32_t*>(pl + 640);
-    const bool alive = (am >> lane) & 1ull;
-    float* mine = pl + 10u * lane;
-    if (alive) {
-        ray_lane[__builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] = lane;
-        mine[0] = st.ro.x; mine[1] = st.ro.y; mine[2] = st.ro.z;
-        mine[3] = st.rd.x; mine[4] = st.rd.y; mine[5] = st.rd.z;
-        mine[6] = st.travelled; mine[7] = st.s;
-        mine[8] = __uint_as_float(st.n_rk); mine[9] = __uint_as_float(st.outside);
-    } else {
-        mine[0] = st.rd.x; mine[1] = st.rd.y; mine[2] = st.rd.z;
-        mine[3] = __uint_as_float(st.n_rk); mine[4] = __uint_as_float(fate); mine[5] = __uint_as_float(steps);
-    }
-    if (lane == 0u) {
-        pl[704] = f.cps.x; pl[705] = f.cps.y; pl[706] = f.cps.z;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t n = (uint32_t)__popcll(am);
-    const uint32_t q = lane >> 2, c = lane & 3u, ce = c == 3u ? 0u : c;  // lane 3 mirrors x
-    const float cps_c = pl[704u + ce];
-    bool active = q < n;
-    uint32_t next = n < SPREAD_MAX ? n : SPREAD_MAX;  // rays handed to quads so far (wave-uniform)
-    uint32_t src = 0;                                  // the lane of this quad's ray
-    SpreadRay R{}, B{}, P{};                           // current, one and two iterations back
-    auto take = [&](uint32_t k) {
-        src = ray_lane[k];
-        const float* in = pl + 10u * src;
-        R.ro = in[ce]; R.rd = in[3u + ce]; R.tr = in[6]; R.s = in[7];
-        R.n_rk = __float_as_uint(in[8]); R.outside = __float_as_uint(in[9]);
-        P = R;
-        P.tr = __uint_as_float(0xFFFFFFFFu);  // no state two back yet: a NaN pattern no arithmetic produces
-    };
-    if (active) take(q);
-    while (__builtin_amdgcn_ballot_w64(active) != 0ull) {
-        bool fin = false;
-        if (active) {
-            B = R;
-            SpreadRay N = R;
-            uint32_t fa;
-            bool bad = false;
-            bool done = step_spread<true, SF>(a, cps_c, R, N, bad, fa);
-            if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0ull, 0)) {  // rare IEEE re-run
-                bool unused = false;
-                N = R;
-                done = step_spread<false, SF>(a, cps_c, R, N, unused, fa);
-            }
-            R = N;  // == the input for the fates decided before the RK update
-            uint32_t fsteps = R.n_rk;
-            if (!done) {
-                // march_cycles' test: the state equals the one two iterations back in every lane of the quad
-                const bool eq = same_f(R.ro, P.ro) & same_f(R.rd, P.rd) & same_f(R.tr, P.tr) & (R.outside == P.outside);
-                if (__builtin_amdgcn_inverse_ballot_w64(quad_all(__builtin_amdgcn_ballot_w64(eq)))) {
-                    if ((a.max_iters - R.n_rk) & 1u) R = B;  // the cycle state of matching parity
-                    R.n_rk = a.max_iters;
-                    fa = BH_FATE_CAP;
-                    done = true;
-                }
-                P = B;
-            }
-            if (done) {
-                float* out = pl + 10u * src;
-                if (c < 3u) out[c] = R.rd;
-                if (c == 0u) {
-                    out[3] = __uint_as_float(R.n_rk);
-                    out[4] = __uint_as_float(fa);
-                    out[5] = __uint_as_float(fsteps);
-                }
-                fin = true;
-            }
-        }
-        // the quads whose ray ended take the next rays, in quad order
-        const uint64_t fq = __builtin_amdgcn_ballot_w64(fin) & 0x1111111111111111ull;
-        if (fq != 0ull) {
-            if (fin) {
-                const uint64_t below = (1ull << (4u * q)) - 1ull;
-                const uint32_t k = next + (uint32_t)__popcll(fq & below);
-                active = k < n;
-                if (active) take(k);
-            }
-            next += (uint32_t)__popcll(fq);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    st.rd = mk(mine[0], mine[1], mine[2]);
-    st.n_rk = __float_as_uint(mine[3]);
-    fate = __float_as_uint(mine[4]);
-    steps = __float_as_uint(mine[5]);
-}
-#endif
-
 // The per-frame fields of frame f of a multi-frame launch: its camera (read before and in the march
 // loop) and its outputs (read after it).
 __device__ __forceinline__ void select_camera(MarchArgs& a, const FrameArgs& F) {
@@ -1261,7 +1012,6 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     st.n_rk = 0;
     st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
-    bool alive = false;
     if (valid) {
         // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
         // writes its input, so no per-step register copies).  The lane's final state is the output
@@ -1276,7 +1026,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         // iteration.  (390 -> 370 VALU per step; with the flag template and the guard pooling
         // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
         RayState sb = st;
-        alive = true;
+        bool alive = true;
         // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
         // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
         constexpr uint32_t TRIP_PAIRS = 3;
@@ -1300,19 +1050,14 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         }
         if (sb.n_rk > st.n_rk) st = sb;
         steps = st.n_rk;
-    }
-    // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds photon-sphere rays
-    // that may run to the cap: raise its issue priority so its serial chain is not stretched by the SIMD's
-    // other waves (the frame's tail), and watch for cycles.  (Full exec here: the branch is wave-uniform.)
-    const uint64_t am = __builtin_amdgcn_ballot_w64(alive);
-    if (am != 0ull) {
-        __builtin_amdgcn_s_setprio(2);
-        __shared__ HistLds hist[BH_WG_WAVES];  // 4 KiB per wave: 8 waves per SIMD still fit (5 KiB x 32)
-#if BH_TAIL_SPREAD
-        march_spread<SF>(a, am, st, fate, steps, hist[threadIdx.x >> 6], lane, f);
-#else
-        if (alive) fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
-#endif
+        if (alive) {
+            // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
+            // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
+            // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
+            __builtin_amdgcn_s_setprio(2);
+            __shared__ HistLds hist[BH_WG_WAVES];  // 4 KiB per wave: 8 waves per SIMD still fit (5 KiB x 32)
+            fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
+        }
     }
     if (valid) {
         // the frame's output pointers are loaded here, from an opaque copy of the frame index: loaded
