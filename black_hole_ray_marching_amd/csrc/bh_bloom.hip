@@ -44,6 +44,27 @@ struct CTex {
 
 struct F4 { float r, g, b, a; };
 
+// Block coordinates with the 8 XCDs' L2s in mind.  The dispatcher hands linear workgroup b to XCD
+// b % 8, so in the raw grid neighbouring blocks -- which stage overlapping halo footprints of the same
+// texture -- run on different XCDs, and every XCD fetches its blocks' footprints through its own L2.
+// Remapped, XCD k processes the k-th eighth of the grid in row-major order (the remainder, fewer than
+// 8 blocks, keeps the raw order): adjacent blocks share an L2.  A bijection of the grid; results never
+// depend on it.  (BH_BLOOM_XCD=0 builds the raw order, for A/B.)
+#ifndef BH_BLOOM_XCD
+#define BH_BLOOM_XCD 1
+#endif
+__device__ __forceinline__ uint2 xcd_block() {
+#if BH_BLOOM_XCD
+    const uint32_t gx = gridDim.x, n = gx * gridDim.y;
+    const uint32_t b = blockIdx.y * gx + blockIdx.x, per = n >> 3;
+    const uint32_t t = b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
+    const uint32_t ty = t / gx;
+    return make_uint2(t - ty * gx, ty);
+#else
+    return make_uint2(blockIdx.x, blockIdx.y);
+#endif
+}
+
 // LDS tables of a block: sRGB decode (256), alpha decode k/255 (256), the encoder's thresholds (257)
 // and base codes (table form, bh_srgb.hpp)
 struct Lds {
@@ -225,7 +246,7 @@ __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float 
 template <int FP, bool RAW>
 __device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW>& src, const Taps&, float, float, uint32_t) {
     const TapPlan& P = *src.P;
-    const uint32_t lx = blockIdx.x * 16u + (threadIdx.x & 15u), ly = blockIdx.y * 16u + (threadIdx.x >> 4);
+    const uint32_t lx = xcd_block().x * 16u + (threadIdx.x & 15u), ly = xcd_block().y * 16u + (threadIdx.x >> 4);
     const int32_t base = ((int32_t)ly - src.y0) * FP + ((int32_t)lx - src.x0);
     F4 s{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -287,7 +308,7 @@ template <int FP, bool RAW = false, class Body>
 __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, const Taps& k, uint32_t ow,
                                             uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, const TapPlan& P,
                                             Body body) {
-    const uint32_t bx = blockIdx.x * 16u, by = blockIdx.y * 16u;
+    const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
     if (P.valid && P.hi_x - P.lo_x + 16 <= FP && P.hi_y - P.lo_y + 16 <= FP) {  // launch-uniform
         // the footprint with clamp-to-edge addressing: row r of the tile is texel row clamp(y0 + r);
         // every load of this thread first, then the decodes
@@ -370,7 +391,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
     __shared__ Lds L;
     __shared__ float4 tile[SH == SH_UP ? FP_UP * FP_UP : 1];
     load_tables(tb, L);
-    const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     if constexpr (SH == SH_UP) {
         const Taps k(rx, ry);
@@ -394,7 +415,7 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
     __shared__ Lds L;
     __shared__ float4 tile[FP_Y * FP_Y];
     load_tables(tb, L);
-    const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)Y.w), Rh = crm::rcp_refined((float)Y.h);
     const Taps k(X.w, X.h);
     with_source<FP_Y>(X, L, tile, k, Y.w, Y.h, Rw, Rh, P, [&](const auto& src) {
@@ -436,7 +457,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     __shared__ Lds L;
     __shared__ float4 tile[FP_YQ * FP_YQ];
     load_tables(tb, L);
-    const uint32_t bx = blockIdx.x * 32u, by = blockIdx.y * 32u;
+    const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;  // the footprint, clamp-to-edge
     {
         const int32_t nx = P.hi_x - P.lo_x + 32, ny = P.hi_y - P.lo_y + 32;
@@ -502,7 +523,7 @@ __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTe
     // decoded form, for a pass that mostly waits on its staging loads), else FP_FINAL^2 float4
     extern __shared__ float4 tile[];
     load_tables(tb, L);
-    const uint32_t x = blockIdx.x * 16u + (threadIdx.x & 15u), y = blockIdx.y * 16u + (threadIdx.x >> 4);
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
     with_source<FP_FINAL, true>(U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
@@ -567,7 +588,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
     __shared__ Lds L;
     __shared__ float4 tile[FP_UPQ * FP_UPQ];
     load_tables(tb, L);
-    const uint32_t bx = blockIdx.x * 32u, by = blockIdx.y * 32u;
+    const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
