@@ -772,6 +772,87 @@ __device__ __forceinline__ v3 shade(const MarchArgs& a, const float* lut, uint32
     return col;
 }
 
+#ifndef BH_SKY_LDS
+#define BH_SKY_LDS 0
+#endif
+#if BH_SKY_LDS && !BH_FAST
+// A/B variant (north_star's "sky texture tile-staged through LDS"): shade() for a whole
+// tile wave, whose rays' bilinear footprints usually fall in a few texels of the sky.  When every sky
+// lane's 2x2 footprint lies in the 8x8 texel box around the first sky lane's, the wave stages that box
+// into LDS (one texel per lane, the wave's 4 KiB history area, free after the march) and each lane reads
+// its four texels from there; otherwise (and in partial tiles) the texels come from global memory as in
+// sample_sky.  The decode and lerps are sample_sky's, so the bits are the same.  Full exec required.
+__device__ __forceinline__ v3 shade_tile(const MarchArgs& a, const float* lut, uint32_t fate, v3 rd, uint32_t* S,
+                                         uint32_t lane) {
+    const bool sky = (fate != BH_FATE_BLACKOUT) & (fate != BH_FATE_SURFACE);
+    float u = 0.0f, v = 0.0f;
+    if (sky) {
+        const v3 n = normalize_x(rd);
+        const crm::Atan2 at = crm::atan2_core(n.z, n.x);
+        float az = at.f;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(at.near) != 0ull, 0)) {
+            if (at.near) az = (float)atan2((double)n.z, (double)n.x);
+        }
+        u = crm::div_core(az + ONE_PI, crm::Rcp{TWO_PI, 1.0f / TWO_PI});
+        v = 1.0f - (n.y + 1.0f) * 0.5f;
+    }
+    const bool nan = (u != u) | (v != v);  // Q8: texel (0, 0)
+    float tx = u * (float)a.sky_w - 0.5f;
+    float ty = v * (float)a.sky_h - 0.5f;
+    tx = fminf(fmaxf(tx, -1.0f), (float)a.sky_w);
+    ty = fminf(fmaxf(ty, -1.0f), (float)a.sky_h);
+    const float fx0 = floorf(tx), fy0 = floorf(ty);
+    const float fa = tx - fx0, fb = ty - fy0;
+    const int32_t wm = (int32_t)a.sky_w - 1, hm = (int32_t)a.sky_h - 1;
+    int32_t x0 = (int32_t)fx0, y0 = (int32_t)fy0;
+    int32_t x1 = clampi(x0 + 1, 0, wm), y1 = clampi(y0 + 1, 0, hm);
+    x0 = clampi(x0, 0, wm);
+    y0 = clampi(y0, 0, hm);
+    if (nan) { x0 = x1 = 0; y0 = y1 = 0; }
+    const bool need = sky;
+    bool staged = false;
+    int32_t bx = 0, by = 0;
+    if (__builtin_amdgcn_read_exec() == ~0ull) {  // a full tile wave (wave-uniform)
+        const uint64_t nm = __builtin_amdgcn_ballot_w64(need);
+        if (nm != 0ull) {
+            const int lead = __builtin_ctzll(nm);
+            bx = __builtin_amdgcn_readlane(x0, lead) - 3;
+            by = __builtin_amdgcn_readlane(y0, lead) - 3;
+            const bool in = !need | ((x0 >= bx) & (x1 <= bx + 7) & (y0 >= by) & (y1 <= by + 7));
+            if (__builtin_amdgcn_ballot_w64(!in) == 0ull) {
+                const int32_t sx = clampi(bx + (int32_t)(lane & 7u), 0, wm), sy = clampi(by + (int32_t)(lane >> 3), 0, hm);
+                S[lane] = a.sky[(size_t)sy * a.sky_w + (size_t)sx];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                staged = true;
+            }
+        }
+    }
+    if (!sky) return fate == BH_FATE_SURFACE ? mk(1.0f, 1.0f, 1.0f) : mk(0.0f, 0.0f, 0.0f);
+    uint32_t w00, w10, w01, w11;
+    if (staged) {
+        const int32_t o = (y0 - by) * 8 + (x0 - bx), dx = x1 - x0, dy = (y1 - y0) * 8;
+        w00 = S[o]; w10 = S[o + dx]; w01 = S[o + dy]; w11 = S[o + dy + dx];
+    } else {
+        w00 = texel_u32(a, x0, y0); w10 = texel_u32(a, x1, y0); w01 = texel_u32(a, x0, y1); w11 = texel_u32(a, x1, y1);
+    }
+    v3 col;
+    if (nan) {
+        col = decode(lut, w00);
+    } else {
+        const v3 t00 = decode(lut, w00), t10 = decode(lut, w10), t01 = decode(lut, w01), t11 = decode(lut, w11);
+        const float ia = 1.0f - fa, ib = 1.0f - fb;
+        const v3 top = add(muls(t00, ia), muls(t10, fa));
+        const v3 bot = add(muls(t01, ia), muls(t11, fa));
+        col = add(muls(top, ib), muls(bot, fb));
+    }
+    col.y = pow15_x(col.y);
+    col.z = pow15_x(col.z);
+    return col;
+}
+#endif
+
 // Output texel store; the format is a template parameter (one kernel instantiation per format keeps
 // the BGRA8 encoder out of the other formats' code: it measured 1.8 % on the RGBA16F kernel).
 template <uint32_t FMT>
@@ -926,6 +1007,13 @@ __device__ __forceinline__ uint32_t state_hash(const RayState& st) {
             __float_as_uint(st.rd.x) ^ __float_as_uint(st.rd.y) ^ __float_as_uint(st.rd.z) ^
             __float_as_uint(st.travelled)) + st.outside * 0x9E3779B9u;
 }
+// The workgroup's history areas (4 KiB per wave: 8 waves per SIMD still fit, 5 KiB x 32).
+template <int>
+__device__ __forceinline__ HistLds* hist_lds() {
+    __shared__ HistLds hist[BH_WG_WAVES];
+    return hist;
+}
+
 // March `st` to termination with the fast-forward; `steps` = RK updates actually executed.
 // (The tail waves are latency-bound: a ping-pong / uniform-trip form of this loop measured slower.)
 template <uint32_t SF>
@@ -1055,8 +1143,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
             // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
             // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
             __builtin_amdgcn_s_setprio(2);
-            __shared__ HistLds hist[BH_WG_WAVES];  // 4 KiB per wave: 8 waves per SIMD still fit (5 KiB x 32)
-            fate = march_cycles<SF>(a, f, st, steps, hist[threadIdx.x >> 6], lane);
+            fate = march_cycles<SF>(a, f, st, steps, hist_lds<0>()[threadIdx.x >> 6], lane);
         }
     }
     if (valid) {
@@ -1067,7 +1154,12 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         asm volatile("" : "+s"(fo));
         if (A.frame_table) select_outputs(a, A.frame_table[fo]);
         else select_outputs(a, A.frames[fo]);
-        write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), shade(a, lut, fate, st.rd), st.n_rk, fate, steps);
+#if BH_SKY_LDS && !BH_FAST
+        const v3 col = shade_tile(a, lut, fate, st.rd, reinterpret_cast<uint32_t*>(&hist_lds<0>()[threadIdx.x >> 6]), lane);
+#else
+        const v3 col = shade(a, lut, fate, st.rd);
+#endif
+        write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), col, st.n_rk, fate, steps);
     }
     if (a.tile_cost) {
         // the next frame's cost and its bucket histogram (a no-return atomic: the wave does not wait);
