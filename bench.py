@@ -97,9 +97,11 @@ def parse(argv=None):
                    help="N>1: rank 0 compares both assembled targets with its own full-frame render (bitwise)")
     p.add_argument("--frames-per-launch", type=int, default=0,
                    help="frames rendered by one bh_render_frames launch (1..256; 0 = auto, DESIGN.md §5 item 9)")
-    p.add_argument("--root-ratio", default="auto",
-                   help="N>1: rank 0's tile share relative to each other rank's (it also unpacks every frame): "
-                        "'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain (tx + 3ty) %% N interleave")
+    p.add_argument("--root-ratio", default="calibrate",
+                   help="N>1: rank 0's tile share relative to each other rank's (it also unpacks every frame, and its "
+                        "own tiles cross no link): 'calibrate' (default: the fastest of a few candidates, measured "
+                        "before the warm-up), 'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain "
+                        "(tx + 3ty) %% N interleave")
     p.add_argument("--plumbing", action="store_true",
                    help="no GPU: the N-rank launch, gather pipeline and RGBM unpack on CPU (gloo) with "
                         "synthetic shards (tests only; prints no measurement)")
@@ -170,7 +172,8 @@ def root_weights(args, n: int):
     if n == 1:
         return None
     from black_hole_ray_marching_amd import multigpu
-    ratio = multigpu.auto_root_ratio(n) if args.root_ratio == "auto" else float(args.root_ratio)
+    # 'calibrate' measures (bench main); without a GPU (plumbing) it falls back to the model's ratio
+    ratio = multigpu.auto_root_ratio(n) if args.root_ratio in ("auto", "calibrate") else float(args.root_ratio)
     w = multigpu.root_weights(n, ratio)
     return None if len(set(w)) == 1 else w
 
@@ -352,6 +355,7 @@ def main() -> int:
     if not 1 <= D <= bh.BH_MAX_FRAMES:
         raise SystemExit(f"--frames-per-launch must be 1..{bh.BH_MAX_FRAMES}")
     weights = None
+    calibration = None
     if not sharded:
         cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
         bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)]
@@ -359,38 +363,85 @@ def main() -> int:
         my_tiles = ((W + 7) // 8) * ((H + 7) // 8)
         my_bytes = W * H * bpp * 2
         pipe = None
+        batches = [scene.prepare_frames(cols, bos, fmt=fmt, schedule=sched, **shard)]
     else:
-        # each rank renders its (tx + 3ty) % n tiles of D frames per launch, col only (blackout target
-        # None == Option::None: its per-pixel decision travels as the RGBM mask), into one packed
-        # buffer; launch i's gather to rank 0 (all D frames in one collective) overlaps launch i+1's
-        # render; rank 0 unpacks every frame's col and blackout_col on a side stream
-        weights = root_weights(args, n)
-        part = bh.Partition(W, H, weights, device=local) if weights else None
-        stride = max(part.counts) if part else multigpu.packed_stride(W, H, n)
         tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
-        my_tiles = part.counts[rank] if part else bh.shard_tile_count(W, H, rank, n)
-        my_bytes = my_tiles * tb + (2 * W * H * bpp if rank == 0 else 0)
         frame_cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         frame_bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
-        shard = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=rank, shard_count=n)
-        if part:
-            shard["partition"] = part
-        launch_frames = {}
+        side = torch.cuda.Stream(dev)
 
-        def on_frame(i, gathered):  # issued on the pipeline's side stream (current stream here)
-            # gathered: (n * D * stride, tb), rank k's block of D frames at k * D * stride
-            for f in range(launch_frames.pop(i)):
-                if part:
-                    bh.tiles_unpack_rgbm_partition(gathered[f * stride:], frame_cols[f], frame_bos[f], part, D * stride,
-                                                   fmt, stream=torch.cuda.current_stream(dev),
-                                                   rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
-                else:
-                    bh.tiles_unpack_rgbm(gathered[f * stride:], frame_cols[f], frame_bos[f], W, H, n, D * stride, fmt,
-                                         stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+        class Rig:
+            """The N>1 data path for one tile partition: each rank renders its share of the batch's D
+            frames, col only (blackout target None == Option::None: its per-pixel decision travels as the
+            RGBM mask), into one packed buffer; batch i's gather to rank 0 (all D frames in one collective)
+            overlaps batch i+1's render; rank 0 unpacks every frame's col and blackout_col on a side stream."""
 
-        pipe = multigpu.GatherPipeline(lambda: torch.empty((D * stride, tb), dtype=torch.uint8, device=dev),
-                                       rank, n, on_frame, side_stream=torch.cuda.Stream(dev),
-                                       collective=True if args.rccl_dry_run else None, timing=True)
+            def __init__(self, weights):
+                self.weights = weights
+                self.part = bh.Partition(W, H, weights, device=local) if weights else None
+                self.stride = max(self.part.counts) if self.part else multigpu.packed_stride(W, H, n)
+                self.my_tiles = self.part.counts[rank] if self.part else bh.shard_tile_count(W, H, rank, n)
+                self.shard = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=rank, shard_count=n)
+                if self.part:
+                    self.shard["partition"] = self.part
+                self.launch_frames = {}
+                self.pipe = multigpu.GatherPipeline(
+                    lambda: torch.empty((D * self.stride, tb), dtype=torch.uint8, device=dev), rank, n, self.on_frame,
+                    side_stream=side, collective=True if args.rccl_dry_run else None, timing=True)
+                self.batches = [scene.prepare_frames([buf[f * self.stride:(f + 1) * self.stride] for f in range(D)],
+                                                     None, fmt=fmt, schedule=sched, **self.shard)
+                                for buf in (self.pipe.buffer(k) for k in range(self.pipe.depth))]
+
+            def on_frame(self, i, gathered):  # issued on the pipeline's side stream (current stream here)
+                # gathered: (n * D * stride, tb), rank k's block of D frames at k * D * stride
+                st = self.stride
+                for f in range(self.launch_frames.pop(i)):
+                    if self.part:
+                        bh.tiles_unpack_rgbm_partition(gathered[f * st:], frame_cols[f], frame_bos[f], self.part, D * st,
+                                                       fmt, stream=torch.cuda.current_stream(dev),
+                                                       rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+                    else:
+                        bh.tiles_unpack_rgbm(gathered[f * st:], frame_cols[f], frame_bos[f], W, H, n, D * st, fmt,
+                                             stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
+
+            def step(self, k):  # one untimed batch (render + exchange), k = its pipeline index
+                self.batches[k % len(self.batches)].render(n=D, stream=stream)
+                self.launch_frames[k] = D
+                self.pipe.submit(k)
+
+        if args.root_ratio == "calibrate" and n > 1:
+            # rank 0's share, measured (DESIGN.md §7): the batch time of a few candidate partitions --
+            # rank 0 renders less when its unpack binds, more when the xGMI ingress of the others' shards
+            # binds (its own tiles cross no link) -- untimed, before the warm-up; every rank takes rank 0's pick
+            ratios = sorted({round(multigpu.auto_root_ratio(n), 3), 0.9, 1.0, 1.15, 1.3})
+            ms = []
+            for r in ratios:
+                rig = Rig(multigpu.root_weights(n, r) if r != 1.0 else None)
+                for k in range(CALIBRATE_WARM):
+                    rig.step(k)
+                rig.pipe.drain()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                t_c = time.perf_counter()
+                for k in range(CALIBRATE_WARM, CALIBRATE_WARM + CALIBRATE_STEPS):
+                    rig.step(k)
+                rig.pipe.drain()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                ms.append((time.perf_counter() - t_c) / CALIBRATE_STEPS * 1e3)
+                del rig
+            pick = [ratios[int(np.argmin(ms))]]
+            dist.broadcast_object_list(pick, src=0)
+            weights = multigpu.root_weights(n, pick[0]) if pick[0] != 1.0 else None
+            calibration = {"root_ratios": ratios, "ms_per_batch": [round(x, 4) for x in ms], "chosen": pick[0],
+                           "batches_each": f"{CALIBRATE_WARM} warm + {CALIBRATE_STEPS} timed (untimed for value)"}
+        else:
+            weights = root_weights(args, n)
+        rig = Rig(weights)
+        part, stride, shard, pipe, batches = rig.part, rig.stride, rig.shard, rig.pipe, rig.batches
+        launch_frames = rig.launch_frames
+        my_tiles = rig.my_tiles
+        my_bytes = my_tiles * tb + (2 * W * H * bpp if rank == 0 else 0)
 
     launch_no = [0]
     frame_no = [0]   # frames launched so far (the orbit path's frame index)
@@ -400,15 +451,6 @@ def main() -> int:
         if (path or args.camera_path) == "fixed":
             return None
         return [orbit[frame_no[0] + f] for f in range(nf)]
-
-    # the timed launches' bh_render_frames calls, prepared once (Scene.prepare_frames): one per pipeline
-    # slot for N > 1 (the slot's packed buffer), else one over cols / bos
-    if pipe is None:
-        batches = [scene.prepare_frames(cols, bos, fmt=fmt, schedule=sched, **shard)]
-    else:
-        batches = [scene.prepare_frames([buf[f * stride:(f + 1) * stride] for f in range(D)], None, fmt=fmt,
-                                        schedule=sched, **shard)
-                   for buf in (pipe.buffer(k) for k in range(pipe.depth))]
 
     def launch(nf, path=None, **kw):
         """One bh_render_frames launch of nf <= D frames (this scene's camera, or the orbit path's); with
@@ -680,6 +722,7 @@ def main() -> int:
             result["backend"] = dist.get_backend()
             result["per_rank_s"] = [round(x, 6) for x in per_rank]
             result["ranks"] = ranks
+            result["partition_calibration"] = calibration
         if args.no_cpu or sharded:
             result["cpu_baseline"] = None
         else:
@@ -697,6 +740,7 @@ def main() -> int:
 EXTRA_SINGLE_FRAMES = 24
 EXTRA_ORBIT_LAUNCHES = 4
 CLOCK_STRIDE = 256   # every 256th wave of a march launch samples the shader clock
+CALIBRATE_WARM, CALIBRATE_STEPS = 2, 3   # batches per candidate partition of --root-ratio calibrate
 PEAK_MHZ = 2400.0    # the shader clock behind the 157.3 TFLOP/s FP32 peak (1024 SIMDs x 32 lanes x 2 x 2.4 GHz)
 
 
