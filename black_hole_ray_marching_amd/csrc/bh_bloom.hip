@@ -65,24 +65,38 @@ __device__ __forceinline__ uint2 xcd_block() {
 #endif
 }
 
-// LDS tables of a block: sRGB decode (256), alpha decode k/255 (256), the encoder's thresholds (257)
-// and base codes (table form, bh_srgb.hpp)
+// LDS tables of a block: sRGB decode (256), alpha decode k/255 (256) and the encoder: its thresholds
+// (257) and base codes (table form), or (BH_BLOOM_ETAB) its code table (one read per channel instead of
+// two dependent ones; bh_srgb.hpp)
+#ifndef BH_BLOOM_ETAB
+#define BH_BLOOM_ETAB 0
+#endif
 struct Lds {
-    float lut[256], alut[256], T[SRGB_TABLE];
+    float lut[256], alut[256];
+#if BH_BLOOM_ETAB
+    uint32_t E[SRGB_CODES];
+#else
+    float T[SRGB_TABLE];
     uint32_t B32[SRGB_BUCKETS / 4];
+#endif
 };
 struct Tables {
     const float* lut;      // 256
     const float* enc;      // 257
     const uint8_t* bkt;    // SRGB_BUCKETS
+    const uint32_t* code;  // SRGB_CODES
 };
 __device__ __forceinline__ void load_tables(Tables tb, Lds& L) {
     L.lut[threadIdx.x] = tb.lut[threadIdx.x];
     L.alut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+#if BH_BLOOM_ETAB
+    for (uint32_t i = threadIdx.x; i < (uint32_t)SRGB_CODES; i += 256) L.E[i] = tb.code[i];
+#else
     L.T[threadIdx.x] = tb.enc[threadIdx.x];
     if (threadIdx.x == 0) L.T[256] = tb.enc[256];
     const uint32_t* b = reinterpret_cast<const uint32_t*>(tb.bkt);
     for (uint32_t i = threadIdx.x; i < SRGB_BUCKETS / 4; i += 256) L.B32[i] = b[i];
+#endif
     __syncthreads();
 }
 
@@ -98,9 +112,14 @@ __device__ __forceinline__ uint32_t unorm8(float a) {
 }
 // the Bgra8UnormSrgb store of a pass's result
 __device__ __forceinline__ uint32_t enc(const Lds& L, F4 c) {
+#if BH_BLOOM_ETAB
+    return srgb_encode_code(c.b, L.E) | (srgb_encode_code(c.g, L.E) << 8) | (srgb_encode_code(c.r, L.E) << 16) |
+           (unorm8(c.a) << 24);
+#else
     const uint8_t* B = reinterpret_cast<const uint8_t*>(L.B32);
     return srgb_encode_lut(c.b, B, L.T) | (srgb_encode_lut(c.g, B, L.T) << 8) | (srgb_encode_lut(c.r, B, L.T) << 16) |
            (unorm8(c.a) << 24);
+#endif
 }
 __device__ __forceinline__ F4 quant(const Lds& L, F4 c) { return dec(L, enc(L, c)); }
 
@@ -826,11 +845,11 @@ extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(ui
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32_t shader, const float* lut,
                                                                          const float* enc, const uint8_t* buckets,
-                                                                         const uint32_t* a,
+                                                                         const uint32_t* codes, const uint32_t* a,
                                                                          uint32_t aw, uint32_t ah, const uint32_t* b,
                                                                          uint32_t rx, uint32_t ry, uint32_t* out,
                                                                          uint32_t ow, uint32_t oh, hipStream_t s) {
-    const Tables tb{lut, enc, buckets};
+    const Tables tb{lut, enc, buckets, codes};
     const CTex A{a, aw, ah}, B{b ? b : a, aw, ah};
     const Tex O{out, ow, oh};
     const TapPlan P = shader == SH_UP ? tap_plan(ow, oh, aw, ah, rx, ry) : TapPlan{};
@@ -853,23 +872,25 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
 }
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
-                                                                      const uint8_t* buckets, const uint32_t* X, uint32_t* Y, uint32_t w,
+                                                                      const uint8_t* buckets, const uint32_t* codes,
+                                                                      const uint32_t* X, uint32_t* Y, uint32_t w,
                                                                       uint32_t h, hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, w, h);
     static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
     if (P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ) {
         hipLaunchKernelGGL(bloom_yq_kernel, dim3((w + 31u) / 32u, (h + 31u) / 32u), dim3(256), 0, s,
-                           Tables{lut, enc, buckets}, CTex{X, w, h}, P, Tex{Y, w, h});
+                           Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P, Tex{Y, w, h});
         return (int)hipGetLastError();
     }
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, w, h);
-    hipLaunchKernelGGL(bloom_y_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets}, CTex{X, w, h}, pm, P,
+    hipLaunchKernelGGL(bloom_y_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, pm, P,
                        Tex{Y, w, h});
     return (int)hipGetLastError();
 }
 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const float* lut, const float* enc,
-                                                                          const uint8_t* buckets, const uint32_t* col, const uint32_t* Y,
+                                                                          const uint8_t* buckets, const uint32_t* codes,
+                                                                          const uint32_t* col, const uint32_t* Y,
                                                                           const uint32_t* U0, uint32_t rx, uint32_t ry,
                                                                           uint32_t* out, uint32_t w, uint32_t h,
                                                                           hipStream_t s) {
@@ -878,7 +899,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
     // the kernel's with_source takes the TapPlan form exactly when this holds (raw words staged)
     const bool plan = P.valid && P.hi_x - P.lo_x + 16 <= FP_FINAL && P.hi_y - P.lo_y + 16 <= FP_FINAL;
     const size_t lds = (size_t)FP_FINAL * FP_FINAL * (plan ? sizeof(uint32_t) : sizeof(float4));
-    hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets}, CTex{col, w, h},
+    hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets, codes}, CTex{col, w, h},
                        CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
     return (int)hipGetLastError();
 }

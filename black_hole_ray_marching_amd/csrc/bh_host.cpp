@@ -23,6 +23,7 @@ struct bh_ctx {
     float* lut = nullptr;          // device sRGB->linear table (256 floats)
     float* enc = nullptr;          // device linear->sRGB threshold table (257 floats)
     uint8_t* enc_b = nullptr;      // device base codes of the table-form encoder (SRGB_BUCKETS bytes)
+    uint32_t* enc_e = nullptr;     // device code table of the code-table encoder (SRGB_CODES words)
     uint32_t* counters = nullptr;  // persistent-schedule work counters (1 KiB, zeroed per launch)
     uint32_t sky_w = 0, sky_h = 0;
     uint32_t grid_exact = 0, grid_fast = 0;  // resident blocks of the persistent kernels
@@ -152,6 +153,33 @@ void srgb_encode_table(float T[257]) {
 }
 
 }  // namespace
+
+// The code-table form of the encoder (bh_srgb.hpp srgb_encode_code): false if a bucket held two thresholds
+// (never, for the normative table: the form would not be exact).
+extern "C" __attribute__((visibility("hidden"))) bool bh_srgb_code_table(const float* T, uint32_t* E) {
+    bool ok = true;
+    for (int i = 0; i < bh::SRGB_CODES; ++i) {
+        const uint32_t hi = (bh::SRGB_BUCKET_BASE + (uint32_t)i) << bh::SRGB_BUCKET_SHIFT;
+        float lo;
+        std::memcpy(&lo, &hi, 4);
+        int k = 0;  // code of the bucket's lower end
+        while (k < 255 && lo >= T[k + 1]) ++k;
+        uint32_t thr = 0x10000u;
+        if (k < 255) {
+            uint32_t tb;
+            std::memcpy(&tb, &T[k + 1], 4);
+            if ((tb >> 16) == (hi >> 16)) {
+                thr = tb & 0xFFFFu;
+                uint32_t t2 = 0;
+                if (k < 254) std::memcpy(&t2, &T[k + 2], 4);
+                if (k < 254 && (t2 >> 16) == (hi >> 16)) ok = false;
+            }
+        }
+        if (i == 0 && thr != 0x10000u) ok = false;  // values below 2^-13 clamp to entry 0
+        E[i] = (uint32_t)k | (thr << 15);
+    }
+    return ok;
+}
 
 extern "C" __attribute__((visibility("hidden"))) void bh_srgb_bucket_table(const float* T, uint8_t* B) {
     for (int i = 0; i < bh::SRGB_BUCKETS; ++i) {
@@ -458,9 +486,15 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     const size_t bytes = (size_t)sky_w * sky_h * 4u;
     float lut[256], enc[257];
     uint8_t enc_b[bh::SRGB_BUCKETS];
+    uint32_t enc_e[bh::SRGB_CODES];
     srgb_lut(lut);
     srgb_encode_table(enc);
     bh_srgb_bucket_table(enc, enc_b);
+    if (!bh_srgb_code_table(enc, enc_e)) {
+        g_last_error = "sRGB code table";
+        delete c;
+        return BH_ERR_UNSUPPORTED;
+    }
     int st = BH_OK;
     if ((e = hipMalloc(&c->sky, bytes)) != hipSuccess) st = (e == hipErrorOutOfMemory) ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "hipMalloc(sky)");
     else if ((e = hipMalloc(&c->lut, sizeof(lut))) != hipSuccess) st = hip_fail(e, "hipMalloc(lut)");
@@ -470,6 +504,8 @@ int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh
     else if ((e = hipMemcpy(c->enc, enc, sizeof(enc), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc)");
     else if ((e = hipMalloc(&c->enc_b, sizeof(enc_b))) != hipSuccess) st = hip_fail(e, "hipMalloc(enc_b)");
     else if ((e = hipMemcpy(c->enc_b, enc_b, sizeof(enc_b), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc_b)");
+    else if ((e = hipMalloc(&c->enc_e, sizeof(enc_e))) != hipSuccess) st = hip_fail(e, "hipMalloc(enc_e)");
+    else if ((e = hipMemcpy(c->enc_e, enc_e, sizeof(enc_e), hipMemcpyHostToDevice)) != hipSuccess) st = hip_fail(e, "hipMemcpy(enc_e)");
     else if ((e = hipMalloc(&c->counters, 1024)) != hipSuccess) st = hip_fail(e, "hipMalloc(counters)");
     if (st == BH_OK) {
         int cus = 0;
@@ -493,6 +529,7 @@ int bh_destroy(bh_ctx* c) {
     if (c->lut) (void)hipFree(c->lut);
     if (c->enc) (void)hipFree(c->enc);
     if (c->enc_b) (void)hipFree(c->enc_b);
+    if (c->enc_e) (void)hipFree(c->enc_e);
     if (c->counters) (void)hipFree(c->counters);
     for (auto& o : c->orders) {
         if (o.tile_cost) (void)hipFree(o.tile_cost);
@@ -547,7 +584,7 @@ struct BloomRun {
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
         if (err == 0)
-            err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, a, aw, ah, b, res[0], res[1], out, ow, oh, s);
+            err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh, s);
     }
 };
 
@@ -603,7 +640,7 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         // same-size passes are identities (same_size_exact): see bh_bloom.hip
         const uint32_t* S = X;
         if (levels > 1) {
-            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, X, copy_in[1], W, H, s);
+            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
             S = copy_in[1];
         }
         const uint32_t* dn = S;  // down[0] == S
@@ -620,7 +657,7 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
             u_src = up[ti];
         }
         if (R.err == 0)
-            R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
+            R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, c->enc_e, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
     } else {
         // literal: the reference's render passes in order (oracle/bh_bloom_oracle.c, bho_bloom)
         if ((e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)

@@ -33,6 +33,7 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 3: div_core with n = d * m for random small integers m (exact quotients) and n = d*q +- ulps
 // op 4: srgb_encode over every 32-bit pattern in [base, base + count) against a binary search of T
 // op 6: srgb_encode_lut (table form) against srgb_encode over every 32-bit pattern in [base, base + count)
+// op 10: srgb_encode_code (code-table form) against srgb_encode over every 32-bit pattern in [base, base + count)
 // op 5: div12 over every 32-bit pattern in [base, base + count) whose magnitude passes the key guard
 // op 8: atan2_core (+ its library fallback where flagged) against (float)atan2((double)y, (double)x) on
 //       `count` random (y, x) pairs seeded by base: random directions, random magnitudes, and the
@@ -43,7 +44,7 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 //       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
 __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, uint64_t count,
                                                       unsigned long long* cnt, uint32_t* ex, const float* T,
-                                                      const uint8_t* B) {
+                                                      const uint8_t* B, const uint32_t* E) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         if (op == 0) {
@@ -73,6 +74,11 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             const uint32_t bits = (uint32_t)(base + i);
             const float x = __uint_as_float(bits);
             const uint32_t got = srgb_encode_lut(x, B, T), want = srgb_encode(x, T);  // op 4 pins srgb_encode
+            if (got != want) record(cnt, ex, bits, 0, got, want);
+        } else if (op == 10) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float x = __uint_as_float(bits);
+            const uint32_t got = srgb_encode_code(x, E), want = srgb_encode(x, T);  // op 4 pins srgb_encode
             if (got != want) record(cnt, ex, bits, 0, got, want);
         } else if (op == 4) {
             const uint32_t bits = (uint32_t)(base + i);
@@ -143,7 +149,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 9 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 10 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;
@@ -151,32 +157,38 @@ extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_
     uint32_t* ex = nullptr;
     float* T = nullptr;
     uint8_t* Bd = nullptr;
+    uint32_t* Ed = nullptr;
     float table[bh::SRGB_TABLE];
     uint8_t btab[bh::SRGB_BUCKETS];
+    uint32_t etab[bh::SRGB_CODES];
     (void)bh_srgb_encode_table(table);
     bh_srgb_bucket_table(table, btab);
+    const bool etab_ok = bh_srgb_code_table(table, etab);
     int st = BH_OK;
     if (hipMalloc(&cnt, sizeof(*cnt)) != hipSuccess || hipMalloc(&ex, 8 * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&T, sizeof(table)) != hipSuccess || hipMalloc(&Bd, sizeof(btab)) != hipSuccess) {
+        hipMalloc(&T, sizeof(table)) != hipSuccess || hipMalloc(&Bd, sizeof(btab)) != hipSuccess ||
+        hipMalloc(&Ed, sizeof(etab)) != hipSuccess) {
         st = BH_ERR_OUT_OF_MEMORY;
     } else {
         (void)hipMemset(cnt, 0, sizeof(*cnt));
         (void)hipMemset(ex, 0, 8 * sizeof(uint32_t));
         (void)hipMemcpy(T, table, sizeof(table), hipMemcpyHostToDevice);
         (void)hipMemcpy(Bd, btab, sizeof(btab), hipMemcpyHostToDevice);
+        (void)hipMemcpy(Ed, etab, sizeof(etab), hipMemcpyHostToDevice);
         int cus = 256;
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex, T, Bd);
+        hipLaunchKernelGGL(bh::selftest_kernel, dim3(cus * 8), dim3(256), 0, 0, op, base, count, cnt, ex, T, Bd, Ed);
         if (hipDeviceSynchronize() != hipSuccess) st = BH_ERR_HIP;
         unsigned long long h = 0;
         (void)hipMemcpy(&h, cnt, sizeof(h), hipMemcpyDeviceToHost);
-        *out_mismatches = h;
+        *out_mismatches = h + ((op == 10 && !etab_ok) ? 1u : 0u);
         if (out_examples) (void)hipMemcpy(out_examples, ex, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost);
     }
     if (cnt) (void)hipFree(cnt);
     if (ex) (void)hipFree(ex);
     if (T) (void)hipFree(T);
     if (Bd) (void)hipFree(Bd);
+    if (Ed) (void)hipFree(Ed);
     (void)hipSetDevice(prev);
     return st;
 }

@@ -43,6 +43,22 @@ __device__ __forceinline__ uint32_t srgb_encode_lut(float x, const uint8_t* B, c
     return c + (xc >= T[c + 1] ? 1u : 0u);
 }
 
+// Code-table form (one LDS read instead of two dependent ones): within a bucket every float shares its
+// upper 16 bits, so the one threshold a bucket may hold is fixed by its low 16 bits.  Entry i =
+// base code | thr17 << 15, thr17 = the threshold's low 16 bits, or 0x10000 (never reached) when the
+// bucket holds none: code = base + (low16(x) >= thr17).  Entry SRGB_BUCKETS is 1.0 (code 255); values
+// below 2^-13 clamp to entry 0, which holds no threshold (T[1] > 2^-13 * (1 + 2^-7)).  Built by the host
+// (bh_host.cpp, bh_srgb_code_table); exhaustively checked on the device (bh_selftest_crmath op 10).
+constexpr int SRGB_CODES = SRGB_BUCKETS + 1;
+__device__ __forceinline__ uint32_t srgb_encode_code(float x, const uint32_t* E) {
+    const float xc = fminf(fmaxf(x, 0.0f), 1.0f);  // fmaxf(NaN, 0) = 0
+    const uint32_t b = __float_as_uint(xc);
+    int32_t i = (int32_t)(b >> SRGB_BUCKET_SHIFT) - (int32_t)SRGB_BUCKET_BASE;
+    i = i < 0 ? 0 : (i > SRGB_BUCKETS ? SRGB_BUCKETS : i);
+    const uint32_t e = E[i];
+    return (e & 0xFFu) + ((b & 0xFFFFu) >= (e >> 15) ? 1u : 0u);
+}
+
 // BGRA8 texel (byte 0 = B) of linear rgb, alpha 1.
 __device__ __forceinline__ uint32_t srgb_bgra8(float r, float g, float b, const float* T) {
     return srgb_encode(b, T) | (srgb_encode(g, T) << 8) | (srgb_encode(r, T) << 16) | 0xFF000000u;

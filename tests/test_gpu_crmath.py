@@ -77,6 +77,13 @@ def test_srgb_encode_table_form_exhaustive(lib):
     assert m == 0, ex
 
 
+def test_srgb_encode_code_table_form_exhaustive(lib):
+    # the code-table form (one read per channel: base code | the bucket's threshold low bits) over all 2^32
+    # patterns; a bucket holding two thresholds would also count as a mismatch
+    m, ex = run(lib, 10, 0, 1 << 32)
+    assert m == 0, ex
+
+
 def test_atan2_core_against_the_library(lib):
     """The shading's f32-rounded atan2 (bh_crmath.hpp atan2_core + the library fallback where it flags a
     near-midpoint angle) equals (float)atan2((double)y, (double)x) on 2^29 pairs: unit vectors as the
