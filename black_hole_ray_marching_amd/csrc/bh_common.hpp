@@ -51,6 +51,9 @@ struct MarchArgs {
     // oracle: photon-sphere centre -normalize(ro0) * 1.5 * RS (:294) and (DP * RS) * -1.5 (:126)
     float cps[3];
     float kfac;
+    // RN(1 / (2W)) and RN(1 / (2H)): the reciprocals of vs_main's interpolation denominators (IEEE on the
+    // host; equal to crm::rcp_refined of 2W, 2H, which is RN(1/d) for every normal d)
+    float rw2, rh2;
     // sky (Rgba8UnormSrgb texels as packed u32, little endian: r | g<<8 | b<<16 | a<<24)
     const uint32_t* sky;
     const float* srgb_lut;     // 256 entries, sRGB byte -> linear

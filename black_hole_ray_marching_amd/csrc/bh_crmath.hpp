@@ -130,9 +130,16 @@ __device__ __forceinline__ Atan2 atan2_core(float yf, float xf) {
     double u = num * r;
     u = __builtin_fma(__builtin_fma(-den, u, num), r, u);
     const double s = u * u;
+    // Horner with each coefficient an SGPR-pair operand of v_fma_f64 (two s_mov_b32 on the scalar unit):
+    // the compiler's own form, v_fmac_f64 with the coefficient first moved into the accumulator's VGPR
+    // pair, issues 20 more VALU instructions per wave
     double p = ATAN_P[0];
 #pragma unroll
-    for (int k = 1; k < 11; ++k) p = __builtin_fma(p, s, ATAN_P[k]);
+    for (int k = 1; k < 11; ++k) {
+        double q;
+        asm("v_fma_f64 %0, %1, %2, %3" : "=v"(q) : "v"(p), "v"(s), "s"(ATAN_P[k]));
+        p = q;
+    }
     double a = __builtin_fma(u * s, p, u);
     a = big ? a + PI_4_F64 : a;
     a = ay > ax ? PI_2_F64 - a : a;

@@ -917,6 +917,8 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     a.sky = c->sky; a.srgb_lut = c->lut; a.srgb_enc = c->enc; a.sky_w = c->sky_w; a.sky_h = c->sky_h;
     // k = (DP * RS) * -1.5 (:126); the per-frame fields (camera, c_ps, outputs)
     a.kfac = (a.dp * a.rs) * -1.5f;
+    a.rw2 = 1.0f / (2.0f * (float)a.width);
+    a.rh2 = 1.0f / (2.0f * (float)a.height);
     a.n_frames = n_frames;
     a.clk = c->clk;
     a.clk_mask = c->clk_mask;

@@ -156,8 +156,12 @@ __device__ __forceinline__ v3 sample_sky(const MarchArgs& a, const float* lut, f
     int32_t x1 = clampi(x0 + 1, 0, wm), y1 = clampi(y0 + 1, 0, hm);
     x0 = clampi(x0, 0, wm);
     y0 = clampi(y0, 0, hm);
-    v3 t00 = decode(lut, texel_u32(a, x0, y0)), t10 = decode(lut, texel_u32(a, x1, y0));
-    v3 t01 = decode(lut, texel_u32(a, x0, y1)), t11 = decode(lut, texel_u32(a, x1, y1));
+    // the four gathers first, then the decodes: one wait for all four (in the source-order build each
+    // decode would otherwise wait for its own load)
+    const uint32_t w00 = texel_u32(a, x0, y0), w10 = texel_u32(a, x1, y0);
+    const uint32_t w01 = texel_u32(a, x0, y1), w11 = texel_u32(a, x1, y1);
+    v3 t00 = decode(lut, w00), t10 = decode(lut, w10);
+    v3 t01 = decode(lut, w01), t11 = decode(lut, w11);
     float ia = 1.0f - fa, ib = 1.0f - fb;
     v3 top = add(muls(t00, ia), muls(t10, fa));
     v3 bot = add(muls(t01, ia), muls(t11, fa));
@@ -183,14 +187,15 @@ __device__ __forceinline__ Frame make_frame(const MarchArgs& a) {
 // vs_main + rasteriser interpolation + fs_main :362 for pixel (px, py): the world-space corner rays of
 // the screen triangle (3,1),(-1,1),(-1,-3) interpolated at the pixel centre, normalised.
 // Exact mode: the two divisions use the division core (numerators in [0.5, 2^32], denominators 2W,
-// 2H in [2, 2^33]: always inside its domain) and the normalisation normalize_x.
+// 2H in [2, 2^33]: always inside its domain) with the reciprocals RN(1/2W), RN(1/2H) from the host, and
+// the normalisation normalize_x.
 __device__ __forceinline__ v3 pixel_ray(const MarchArgs& a, uint32_t px, uint32_t py) {
 #if BH_FAST
     const float l0 = ((float)px + 0.5f) / (2.0f * (float)a.width);
     const float l2 = ((float)py + 0.5f) / (2.0f * (float)a.height);
 #else
-    const float l0 = crm::div_core((float)px + 0.5f, crm::rcp_refined(2.0f * (float)a.width));
-    const float l2 = crm::div_core((float)py + 0.5f, crm::rcp_refined(2.0f * (float)a.height));
+    const float l0 = crm::div_core((float)px + 0.5f, crm::Rcp{2.0f * (float)a.width, a.rw2});
+    const float l2 = crm::div_core((float)py + 0.5f, crm::Rcp{2.0f * (float)a.height, a.rh2});
 #endif
     const float l1 = (1.0f - l0) - l2;
     const v3 d = add(add(smul(l0, mk(a.c0[0], a.c0[1], a.c0[2])), smul(l1, mk(a.c1[0], a.c1[1], a.c1[2]))),
