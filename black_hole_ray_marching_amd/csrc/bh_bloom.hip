@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <utility>
 
 #include "bh_common.hpp"
 #include "bh_crmath.hpp"
@@ -127,11 +128,15 @@ __device__ __forceinline__ F4 quant(const Lds& L, F4 c) { return dec(L, enc(L, c
 // reciprocal of n shared by the block (exact: n >= 1 and i + 0.5 >= 0.5 are inside its domain).
 __device__ __forceinline__ float texcoord(uint32_t i, const crm::Rcp& R) { return crm::div_core((float)i + 0.5f, R); }
 
-// x / 12 of the up-sampling filter: the div12 core where it is exact (x == 0 or |x| >= 2^-60,
-// selftest op 5), IEEE division otherwise (never taken by sums of decoded texels).
-__device__ __forceinline__ float div12(float x) {
-    float q = crm::div12(x);
-    if (__builtin_expect(crm::key(x) < crm::KEY_MIN, 0)) q = x / 12.0f;
+// x / 12 of the up-sampling filter, for the four channels of a sum: the div12 core where it is exact
+// (x == 0 or |x| >= 2^-60, selftest op 5), IEEE division for all four when any channel of any lane is
+// outside that (never taken by sums of decoded texels).  One test after all four cores keeps the sums'
+// arithmetic in one basic block: a branch per channel let the compiler sink the other channels' sums
+// past it, keeping every tap's texels live.
+__device__ __forceinline__ F4 div12(const F4& s) {
+    F4 q{crm::div12(s.r), crm::div12(s.g), crm::div12(s.b), crm::div12(s.a)};
+    const uint32_t k = crm::kmin3(crm::key(s.r), crm::key(s.g), min(crm::key(s.b), crm::key(s.a)));
+    if (__builtin_expect(k < crm::KEY_MIN, 0)) q = {s.r / 12.0f, s.g / 12.0f, s.b / 12.0f, s.a / 12.0f};
     return q;
 }
 
@@ -205,6 +210,14 @@ struct Taps {
     __device__ __forceinline__ float dv_min() const { return dv(6); }
     __device__ __forceinline__ float dv_max() const { return dv(2); }
 };
+// tap i's offset multiplier along an axis (Taps::du / dv), and floor / remainder in eighths (the
+// standard plans, see quad_tap_std)
+__host__ __device__ constexpr int tap_m(int axis, int i) {
+    return (int)(((axis ? 0x10123432u : 0x12343210u) >> (4 * i)) & 15u) - 2;
+}
+__host__ __device__ constexpr int fdiv8(int v) { return v >= 0 ? v / 8 : -((7 - v) / 8); }
+__host__ __device__ constexpr int fmod8(int v) { return v - 8 * fdiv8(v); }
+
 // The structured form of an 8-tap pass, proven by the host for every pixel of a launch
 // (bh_bloom_tap_plan): along each axis tap i's unclamped texel coordinate u*n - 0.5 equals x + o_i + f_i
 // exactly, with an integer offset o_i and a weight f_i of 0 (point) or 1/2 (half).  The bilinear sample
@@ -224,7 +237,7 @@ struct TapPlan {
 // (clamp(x), clamp(y)) for the logical coordinates [x0, x0 + FP) x [y0, y0 + FP): decoded (float4), or
 // with RAW the BGRA8 word (4 B instead of 16: the final pass's 44 x 44 footprint then takes 7.6 KiB of
 // LDS instead of 30 KiB, so twice as many blocks fit a CU), decoded when a tap reads it.
-template <int FP, bool RAW = false>
+template <int FP, bool RAW = false, int STD = 0>
 struct PlanSrc {
     CTex t;
     const void* tile;
@@ -245,6 +258,39 @@ struct PlanSrc {
     }
 };
 
+// up8's sums, tap by tap: s + q * w with w = 1 (even taps) or 2 (odd taps).  q * 2 is exact for every
+// finite q, so RN(s + RN(q * 2)) == fma(q, 2, s): one instruction per channel instead of two.
+__device__ __forceinline__ void acc(F4& s, const F4& q, int i) {
+    if (i == 0) {
+        s = q;
+    } else if (i & 1) {
+        s.r = __builtin_fmaf(q.r, 2.0f, s.r); s.g = __builtin_fmaf(q.g, 2.0f, s.g);
+        s.b = __builtin_fmaf(q.b, 2.0f, s.b); s.a = __builtin_fmaf(q.a, 2.0f, s.a);
+    } else {
+        s.r = s.r + q.r; s.g = s.g + q.g; s.b = s.b + q.b; s.a = s.a + q.a;
+    }
+}
+// A TapPlan tap's contribution, exactly: the half-weight forms reduce a tap to h * 2^-k with h a sum of
+// decoded texels (0 or >= 2^-12, so every product by a power of two below is exact), and the tap's
+// weight w = 1 or 2 then folds into one fma:  s + RN(h * 0.5) * 2 == s + h,  s + RN(h * 0.5) ==
+// fma(h, 0.5, s),  s + RN(h * 0.25) * 2 == fma(h, 0.5, s),  s + RN(h * 0.25) == fma(h, 0.25, s).
+// `sh` = the tap's scale exponent k (0: a point tap, 1: one half axis, 2: both).
+__device__ __forceinline__ void acc_scaled(F4& s, const float4& h, int sh, int i) {
+    const float sc = sh == 0 ? 1.0f : (sh == 1 ? 0.5f : 0.25f);
+    if (i == 0) {
+        s = {h.x * sc, h.y * sc, h.z * sc, h.w * sc};
+        return;
+    }
+    const int e = sh - (i & 1);  // s gains h * 2^-e, exactly
+    if (e == 0) {
+        s.r = s.r + h.x; s.g = s.g + h.y; s.b = s.b + h.z; s.a = s.a + h.w;
+    } else {
+        const float m = e < 0 ? 2.0f : (e == 1 ? 0.5f : 0.25f);
+        s.r = __builtin_fmaf(h.x, m, s.r); s.g = __builtin_fmaf(h.y, m, s.g);
+        s.b = __builtin_fmaf(h.z, m, s.b); s.a = __builtin_fmaf(h.w, m, s.a);
+    }
+}
+
 // `point`: bit i set = tap i's weights are exactly 0 for every pixel of this launch
 template <class Src>
 __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float v, uint32_t point) {
@@ -255,54 +301,52 @@ __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float 
         // take 160 VGPRs (3 waves per SIMD); the rolled loop recomputes the offsets every tap
         __builtin_amdgcn_sched_barrier(0);
         const float tu = u + k.du(i), tv = v + k.dv(i);
-        const F4 q = ((point >> i) & 1u) ? sample_point(src, tu, tv) : sample(src, tu, tv);
-        const float w = (i & 1) ? 2.0f : 1.0f;  // x * 1.0 == x exactly: one form for both weights
-        s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
+        acc(s, ((point >> i) & 1u) ? sample_point(src, tu, tv) : sample(src, tu, tv), i);
     }
-    return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
+    return div12(s);
 }
 // up8 over a TapPlan-staged footprint: the same sums, each tap 1, 2 or 4 LDS reads at constant offsets
-template <int FP, bool RAW>
-__device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW>& src, const Taps&, float, float, uint32_t) {
+// (STD: the standard plan A = STD, its offsets and halves constants -- see quad_tap_std)
+template <int FP, bool RAW, int STD>
+__device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW, STD>& src, const Taps&, float, float, uint32_t) {
     const TapPlan& P = *src.P;
     const uint32_t lx = xcd_block().x * 16u + (threadIdx.x & 15u), ly = xcd_block().y * 16u + (threadIdx.x >> 4);
     const int32_t base = ((int32_t)ly - src.y0) * FP + ((int32_t)lx - src.x0);
     F4 s{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        const int32_t o = base + P.oy[i] * FP + P.ox[i];
+        const int32_t o = base + (STD ? fdiv8(STD * tap_m(1, i)) * FP + fdiv8(STD * tap_m(0, i)) : P.oy[i] * FP + P.ox[i]);
         float4 q = src.fetch(o);
-        const bool hx = (P.hx >> i) & 1u, hy = (P.hy >> i) & 1u;
+        const bool hx = STD ? fmod8(STD * tap_m(0, i)) == 4 : (P.hx >> i) & 1u;
+        const bool hy = STD ? fmod8(STD * tap_m(1, i)) == 4 : (P.hy >> i) & 1u;
         if (hx && hy) {
             const float4 a = src.fetch(o + 1), b = src.fetch(o + FP), c = src.fetch(o + FP + 1);
-            q = make_float4(((q.x + a.x) + (b.x + c.x)) * 0.25f, ((q.y + a.y) + (b.y + c.y)) * 0.25f,
-                            ((q.z + a.z) + (b.z + c.z)) * 0.25f, ((q.w + a.w) + (b.w + c.w)) * 0.25f);
+            q = make_float4((q.x + a.x) + (b.x + c.x), (q.y + a.y) + (b.y + c.y), (q.z + a.z) + (b.z + c.z),
+                            (q.w + a.w) + (b.w + c.w));
+            acc_scaled(s, q, 2, i);
         } else if (hx || hy) {
             const float4 a = src.fetch(o + (hx ? 1 : FP));
-            q = make_float4((q.x + a.x) * 0.5f, (q.y + a.y) * 0.5f, (q.z + a.z) * 0.5f, (q.w + a.w) * 0.5f);
-        }
-        if (i == 0) {
-            s = {q.x, q.y, q.z, q.w};
+            acc_scaled(s, make_float4(q.x + a.x, q.y + a.y, q.z + a.z, q.w + a.w), 1, i);
         } else {
-            const float w = (i & 1) ? 2.0f : 1.0f;
-            s.r = s.r + q.x * w; s.g = s.g + q.y * w; s.b = s.b + q.z * w; s.a = s.a + q.w * w;
+            acc_scaled(s, q, 0, i);
         }
     }
-    return {div12(s.r), div12(s.g), div12(s.b), div12(s.a)};
+    return div12(s);
 }
 
-__device__ __forceinline__ void acc(F4& s, const F4& q, int i) {
-    if (i == 0) {
-        s = q;
-    } else {
-        const float w = (i & 1) ? 2.0f : 1.0f;  // up8's sums, tap by tap
-        s.r = s.r + q.r * w; s.g = s.g + q.g * w; s.b = s.b + q.b * w; s.a = s.a + q.a * w;
-    }
+// the 16 sums complete here (an empty asm that reads them): keeps the compiler from sinking part of a
+// tap's arithmetic below later taps, which would keep every tap's texels live at once (~240 VGPRs)
+__device__ __forceinline__ void pin(F4 (&s)[2][2]) {
+    asm volatile("" ::"v"(s[0][0].r), "v"(s[0][0].g), "v"(s[0][0].b), "v"(s[0][0].a), "v"(s[0][1].r), "v"(s[0][1].g),
+                 "v"(s[0][1].b), "v"(s[0][1].a), "v"(s[1][0].r), "v"(s[1][0].g), "v"(s[1][0].b), "v"(s[1][0].a),
+                 "v"(s[1][1].r), "v"(s[1][1].g), "v"(s[1][1].b), "v"(s[1][1].a));
 }
-
 // remix.wgsl:22-24
+// c1 * 0.5 is exact (c1 a sum / lerp of decoded texels: 0 or far above the subnormals), so
+// c0 + RN(c1 * 0.5) == fma(c1, 0.5, c0)
 __device__ __forceinline__ F4 remix(F4 c0, F4 c1) {
-    return {c0.r + c1.r * 0.5f, c0.g + c1.g * 0.5f, c0.b + c1.b * 0.5f, c0.a + c1.a * 0.5f};
+    return {__builtin_fmaf(c1.r, 0.5f, c0.r), __builtin_fmaf(c1.g, 0.5f, c0.g), __builtin_fmaf(c1.b, 0.5f, c0.b),
+            __builtin_fmaf(c1.a, 0.5f, c0.a)};
 }
 
 enum Shader : uint32_t { SH_COPY = bh_bloom_shader_copy, SH_DOWN = bh_bloom_shader_down, SH_UP = bh_bloom_shader_up,
@@ -322,9 +366,10 @@ __device__ __forceinline__ Span tap_span(uint32_t first, uint32_t last, const cr
 // Run `body(src)` with the block's input footprint staged in LDS (decoded) when it fits FP x FP,
 // else straight from global memory; both give identical values.  Called by every thread.  RAW: a
 // TapPlan footprint is staged as BGRA8 words (PlanSrc<FP, true>; `tile` then needs FP*FP*4 bytes,
-// else FP*FP*16).
-template <int FP, bool RAW = false, class Body>
-__device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, const Taps& k, uint32_t ow,
+// else FP*FP*16).  It also loads the block's tables (load_tables), after issuing the footprint's loads:
+// the two global round trips overlap instead of following each other.
+template <int FP, bool RAW = false, int STD = 0, class Body>
+__device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* tile, const Taps& k, uint32_t ow,
                                             uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, const TapPlan& P,
                                             Body body) {
     const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
@@ -345,6 +390,7 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
                 if (ly < ny && lx < nx)
                     raw[a][b] = t.px[(size_t)clampi(y0 + ly, 0, hm) * t.w + clampi(x0 + lx, 0, wm)];
             }
+        load_tables(tb, L);
 #pragma unroll
         for (int a = 0; a < R; ++a)
 #pragma unroll
@@ -360,7 +406,7 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
                 }
             }
         __syncthreads();
-        body(PlanSrc<FP, RAW>{t, tile, x0, y0, &P, &L});
+        body(PlanSrc<FP, RAW, STD>{t, tile, x0, y0, &P, &L});
         return;
     }
     const Span sx = tap_span(bx, min(bx + 15u, ow - 1u), Rw, k.du_min(), k.du_max(), t.w);
@@ -378,6 +424,7 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
                 raw[r] = t.px[(size_t)(sy.lo + ly) * t.w + (sx.lo + lx)];
             }
         }
+        load_tables(tb, L);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int32_t i = (int32_t)threadIdx.x + r * 256;
@@ -390,6 +437,7 @@ __device__ __forceinline__ void with_source(CTex t, const Lds& L, float4* tile, 
         __syncthreads();
         body(TileSrc<FP>{t, tile, sx.lo, sy.lo});
     } else {
+        load_tables(tb, L);
         body(GlobalSrc{t, &L});
     }
 }
@@ -409,16 +457,16 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
                                         Tex out) {
     __shared__ Lds L;
     __shared__ float4 tile[SH == SH_UP ? FP_UP * FP_UP : 1];
-    load_tables(tb, L);
     const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     if constexpr (SH == SH_UP) {
         const Taps k(rx, ry);
-        with_source<FP_UP>(a, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
+        with_source<FP_UP>(tb, a, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
             if (x >= out.w || y >= out.h) return;
             out.px[(size_t)y * out.w + x] = enc(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         });
     } else {
+        load_tables(tb, L);
         if (x >= out.w || y >= out.h) return;
         const float u = texcoord(x, Rw), v = texcoord(y, Rh);
         const GlobalSrc A{a, &L};
@@ -433,11 +481,10 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
 __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, TapPlan P, Tex Y) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_Y * FP_Y];
-    load_tables(tb, L);
     const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)Y.w), Rh = crm::rcp_refined((float)Y.h);
     const Taps k(X.w, X.h);
-    with_source<FP_Y>(X, L, tile, k, Y.w, Y.h, Rw, Rh, P, [&](const auto& src) {
+    with_source<FP_Y>(tb, X, L, tile, k, Y.w, Y.h, Rw, Rh, P, [&](const auto& src) {
         if (x >= Y.w || y >= Y.h) return;
         const F4 b1 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         Y.px[(size_t)y * Y.w + x] = enc(L, remix(src.at((int32_t)x, (int32_t)y), b1));
@@ -463,19 +510,19 @@ __device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2])
             float4 q = t[b][a];
             if constexpr (HX && HY) {
                 const float4 u = t[b][a + 1], v = t[b + 1][a], w = t[b + 1][a + 1];
-                q = make_float4(((q.x + u.x) + (v.x + w.x)) * 0.25f, ((q.y + u.y) + (v.y + w.y)) * 0.25f,
-                                ((q.z + u.z) + (v.z + w.z)) * 0.25f, ((q.w + u.w) + (v.w + w.w)) * 0.25f);
+                q = make_float4((q.x + u.x) + (v.x + w.x), (q.y + u.y) + (v.y + w.y), (q.z + u.z) + (v.z + w.z),
+                                (q.w + u.w) + (v.w + w.w));
             } else if constexpr (HX || HY) {
                 const float4 u = HX ? t[b][a + 1] : t[b + 1][a];
-                q = make_float4((q.x + u.x) * 0.5f, (q.y + u.y) * 0.5f, (q.z + u.z) * 0.5f, (q.w + u.w) * 0.5f);
+                q = make_float4(q.x + u.x, q.y + u.y, q.z + u.z, q.w + u.w);
             }
-            acc(s[b][a], {q.x, q.y, q.z, q.w}, i);
+            acc_scaled(s[b][a], q, HX + HY, i);
         }
 }
+template <int STD>
 __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_YQ * FP_YQ];
-    load_tables(tb, L);
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;  // the footprint, clamp-to-edge
     {
@@ -488,6 +535,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
             if (ly < ny) raw[r] = X.px[(size_t)clampi(y0 + ly, 0, hm) * X.w + clampi(x0 + lx, 0, wm)];
         }
+        load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
@@ -502,14 +550,30 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     if (x >= Y.w || y >= Y.h) return;
     const int32_t base = ((int32_t)y - y0) * FP_YQ + ((int32_t)x - x0);
     F4 s[2][2];
+    if constexpr (STD != 0) {
+        // the standard plan: constant offsets and halves, one tap at a time (see quad_taps_std)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const float4* T = tile + (base + fdiv8(STD * tap_m(1, i)) * FP_YQ + fdiv8(STD * tap_m(0, i)));
+            switch ((fmod8(STD * tap_m(0, i)) == 4 ? 1 : 0) | (fmod8(STD * tap_m(1, i)) == 4 ? 2 : 0)) {
+                case 0: yquad_tap<0, 0>(T, i, s); break;
+                case 1: yquad_tap<1, 0>(T, i, s); break;
+                case 2: yquad_tap<0, 1>(T, i, s); break;
+                default: yquad_tap<1, 1>(T, i, s); break;
+            }
+            pin(s);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
 #pragma unroll 1
-    for (int i = 0; i < 8; i++) {
-        const float4* T = tile + (base + P.oy[i] * FP_YQ + P.ox[i]);
-        switch (((P.hx >> i) & 1u) | ((P.hy >> i) & 1u) << 1) {  // launch-uniform
-            case 0: yquad_tap<0, 0>(T, i, s); break;
-            case 1: yquad_tap<1, 0>(T, i, s); break;
-            case 2: yquad_tap<0, 1>(T, i, s); break;
-            default: yquad_tap<1, 1>(T, i, s); break;
+        for (int i = 0; i < 8; i++) {
+            const float4* T = tile + (base + P.oy[i] * FP_YQ + P.ox[i]);
+            switch (((P.hx >> i) & 1u) | ((P.hy >> i) & 1u) << 1) {  // launch-uniform
+                case 0: yquad_tap<0, 0>(T, i, s); break;
+                case 1: yquad_tap<1, 0>(T, i, s); break;
+                case 2: yquad_tap<0, 1>(T, i, s); break;
+                default: yquad_tap<1, 1>(T, i, s); break;
+            }
         }
     }
     // both pixels of each quad row in one 8-byte store: inside the frame, and rows 8-byte aligned (even
@@ -520,7 +584,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
         uint32_t c[2];
 #pragma unroll
         for (int a = 0; a < 2; ++a) {
-            const F4 b1 = quant(L, {div12(s[b][a].r), div12(s[b][a].g), div12(s[b][a].b), div12(s[b][a].a)});
+            const F4 b1 = quant(L, div12(s[b][a]));
             const float4 v = tile[base + b * FP_YQ + a];  // the pixel's own texel
             c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
         }
@@ -535,22 +599,25 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
 }
 
 // Fused last stage: out = col + 0.5 * q(Z), Z = Y + 0.5 * q(up8(U0, res (rx, ry))).
-__global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTex U0, uint32_t rx,
+template <int STD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) bloom_final_kernel(Tables tb, CTex col, CTex Y, CTex U0, uint32_t rx,
                                                    uint32_t ry, uint32_t point, TapPlan P, Tex out) {
     __shared__ Lds L;
     // dynamic: FP_FINAL^2 BGRA8 words for the TapPlan form (7.6 KiB: ~2x the resident blocks of the
     // decoded form, for a pass that mostly waits on its staging loads), else FP_FINAL^2 float4
     extern __shared__ float4 tile[];
-    load_tables(tb, L);
     const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
-    with_source<FP_FINAL, true>(U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
-        if (x >= out.w || y >= out.h) return;
-        const size_t i = (size_t)y * out.w + x;
+    // the pixel's own Y and col texels: loaded before the footprint and the tables, used last
+    const bool in = x < out.w && y < out.h;
+    const size_t i = (size_t)y * out.w + x;
+    const uint32_t yv = in ? Y.px[i] : 0u, cv = in ? col.px[i] : 0u;
+    with_source<FP_FINAL, true, STD>(tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
+        if (!in) return;
         const F4 b3 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
-        const F4 z = quant(L, remix(dec(L, Y.px[i]), b3));
-        out.px[i] = enc(L, remix(dec(L, col.px[i]), z));
+        const F4 z = quant(L, remix(dec(L, yv), b3));
+        out.px[i] = enc(L, remix(dec(L, cv), z));
     });
 }
 
@@ -563,6 +630,7 @@ __global__ void BLOOM_BOUNDS bloom_final_kernel(Tables tb, CTex col, CTex Y, CTe
 // texels (x>>1) + o and + 1 with weights f, 1 - f -- the general sampler's own arithmetic, without its
 // texcoord, floor and clamp work.  One lane computes a 2x2 pixel quad: per tap the four pixels' texels
 // lie in a 3x3 (2x2 when both parities share o) neighbourhood of (x>>1, y>>1), read once for all four.
+
 struct Up2Plan {
     int32_t ox[2][8], oy[2][8];      // [pixel parity][tap]: floor(t) - (x >> 1)
     float fx[2][8], fy[2][8];        // t - floor(t)
@@ -599,14 +667,69 @@ __device__ __forceinline__ void quad_tap(const float4* T, const Up2Plan& P, int 
         }
 }
 
+// ---- compile-time plans of the standard chain ---------------------------------------------------
+// On power-of-two frames at levels 3 (the reference's chain: src/state.rs:125) every 8-tap pass has the
+// same plan whatever the size, because each tap's texel offset scales with the texture: tap (mx, my)'s
+// coordinate along an axis is  x + A*m/8  (same-size passes: Y, A = 12; the final pass, A = 48) or
+// (x >> 1) + (A*m -+ 2)/8 for even / odd pixels (2:1 up passes: the half-size one A = 3, the full-size
+// one A = 12), in eighths of a texel.  A kernel instantiated for such an A reads every tap at constant
+// LDS offsets with constant weights: no plan loads, no per-tap branches, and the exact forms below.  The
+// host takes it only when the plan it proves for the launch (tap_plan / up2_plan) equals this one
+// entry for entry (std_tap_plan / std_up2_plan); otherwise the runtime-plan kernels run.
+// a lerp t0 (1 - f) + t1 f with f = F/8 known: f = 0 returns t0 (t0 * 1 + t1 * 0); when one weight is a
+// power of two its product is exact (texels and their lerps are 0 or far from the subnormals), so the
+// sum is one fma on the other product -- RN(RN(t0 g) + t1 f) == fma(t1, f, RN(t0 g)) -- the same bits
+template <int F>
+__device__ __forceinline__ float clerp(float t0, float t1) {
+    constexpr float f = (float)F / 8.0f, g = 1.0f - f;
+    if constexpr (F == 0) return t0;
+    else if constexpr (F == 1 || F == 2 || F == 4) return __builtin_fmaf(t1, f, t0 * g);
+    else if constexpr (F == 6 || F == 7) return __builtin_fmaf(t0, g, t1 * f);
+    else return t0 * g + t1 * f;
+}
+template <int FA, int FB>
+__device__ __forceinline__ F4 clerp2(const float4& t00, const float4& t10, const float4& t01, const float4& t11) {
+    F4 q;
+    q.r = clerp<FB>(clerp<FA>(t00.x, t10.x), clerp<FA>(t01.x, t11.x));
+    q.g = clerp<FB>(clerp<FA>(t00.y, t10.y), clerp<FA>(t01.y, t11.y));
+    q.b = clerp<FB>(clerp<FA>(t00.z, t10.z), clerp<FA>(t01.z, t11.z));
+    q.a = clerp<FB>(clerp<FA>(t00.w, t10.w), clerp<FA>(t01.w, t11.w));
+    return q;
+}
+// tap I of a 2:1 up pass with the standard plan A, for the quad at `base` (the even pixels' texel)
+template <int FP, int A, int I>
+__device__ __forceinline__ void quad_tap_std(const float4* base, F4 (&s)[2][2]) {
+    constexpr int vx0 = A * tap_m(0, I) - 2, vx1 = A * tap_m(0, I) + 2;
+    constexpr int vy0 = A * tap_m(1, I) - 2, vy1 = A * tap_m(1, I) + 2;
+    constexpr int DX = fdiv8(vx1) - fdiv8(vx0), DY = fdiv8(vy1) - fdiv8(vy0);
+    static_assert((DX == 0 || DX == 1) && (DY == 0 || DY == 1), "the quad's texels span 2 or 3 per axis");
+    const float4* T = base + fdiv8(vy0) * FP + fdiv8(vx0);
+    float4 t[2 + DY][2 + DX];
+#pragma unroll
+    for (int r = 0; r < 2 + DY; ++r)
+#pragma unroll
+        for (int c = 0; c < 2 + DX; ++c) t[r][c] = T[r * FP + c];
+    acc(s[0][0], clerp2<fmod8(vx0), fmod8(vy0)>(t[0][0], t[0][1], t[1][0], t[1][1]), I);
+    acc(s[0][1], clerp2<fmod8(vx1), fmod8(vy0)>(t[0][DX], t[0][DX + 1], t[1][DX], t[1][DX + 1]), I);
+    acc(s[1][0], clerp2<fmod8(vx0), fmod8(vy1)>(t[DY][0], t[DY][1], t[DY + 1][0], t[DY + 1][1]), I);
+    acc(s[1][1], clerp2<fmod8(vx1), fmod8(vy1)>(t[DY][DX], t[DY][DX + 1], t[DY + 1][DX], t[DY + 1][DX + 1]), I);
+}
+template <int FP, int A, int... I>
+__device__ __forceinline__ void quad_taps_std(const float4* base, F4 (&s)[2][2], std::integer_sequence<int, I...>) {
+    // one tap at a time: the sched barrier keeps the next tap's reads from being hoisted over this one's
+    // arithmetic, pin() keeps this tap's arithmetic from sinking below the next
+    ((quad_tap_std<FP, A, I>(base, s), pin(s), __builtin_amdgcn_sched_barrier(0)), ...);
+}
+
 // A 2:1 up pass (kawase_upsample.wgsl): 32x32 pixels per 256-thread block, one 2x2 quad per lane; the
-// outermost blocks (and footprints over FP) take the general sampler per pixel.
+// outermost blocks (and footprints over FP) take the general sampler per pixel.  STD: 0 = the runtime
+// plan P, else the standard plan A = STD (P still gives the interior).
 constexpr int FP_UPQ = 28;  // footprint of 16 texels + the taps' reach (24 at 4096x2048)
+template <int STD>
 __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P,
                                         Tex out) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_UPQ * FP_UPQ];
-    load_tables(tb, L);
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
@@ -627,6 +750,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
                 raw[r] = a.px[(size_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
             }
         }
+        load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int32_t i = (int32_t)threadIdx.x + r * 256;
@@ -637,6 +761,8 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
             }
         }
         __syncthreads();
+    } else {
+        load_tables(tb, L);
     }
     if (x >= out.w || y >= out.h) return;  // out.w, out.h are even (2n): the whole quad is outside
     const bool inner = staged && (int32_t)bx >= P.x_lo && (int32_t)bx + 31 <= P.x_hi && (int32_t)by >= P.y_lo &&
@@ -655,23 +781,27 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
     }
     F4 s[2][2];
     const int32_t base = ((int32_t)(y >> 1) - sy.lo) * FP_UPQ + ((int32_t)(x >> 1) - sx.lo);
-    // rolled (the plan read by scalar loads; unrolled, the taps' LDS reads are hoisted together)
+    if constexpr (STD != 0) {
+        quad_taps_std<FP_UPQ, STD>(tile + base, s, std::make_integer_sequence<int, 8>{});
+    } else {
+        // rolled (the plan read by scalar loads; unrolled, the taps' LDS reads are hoisted together)
 #pragma unroll 1
-    for (int i = 0; i < 8; i++) {
-        const float4* T = tile + (base + P.oy[0][i] * FP_UPQ + P.ox[0][i]);
-        const uint32_t d = (uint32_t)(P.ox[1][i] - P.ox[0][i]) | (uint32_t)(P.oy[1][i] - P.oy[0][i]) << 1;
-        switch (d) {  // wave-uniform
-            case 0: quad_tap<FP_UPQ, 0, 0>(T, P, i, s); break;
-            case 1: quad_tap<FP_UPQ, 1, 0>(T, P, i, s); break;
-            case 2: quad_tap<FP_UPQ, 0, 1>(T, P, i, s); break;
-            default: quad_tap<FP_UPQ, 1, 1>(T, P, i, s); break;
+        for (int i = 0; i < 8; i++) {
+            const float4* T = tile + (base + P.oy[0][i] * FP_UPQ + P.ox[0][i]);
+            const uint32_t d = (uint32_t)(P.ox[1][i] - P.ox[0][i]) | (uint32_t)(P.oy[1][i] - P.oy[0][i]) << 1;
+            switch (d) {  // wave-uniform
+                case 0: quad_tap<FP_UPQ, 0, 0>(T, P, i, s); break;
+                case 1: quad_tap<FP_UPQ, 1, 0>(T, P, i, s); break;
+                case 2: quad_tap<FP_UPQ, 0, 1>(T, P, i, s); break;
+                default: quad_tap<FP_UPQ, 1, 1>(T, P, i, s); break;
+            }
         }
     }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
         uint2 w;
-        w.x = enc(L, {div12(s[b][0].r), div12(s[b][0].g), div12(s[b][0].b), div12(s[b][0].a)});
-        w.y = enc(L, {div12(s[b][1].r), div12(s[b][1].g), div12(s[b][1].b), div12(s[b][1].a)});
+        w.x = enc(L, div12(s[b][0]));
+        w.y = enc(L, div12(s[b][1]));
         *reinterpret_cast<uint2*>(out.px + (size_t)(y + b) * out.w + x) = w;  // x even: 8-byte aligned
     }
 }
@@ -829,6 +959,38 @@ Up2Plan up2_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx
     return P;
 }
 
+// The standard plan (see quad_tap_std) a runtime plan equals, or 0: A = 12 or 3 for a 2:1 up pass, A =
+// 12 or 48 for a same-size TapPlan pass.  BH_BLOOM_NO_STD (A/B) disables them.
+static const bool g_no_std = std::getenv("BH_BLOOM_NO_STD") != nullptr;
+int std_up2_plan(const Up2Plan& P) {
+    if (!P.valid || g_no_std) return 0;
+    for (int A : {12, 3}) {
+        bool eq = true;
+        for (int i = 0; i < 8 && eq; ++i)
+            for (int p = 0; p < 2 && eq; ++p) {
+                const int vx = A * tap_m(0, i) + (p ? 2 : -2), vy = A * tap_m(1, i) + (p ? 2 : -2);
+                eq = P.ox[p][i] == fdiv8(vx) && P.oy[p][i] == fdiv8(vy) && P.fx[p][i] == (float)fmod8(vx) / 8.0f &&
+                     P.fy[p][i] == (float)fmod8(vy) / 8.0f;
+            }
+        if (eq) return A;
+    }
+    return 0;
+}
+int std_tap_plan(const TapPlan& P) {
+    if (!P.valid || g_no_std) return 0;
+    for (int A : {12, 48}) {
+        bool eq = true;
+        for (int i = 0; i < 8 && eq; ++i) {
+            const int vx = A * tap_m(0, i), vy = A * tap_m(1, i);
+            eq = (fmod8(vx) == 0 || fmod8(vx) == 4) && (fmod8(vy) == 0 || fmod8(vy) == 4) && P.ox[i] == fdiv8(vx) &&
+                 P.oy[i] == fdiv8(vy) && ((P.hx >> i) & 1u) == (fmod8(vx) == 4 ? 1u : 0u) &&
+                 ((P.hy >> i) & 1u) == (fmod8(vy) == 4 ? 1u : 0u);
+        }
+        if (eq) return A;
+    }
+    return 0;
+}
+
 // bit i: tap i of kawase_upsample.wgsl samples texel centres exactly for every pixel of an
 // ow x oh pass over a tw x th texture with resolution uniform (rx, ry)
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(uint32_t ow, uint32_t oh, uint32_t tw,
@@ -858,7 +1020,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     if (shader == SH_UP && !P.valid && !no_up2) {
         const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
         if (Q.valid) {
-            hipLaunchKernelGGL(up2_kernel, dim3((ow + 31u) / 32u, (oh + 31u) / 32u), dim3(256), 0, s, tb, A, rx, ry, pm, Q, O);
+            const dim3 g((ow + 31u) / 32u, (oh + 31u) / 32u);
+            switch (std_up2_plan(Q)) {
+                case 12: hipLaunchKernelGGL(up2_kernel<12>, g, dim3(256), 0, s, tb, A, rx, ry, pm, Q, O); break;
+                case 3: hipLaunchKernelGGL(up2_kernel<3>, g, dim3(256), 0, s, tb, A, rx, ry, pm, Q, O); break;
+                default: hipLaunchKernelGGL(up2_kernel<0>, g, dim3(256), 0, s, tb, A, rx, ry, pm, Q, O); break;
+            }
             return (int)hipGetLastError();
         }
     }
@@ -878,8 +1045,13 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const flo
     const TapPlan P = tap_plan(w, h, w, h, w, h);
     static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
     if (P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ) {
-        hipLaunchKernelGGL(bloom_yq_kernel, dim3((w + 31u) / 32u, (h + 31u) / 32u), dim3(256), 0, s,
-                           Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P, Tex{Y, w, h});
+        const dim3 g((w + 31u) / 32u, (h + 31u) / 32u);
+        if (std_tap_plan(P) == 12)
+            hipLaunchKernelGGL(bloom_yq_kernel<12>, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P,
+                               Tex{Y, w, h});
+        else
+            hipLaunchKernelGGL(bloom_yq_kernel<0>, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P,
+                               Tex{Y, w, h});
         return (int)hipGetLastError();
     }
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, w, h);
@@ -899,7 +1071,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
     // the kernel's with_source takes the TapPlan form exactly when this holds (raw words staged)
     const bool plan = P.valid && P.hi_x - P.lo_x + 16 <= FP_FINAL && P.hi_y - P.lo_y + 16 <= FP_FINAL;
     const size_t lds = (size_t)FP_FINAL * FP_FINAL * (plan ? sizeof(uint32_t) : sizeof(float4));
-    hipLaunchKernelGGL(bloom_final_kernel, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets, codes}, CTex{col, w, h},
-                       CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
+    if (plan && std_tap_plan(P) == 48)
+        hipLaunchKernelGGL(bloom_final_kernel<48>, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets, codes},
+                           CTex{col, w, h}, CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
+    else
+        hipLaunchKernelGGL(bloom_final_kernel<0>, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets, codes},
+                           CTex{col, w, h}, CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
     return (int)hipGetLastError();
 }
