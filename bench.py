@@ -685,8 +685,9 @@ def main() -> int:
                        "note": "avg/min/max over the K timed launches (HIP events on the render stream, the order "
                                "kernel included); sum_n_rk / sum_steps per frame (this rank's tiles)"},
             "clock": (dict(clock, stride=CLOCK_STRIDE,
-                           note="shader clock during the timed launches: every "
-                                f"{CLOCK_STRIDE}th wave of the march kernel reads s_memtime (shader clock) and "
+                           note="shader clock during the timed launches: one wave in "
+                                f"{CLOCK_STRIDE} of the march kernel (spread over the XCDs; per_xcd_mhz by "
+                                "HW_REG_XCC_ID) reads s_memtime (shader clock) and "
                                 "s_memrealtime (100 MHz) at its start and end (bh_set_clock_probe); mhz = 100 x "
                                 "sum(shader ticks) / sum(100 MHz ticks) over those waves; peak_mhz is the clock "
                                 "the 157.3 TFLOP/s peak assumes") | {"peak_mhz": PEAK_MHZ}) if clock else None,
@@ -739,7 +740,7 @@ def main() -> int:
 # extra legs after the timed region (N = 1): single-frame launches, orbit-path launches
 EXTRA_SINGLE_FRAMES = 24
 EXTRA_ORBIT_LAUNCHES = 4
-CLOCK_STRIDE = 256   # every 256th wave of a march launch samples the shader clock
+CLOCK_STRIDE = 256   # one wave in 256 of a march launch samples the shader clock
 CALIBRATE_WARM, CALIBRATE_STEPS = 2, 3   # batches per candidate partition of --root-ratio calibrate
 PEAK_MHZ = 2400.0    # the shader clock behind the 157.3 TFLOP/s FP32 peak (1024 SIMDs x 32 lanes x 2 x 2.4 GHz)
 

@@ -69,7 +69,7 @@ struct MarchArgs {
     // up to BH_INLINE_FRAMES of them inline, more from a device table (frame_table, else null)
     uint32_t n_frames;
     const FrameArgs* frame_table;
-    // shader-clock probe (bh_set_clock_probe): per-XCD accumulators, sampled slots = slot & clk_mask == 0
+    // shader-clock probe (bh_set_clock_probe): per-XCD accumulators, sampled slots: (slot + slot / 256) & clk_mask == 0
     unsigned long long* clk;
     uint32_t clk_mask;
     FrameArgs frames[BH_INLINE_FRAMES];

@@ -1208,7 +1208,9 @@ __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs 
     __syncthreads();
     const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
     if (slot >= A.n_tiles * A.n_frames) return;  // wave-uniform
-    const bool probe = A.clk && (slot & A.clk_mask) == 0u;
+    // one slot in `stride`, rotated by slot / stride: the dispatcher deals workgroups to the 8 XCDs round
+    // robin, so plain multiples of the stride would all land on one XCD
+    const bool probe = A.clk && ((slot + (slot >> 8)) & A.clk_mask) == 0u;
     ClockStart c0{0u, 0u};
     if (probe) c0 = clock_start();
     march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);

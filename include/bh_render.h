@@ -348,8 +348,9 @@ int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mism
                        uint32_t* out_examples, int device);
 
 /* Diagnostics: the shader clock DURING march launches (the bench's "clock" block).  While armed
- * (acc != NULL), every wave of the tile schedule's march kernels of this ctx whose dispatch slot is a
- * multiple of `stride` (a power of two) reads the shader-clock counter (s_memtime) and the constant
+ * (acc != NULL), one wave in `stride` (a power of two) of the tile schedule's march kernels of this ctx --
+ * dispatch slots k with (k + k / 256) % stride == 0, spread over the XCDs -- reads the shader-clock
+ * counter (s_memtime) and the constant
  * 100 MHz counter (s_memrealtime) when it starts and when it ends, and adds the differences to its
  * XCD's slot: acc[16*x + 0] += shader ticks, acc[16*x + 1] += 100 MHz ticks, acc[16*x + 2] += 1 (x =
  * the XCD, 0..7; acc = 128 u64 of device memory, zeroed by the caller, 128 B per XCD).  The clock of

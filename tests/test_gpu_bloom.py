@@ -58,6 +58,23 @@ def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     scene.close()
 
 
+@pytest.mark.parametrize("H,W,levels", [(128, 256, 3), (256, 512, 3), (120, 200, 3)])
+def test_bloom_bitexact_any_alpha(torch_cuda, sky_small, H, W, levels):
+    """Inputs with every alpha byte (the march writes 255, but bh_bloom takes any BGRA8 texels): the
+    exact fma forms of the standard-plan kernels (acc_scaled, clerp, remix) rest on the products by
+    powers of two being exact for every decoded channel, alpha k/255 included."""
+    rng = np.random.default_rng(W * 3 + H)
+    col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
+    col[..., 3] = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
+    bo[..., 3] = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
+    scene = bh.Scene(16, 16, sky=sky_small)
+    for schedule in (bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL):
+        got = _gpu_bloom(torch_cuda, scene, col, bo, levels, schedule)
+        want = oracle.bloom(col, bo, levels)
+        assert np.array_equal(got, want), (schedule, np.argwhere(got != want)[:5])
+    scene.close()
+
+
 def test_render_then_bloom_matches_oracle_chain(torch_cuda, sky_small):
     """The reference's frame: Scene::render into the two Bgra8UnormSrgb targets, then
     Bloom::render to the surface -- GPU end to end vs the two oracles end to end."""

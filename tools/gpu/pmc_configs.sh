@@ -23,7 +23,9 @@ LIST="${@:-c1 c2 c3A c3B c5 c3A_D1 c5_D1}"
 for C in $LIST; do
   OUT=$ROOT/gpurun_out/pmc_$TAG/$C
   mkdir -p $OUT
-  A="$ROOT/bench.py --no-cpu --steps 48 --warmup 48 ${CFG[$C]}"
+  # a step is one batch (one launch); one-frame launches get more of them
+  case $C in *_D1) SW="--steps 100 --warmup 30";; *) SW="--steps 20 --warmup 10";; esac
+  A="$ROOT/bench.py --no-cpu --no-extra $SW ${CFG[$C]}"
   echo "$A" > $OUT/cmd.txt
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $A > $OUT/trace.log 2>&1 || exit 1
   i=0

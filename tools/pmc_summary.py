@@ -15,6 +15,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import Counter, defaultdict
 from pathlib import Path
@@ -66,9 +67,13 @@ def summarise(cdir):
             g = Counter(x for x, _ in d).most_common(1)[0][0]
             full = [t for x, t in d if x == g]
             out["rocprof_avg_ms_all_full_launches"] = round(sum(full) / len(full), 5)
-            # the bench's timed launches: the last steps // frames_per_launch full launches (the
-            # warm-up launches before them run on a still ramping clock)
-            nt = (bench["steps"] // bench["kernel"]["frames_per_launch"]) if bench else len(full)
+            # the bench's timed launches: the last K full launches (a step is one launch; older bench
+            # lines timed `steps` frames in steps // frames_per_launch launches).  The warm-up launches
+            # before them run on a still ramping clock
+            if bench:
+                nt = bench["kernel"].get("launches") or bench["steps"] // bench["kernel"]["frames_per_launch"]
+            else:
+                nt = len(full)
             timed = full[-nt:] if 0 < nt <= len(full) else full
             out["rocprof_avg_ms"] = round(sum(timed) / len(timed), 5)
             out["rocprof_full_launches"] = len(timed)
@@ -122,7 +127,8 @@ def main():
         key = s.pop("_key", None)
         print(os.path.basename(cdir.rstrip("/")), json.dumps(s))
         if key and a.write:
-            s["source"] = a.source or f"rocprofv3 of `{open(cdir + 'cmd.txt').read().strip()}` ({cdir})"
+            cmd = re.sub(r"\S*/bench\.py", "bench.py", open(cdir + "cmd.txt").read().strip())
+            s["source"] = a.source or f"rocprofv3 of `{cmd}` ({cdir})"
             s["correction"] = ("FETCH_SIZE x2 per MI355X_MICROARCH.md (gfx950 reports half of wide coalesced reads; "
                                "the sky's 4-B gathers are uncalibrated: true fetch between raw and x2); WRITE_SIZE as read")
             table[pmc_key(*key)] = s
