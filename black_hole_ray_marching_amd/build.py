@@ -47,7 +47,10 @@ TU_FLAGS = {
                           "-mllvm", "-enable-misched=0", "-mllvm", "-enable-post-misched=0"],
     "bh_tiles.hip": [],
     # post-RA scheduling off: fused bloom chain 0.556 -> 0.548 ms (A/B r01; pre-RA off too: 0.561)
-    "bh_bloom.hip": ["-ffp-contract=off", "-mllvm", "-enable-post-misched=0"],
+    # no SLP vectorisation: packed-FP32 forms of the filter's adjacent channel ops cost more than the
+    # scalar ops on gfx950 (a v_pk op issues slower than two scalar ones, plus the shuffles and hazard
+    # nops around it) and hold more VGPRs
+    "bh_bloom.hip": ["-ffp-contract=off", "-fno-slp-vectorize", "-mllvm", "-enable-post-misched=0"],
     "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
 }

@@ -101,15 +101,32 @@ __device__ __forceinline__ void load_tables(Tables tb, Lds& L) {
     __syncthreads();
 }
 
+// A1: the caller knows the texel's alpha byte is 255 (a block whose inputs are all opaque, see
+// with_source): alpha decodes to 1.0 without a table read, and the compiler folds the alpha channel's
+// whole arithmetic (sums, x/12, the encoder) to constants
+#ifndef BH_BLOOM_OPAQUE
+#define BH_BLOOM_OPAQUE 1  // 0 (A/B): never take the opaque-block forms
+#endif
+// Block-wide AND of a predicate at a barrier the caller needs anyway: one ballot per wave, its lane 0's
+// word in LDS, the barrier, then every thread reads the 4 words (__syncthreads_and costs an LDS atomic
+// per thread on one address).
+__device__ __forceinline__ bool barrier_and(bool p) {
+    __shared__ uint32_t w[4];
+    const bool all = __builtin_amdgcn_ballot_w64(!p) == 0ull;
+    if ((threadIdx.x & 63u) == 0u) w[threadIdx.x >> 6] = all ? 1u : 0u;
+    __syncthreads();
+    return (w[0] & w[1] & w[2] & w[3]) != 0u;
+}
+template <bool A1 = false>
 __device__ __forceinline__ F4 dec(const Lds& L, uint32_t t) {
-    return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], L.alut[t >> 24]};
+    return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : L.alut[t >> 24]};
 }
 __device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 __device__ __forceinline__ uint32_t unorm8(float a) {
-    if (!(a > 0.0f)) return 0u;
-    if (a >= 1.0f) return 255u;
-    return (uint32_t)__double2int_rd((double)a * 255.0 + 0.5);
+    // branch-free: the conversion of an out-of-range a is discarded by the selects
+    const uint32_t v = (uint32_t)__double2int_rd((double)fminf(fmaxf(a, 0.0f), 1.0f) * 255.0 + 0.5);
+    return !(a > 0.0f) ? 0u : (a >= 1.0f ? 255u : v);
 }
 // the Bgra8UnormSrgb store of a pass's result
 __device__ __forceinline__ uint32_t enc(const Lds& L, F4 c) {
@@ -122,7 +139,8 @@ __device__ __forceinline__ uint32_t enc(const Lds& L, F4 c) {
            (unorm8(c.a) << 24);
 #endif
 }
-__device__ __forceinline__ F4 quant(const Lds& L, F4 c) { return dec(L, enc(L, c)); }
+template <bool A1 = false>
+__device__ __forceinline__ F4 quant(const Lds& L, F4 c) { return dec<A1>(L, enc(L, c)); }
 
 // Texcoord of pixel i of an n-pixel axis, (i + 0.5) / n: the correctly rounded division core with the
 // reciprocal of n shared by the block (exact: n >= 1 and i + 0.5 >= 0.5 are inside its domain).
@@ -143,12 +161,14 @@ __device__ __forceinline__ F4 div12(const F4& s) {
 // Texel sources: decoded texel (x, y) of a BGRA8 texture straight from global memory, or from a
 // block's LDS tile of pre-decoded texels covering exactly the footprint the block samples.
 struct GlobalSrc {
+    static constexpr bool kA1 = false;
     CTex t;
     const Lds* L;
     __device__ __forceinline__ F4 at(int32_t x, int32_t y) const { return dec(*L, t.px[(size_t)y * t.w + x]); }
 };
 template <int FP>
 struct TileSrc {
+    static constexpr bool kA1 = false;
     CTex t;
     const float4* tile;  // decoded texels [y0, y0 + FP) x [x0, x0 + FP)
     int32_t x0, y0;
@@ -237,19 +257,22 @@ struct TapPlan {
 // (clamp(x), clamp(y)) for the logical coordinates [x0, x0 + FP) x [y0, y0 + FP): decoded (float4), or
 // with RAW the BGRA8 word (4 B instead of 16: the final pass's 44 x 44 footprint then takes 7.6 KiB of
 // LDS instead of 30 KiB, so twice as many blocks fit a CU), decoded when a tap reads it.
-template <int FP, bool RAW = false, int STD = 0>
+template <int FP, bool RAW = false, int STD = 0, bool A1 = false>
 struct PlanSrc {
+    static constexpr bool kA1 = A1;
     CTex t;
     const void* tile;
     int32_t x0, y0;
     const TapPlan* P;
     const Lds* L;
+    int32_t px, py;  // the pixel this thread computes (up8)
     __device__ __forceinline__ float4 fetch(int32_t i) const {
         if constexpr (RAW) {
-            const F4 d = dec(*L, static_cast<const uint32_t*>(tile)[i]);
+            const F4 d = dec<A1>(*L, static_cast<const uint32_t*>(tile)[i]);
             return make_float4(d.r, d.g, d.b, d.a);
         } else {
-            return static_cast<const float4*>(tile)[i];
+            const float4 v = static_cast<const float4*>(tile)[i];
+            return make_float4(v.x, v.y, v.z, A1 ? 1.0f : v.w);
         }
     }
     __device__ __forceinline__ F4 at(int32_t x, int32_t y) const {
@@ -307,11 +330,10 @@ __device__ __forceinline__ F4 up8(const Src& src, const Taps& k, float u, float 
 }
 // up8 over a TapPlan-staged footprint: the same sums, each tap 1, 2 or 4 LDS reads at constant offsets
 // (STD: the standard plan A = STD, its offsets and halves constants -- see quad_tap_std)
-template <int FP, bool RAW, int STD>
-__device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW, STD>& src, const Taps&, float, float, uint32_t) {
+template <int FP, bool RAW, int STD, bool A1>
+__device__ __forceinline__ F4 up8(const PlanSrc<FP, RAW, STD, A1>& src, const Taps&, float, float, uint32_t) {
     const TapPlan& P = *src.P;
-    const uint32_t lx = xcd_block().x * 16u + (threadIdx.x & 15u), ly = xcd_block().y * 16u + (threadIdx.x >> 4);
-    const int32_t base = ((int32_t)ly - src.y0) * FP + ((int32_t)lx - src.x0);
+    const int32_t base = (src.py - src.y0) * FP + (src.px - src.x0);
     F4 s{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -367,11 +389,14 @@ __device__ __forceinline__ Span tap_span(uint32_t first, uint32_t last, const cr
 // else straight from global memory; both give identical values.  Called by every thread.  RAW: a
 // TapPlan footprint is staged as BGRA8 words (PlanSrc<FP, true>; `tile` then needs FP*FP*4 bytes,
 // else FP*FP*16).  It also loads the block's tables (load_tables), after issuing the footprint's loads:
-// the two global round trips overlap instead of following each other.
+// the two global round trips overlap instead of following each other.  In the TapPlan form a block
+// whose staged texels (and the caller's `opaque` inputs of every thread) all have alpha byte 255 runs
+// `body` with an A1 source (PlanSrc<..., true>: see dec): alpha is then 1.0 everywhere and its arithmetic
+// folds away.  Both forms give the same bytes.
 template <int FP, bool RAW = false, int STD = 0, class Body>
 __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* tile, const Taps& k, uint32_t ow,
                                             uint32_t oh, const crm::Rcp& Rw, const crm::Rcp& Rh, const TapPlan& P,
-                                            Body body) {
+                                            Body body, bool opaque = false) {
     const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
     if (P.valid && P.hi_x - P.lo_x + 16 <= FP && P.hi_y - P.lo_y + 16 <= FP) {  // launch-uniform
         // the footprint with clamp-to-edge addressing: row r of the tile is texel row clamp(y0 + r);
@@ -387,6 +412,7 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
 #pragma unroll
             for (int b = 0; b < R; ++b) {
                 const int32_t ly = ty + 16 * a, lx = tx + 16 * b;
+                raw[a][b] = 0xFF000000u;
                 if (ly < ny && lx < nx)
                     raw[a][b] = t.px[(size_t)clampi(y0 + ly, 0, hm) * t.w + clampi(x0 + lx, 0, wm)];
             }
@@ -405,8 +431,15 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
                     }
                 }
             }
-        __syncthreads();
-        body(PlanSrc<FP, RAW, STD>{t, tile, x0, y0, &P, &L});
+        uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = 0; b < R; ++b) m = min(m, raw[a][b]);
+        const bool a1 = barrier_and(opaque && m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+        const int32_t px = (int32_t)bx + tx, py = (int32_t)by + ty;
+        if (a1) body(PlanSrc<FP, RAW, STD, true>{t, tile, x0, y0, &P, &L, px, py});
+        else body(PlanSrc<FP, RAW, STD, false>{t, tile, x0, y0, &P, &L, px, py});
         return;
     }
     const Span sx = tap_span(bx, min(bx + 15u, ow - 1u), Rw, k.du_min(), k.du_max(), t.w);
@@ -550,6 +583,28 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     if (x >= Y.w || y >= Y.h) return;
     const int32_t base = ((int32_t)y - y0) * FP_YQ + ((int32_t)x - x0);
     F4 s[2][2];
+    // Y = X + 0.5 q(blur1 / 12) per pixel of the quad; both pixels of each quad row in one 8-byte store:
+    // inside the frame, and rows 8-byte aligned (even width; x is even); else one word per pixel
+    auto finish = [&]() {
+        const bool full = x + 1u < Y.w && y + 1u < Y.h && (Y.w & 1u) == 0u;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            uint32_t c[2];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const F4 b1 = quant(L, div12(s[b][a]));
+                const float4 v = tile[base + b * FP_YQ + a];  // the pixel's own texel
+                c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
+            }
+            if (full) {
+                *reinterpret_cast<uint2*>(Y.px + (size_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
+            } else {
+#pragma unroll
+                for (int a = 0; a < 2; ++a)
+                    if (x + a < Y.w && y + b < Y.h) Y.px[(size_t)(y + b) * Y.w + x + a] = c[a];
+            }
+        }
+    };
     if constexpr (STD != 0) {
         // the standard plan: constant offsets and halves, one tap at a time (see quad_taps_std)
 #pragma unroll
@@ -564,6 +619,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             pin(s);
             __builtin_amdgcn_sched_barrier(0);
         }
+        finish();
     } else {
 #pragma unroll 1
         for (int i = 0; i < 8; i++) {
@@ -575,26 +631,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
                 default: yquad_tap<1, 1>(T, i, s); break;
             }
         }
-    }
-    // both pixels of each quad row in one 8-byte store: inside the frame, and rows 8-byte aligned (even
-    // width; x is even); else one word per pixel
-    const bool full = x + 1u < Y.w && y + 1u < Y.h && (Y.w & 1u) == 0u;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-        uint32_t c[2];
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-            const F4 b1 = quant(L, div12(s[b][a]));
-            const float4 v = tile[base + b * FP_YQ + a];  // the pixel's own texel
-            c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
-        }
-        if (full) {
-            *reinterpret_cast<uint2*>(Y.px + (size_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
-        } else {
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-                if (x + a < Y.w && y + b < Y.h) Y.px[(size_t)(y + b) * Y.w + x + a] = c[a];
-        }
+        finish();
     }
 }
 
@@ -613,12 +650,122 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
     const bool in = x < out.w && y < out.h;
     const size_t i = (size_t)y * out.w + x;
     const uint32_t yv = in ? Y.px[i] : 0u, cv = in ? col.px[i] : 0u;
-    with_source<FP_FINAL, true, STD>(tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
-        if (!in) return;
-        const F4 b3 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
-        const F4 z = quant(L, remix(dec(L, yv), b3));
-        out.px[i] = enc(L, remix(dec(L, cv), z));
-    });
+    with_source<FP_FINAL, true, STD>(
+        tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P,
+        [&](const auto& src) {
+            constexpr bool A1 = std::decay_t<decltype(src)>::kA1;
+            if (!in) return;
+            const F4 b3 = quant<A1>(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
+            const F4 z = quant<A1>(L, remix(dec<A1>(L, yv), b3));
+            out.px[i] = enc(L, remix(dec<A1>(L, cv), z));
+        },
+        !in || (min(yv, cv) >= 0xFF000000u));
+}
+
+// ---- persistent blocks (standard plans) ------------------------------------------------------------
+// The grid is the resident block count (a multiple of 8); block b walks the 16x16 tiles of one eighth of
+// the frame (b % 8: the blocks the dispatcher deals to one XCD, whose L2 then holds the halos its tiles
+// share) with stride gridDim / 8.  While a tile is computed from one LDS buffer, the next tile's
+// footprint streams into the other by LDS DMA (global_load_lds: no VGPRs, and the compiler does not
+// wait on it for reads of the other buffer -- a distinct __shared__ array), and the next tile's own
+// per-pixel loads are in flight in registers; the one barrier per tile waits for both.  This hides the
+// staging latency that one-tile blocks expose at every block start, amortises the table loads over the
+// block's tiles and removes the grid's last partial wave of blocks.
+struct TileWalk {
+    uint32_t t, end, step;
+    __device__ __forceinline__ TileWalk(uint32_t n_tiles) {
+        const uint32_t per = (n_tiles + 7u) >> 3, x = blockIdx.x & 7u;
+        const uint32_t start = min(x * per, n_tiles);
+        end = min(start + per, n_tiles);
+        step = gridDim.x >> 3;
+        t = start + (blockIdx.x >> 3);
+    }
+    __device__ __forceinline__ bool valid(uint32_t u) const { return u < end; }
+};
+
+// One 16x16 tile's footprint of a same-size A = STD pass: (16 + 2R)^2 BGRA8 words, row-major, clamped to
+// the texture, by LDS DMA into `buf` (each wave-instruction fills 64 consecutive words).
+template <int STD>
+struct FinalStd {
+    static constexpr int RCH = 2 * (STD / 8);  // the taps' reach: |offset| <= 2 * A / 8 texels
+    static constexpr int NX = 16 + 2 * RCH, NN = NX * NX, ROUNDS = (NN + 255) / 256;
+};
+template <int STD>
+__device__ __forceinline__ void stage_final_dma(const CTex& U, uint32_t t, uint32_t tiles_x, uint32_t* buf) {
+    using F = FinalStd<STD>;
+    const uint32_t ty = t / tiles_x, tx = t - ty * tiles_x;
+    const int32_t x0 = (int32_t)tx * 16 - F::RCH, y0 = (int32_t)ty * 16 - F::RCH;
+    const int32_t wm = (int32_t)U.w - 1, hm = (int32_t)U.h - 1;
+#pragma unroll
+    for (int r = 0; r < F::ROUNDS; ++r) {
+        const int32_t i = r * 256 + (int32_t)threadIdx.x;
+        if (r * 256 + (int32_t)(threadIdx.x & ~63u) < F::NN) {  // wave-uniform: whole 64-word runs
+            const int32_t ly = min(i, F::NN - 1) / F::NX, lx = min(i, F::NN - 1) - ly * F::NX;
+            const uint32_t* g = U.px + (size_t)clampi(y0 + ly, 0, hm) * U.w + clampi(x0 + lx, 0, wm);
+            __builtin_amdgcn_global_load_lds(g, buf + r * 256 + (threadIdx.x & ~63u), 4, 0, 0);
+        }
+    }
+}
+// Fused last stage (bloom_final_kernel) with the standard plan A = STD, persistent.
+template <int STD>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7)))
+bloom_final_pkernel(Tables tb, CTex col, CTex Y, CTex U0, TapPlan P, Tex out, uint32_t tiles_x, uint32_t n_tiles) {
+    using F = FinalStd<STD>;
+    static_assert(F::NN % 64 == 0, "whole 64-word DMA runs");
+    __shared__ Lds L;
+    __shared__ uint32_t B0[F::NN], B1[F::NN];
+    TileWalk w(n_tiles);
+    const int32_t lx = (int32_t)(threadIdx.x & 15u), ly = (int32_t)(threadIdx.x >> 4);
+    auto pix = [&](uint32_t t, int32_t& x, int32_t& y) {
+        const uint32_t ty = t / tiles_x;
+        x = (int32_t)(t - ty * tiles_x) * 16 + lx;
+        y = (int32_t)ty * 16 + ly;
+    };
+    auto fetch_px = [&](uint32_t t, uint32_t& yv, uint32_t& cv) {
+        int32_t x, y;
+        pix(t, x, y);
+        const bool in = x < (int32_t)out.w && y < (int32_t)out.h;
+        const size_t i = in ? (size_t)y * out.w + (size_t)x : 0;
+        yv = Y.px[i];
+        cv = col.px[i];
+    };
+    uint32_t yv = 0, cv = 0;
+    if (w.valid(w.t)) {
+        fetch_px(w.t, yv, cv);
+        stage_final_dma<STD>(U0, w.t, tiles_x, B0);
+    }
+    load_tables(tb, L);
+    // one tile from `cur` while the next streams into `nxt` (the loop is unrolled by two so that each
+    // buffer stays a distinct array in the code)
+    auto tile = [&](const uint32_t* cur, uint32_t* nxt) -> bool {
+        if (!w.valid(w.t)) return false;  // block-uniform
+        // cur's DMA (every wave's share) and this tile's pixel loads landed, nxt's last readers are done:
+        // each wave drains its own vector-memory counter first (the compiler does not count the LDS
+        // DMA's writes as LDS stores that the barrier must order), then the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t t = w.t, tn = t + w.step;
+        uint32_t yn = 0, cn = 0;
+        if (w.valid(tn)) {
+            fetch_px(tn, yn, cn);
+            stage_final_dma<STD>(U0, tn, tiles_x, nxt);
+        }
+        int32_t x, y;
+        pix(t, x, y);
+        if (x < (int32_t)out.w && y < (int32_t)out.h) {
+            const int32_t x0 = x - lx - F::RCH, y0 = y - ly - F::RCH;
+            const PlanSrc<F::NX, true, STD> src{U0, cur, x0, y0, &P, &L, x, y};
+            const F4 b3 = quant(L, up8(src, Taps(1u, 1u), 0.0f, 0.0f, 0u));
+            const F4 z = quant(L, remix(dec(L, yv), b3));
+            out.px[(size_t)y * out.w + (size_t)x] = enc(L, remix(dec(L, cv), z));
+        }
+        yv = yn;
+        cv = cn;
+        w.t = tn;
+        return true;
+    };
+    while (tile(B0, B1) && tile(B1, B0)) {
+    }
 }
 
 // The 2:1 form of an 8-tap pass: an up pass from a texture of n texels to 2n pixels along each axis
@@ -959,6 +1106,16 @@ Up2Plan up2_plan(uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx
     return P;
 }
 
+// Grid of a persistent bloom kernel: `per_cu` resident blocks on every CU of the current device, a
+// multiple of 8 (TileWalk splits the tiles into 8 runs).
+uint32_t persistent_grid(uint32_t per_cu) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+        cus = 256;
+    return std::max(8u, ((uint32_t)cus * per_cu) & ~7u);
+}
+
 // The standard plan (see quad_tap_std) a runtime plan equals, or 0: A = 12 or 3 for a 2:1 up pass, A =
 // 12 or 48 for a same-size TapPlan pass.  BH_BLOOM_NO_STD (A/B) disables them.
 static const bool g_no_std = std::getenv("BH_BLOOM_NO_STD") != nullptr;
@@ -1071,7 +1228,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
     // the kernel's with_source takes the TapPlan form exactly when this holds (raw words staged)
     const bool plan = P.valid && P.hi_x - P.lo_x + 16 <= FP_FINAL && P.hi_y - P.lo_y + 16 <= FP_FINAL;
     const size_t lds = (size_t)FP_FINAL * FP_FINAL * (plan ? sizeof(uint32_t) : sizeof(float4));
-    if (plan && std_tap_plan(P) == 48)
+    const bool std48 = plan && std_tap_plan(P) == 48;
+    // persistent blocks: measured no faster; BH_BLOOM_PERSIST=1 takes them (A/B)
+    static const bool persist = std::getenv("BH_BLOOM_PERSIST") != nullptr;
+    const uint32_t tiles_x = (w + 15u) / 16u, n_tiles = tiles_x * ((h + 15u) / 16u);
+    const uint32_t G = persistent_grid(7u);
+    if (std48 && persist && n_tiles >= 2u * G)
+        hipLaunchKernelGGL(bloom_final_pkernel<48>, dim3(G), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
+                           CTex{col, w, h}, CTex{Y, w, h}, CTex{U0, w, h}, P, Tex{out, w, h}, tiles_x, n_tiles);
+    else if (std48)
         hipLaunchKernelGGL(bloom_final_kernel<48>, grid_for(w, h), dim3(256), lds, s, Tables{lut, enc, buckets, codes},
                            CTex{col, w, h}, CTex{Y, w, h}, CTex{U0, w, h}, rx, ry, pm, P, Tex{out, w, h});
     else

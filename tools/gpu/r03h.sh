@@ -13,8 +13,8 @@ b() {  # name [lib] [env]
 }
 for r in 1 2 3; do
   b new_$r
-  b head_$r tools/variants/head.so
-  b nostd_$r "" BH_BLOOM_NO_STD=1
+  b head_$r ${HEADLIB:-tools/variants/head.so}
+  b alt_$r "" ${ALT:-BH_BLOOM_NO_STD=1}
 done
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_new -o run -- python tools/bench_bloom.py --steps 100 > $O/prof_new.log 2>&1 || exit 1
