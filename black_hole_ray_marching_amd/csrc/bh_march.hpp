@@ -1021,6 +1021,13 @@ __device__ __forceinline__ HistLds* hist_lds() {
 
 // March `st` to termination with the fast-forward; `steps` = RK updates actually executed.
 // (The tail waves are latency-bound: a ping-pong / uniform-trip form of this loop measured slower.)
+// Cycles are looked for until iteration CYCLE_ITERS_END only: the ones found start by iteration ~50
+// (median 30); the rays still marching after that crawl or orbit without repeating, and
+// stopping the search never changes a result -- the loop then just runs to its normative end.
+#ifndef BH_CYCLE_ITERS_END
+#define BH_CYCLE_ITERS_END 192u
+#endif
+constexpr uint32_t CYCLE_ITERS_END = BH_CYCLE_ITERS_END;
 template <uint32_t SF>
 __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& steps,
                                                  HistLds& H, uint32_t lane) {
@@ -1035,6 +1042,7 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
         h1 = state_hash(st);
         const uint32_t fate = march_step_tail<SF>(a, f, st);
         if (fate != 0xFFu) { steps = st.n_rk; return fate; }
+        if (st.n_rk >= CYCLE_ITERS_END) break;  // wave-uniform: every live lane is at the same iteration
         if (state_hash(st) == h2) {
             const float4 q0 = H.a[p ^ 1u][0][lane], q1 = H.a[p ^ 1u][1][lane];
             const Hist hs{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z), q0.w, __float_as_uint(q1.w)};
@@ -1049,6 +1057,12 @@ __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame
             }
         }
         h2 = h1;
+    }
+    // past CYCLE_ITERS_END: the plain loop, no history writes or hashes (a lone tail wave's step is
+    // issue-bound, and those were ~8 % of its instructions)
+    for (;;) {
+        const uint32_t fate = march_step_tail<SF>(a, f, st);
+        if (fate != 0xFFu) { steps = st.n_rk; return fate; }
     }
 }
 

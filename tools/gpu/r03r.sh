@@ -1,8 +1,8 @@
 #!/bin/bash
-# round 3: march -- early issue priority for tiles whose previous cost predicts a long march; GPU suite,
-# then interleaved A/B vs the same build without it (tools/variants/noeprio.so)
+# round 3: march A/B -- the working tree against OLDLIB (a variant .so), interleaved, after the GPU suite
+# (OUT names the output directory)
 set -o pipefail
-O=gpurun_out/r03r; mkdir -p $O
+O=gpurun_out/${OUT:-r03r}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 run() {  # name lib args...
@@ -13,15 +13,15 @@ run() {  # name lib args...
 }
 for r in 1 2 3; do
   run c5d1_new_$r base --config 5 --frames-per-launch 1 --steps 100 --warmup 30
-  run c5d1_old_$r tools/variants/noeprio.so --config 5 --frames-per-launch 1 --steps 100 --warmup 30
+  run c5d1_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 5 --frames-per-launch 1 --steps 100 --warmup 30
   run c3_new_$r base --steps 20 --warmup 10
-  run c3_old_$r tools/variants/noeprio.so --steps 20 --warmup 10
+  run c3_old_$r ${OLDLIB:-tools/variants/noeprio.so} --steps 20 --warmup 10
 done
 for r in 1 2; do
   run c3d1_new_$r base --frames-per-launch 1 --steps 100 --warmup 30
-  run c3d1_old_$r tools/variants/noeprio.so --frames-per-launch 1 --steps 100 --warmup 30
+  run c3d1_old_$r ${OLDLIB:-tools/variants/noeprio.so} --frames-per-launch 1 --steps 100 --warmup 30
   run c5_new_$r base --config 5 --steps 20 --warmup 10
-  run c5_old_$r tools/variants/noeprio.so --config 5 --steps 20 --warmup 10
+  run c5_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 5 --steps 20 --warmup 10
   run c2_new_$r base --config 2 --steps 20 --warmup 10
-  run c2_old_$r tools/variants/noeprio.so --config 2 --steps 20 --warmup 10
+  run c2_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 2 --steps 20 --warmup 10
 done
