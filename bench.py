@@ -510,23 +510,24 @@ def main() -> int:
         settle_frames += D
     settle_ms = (time.perf_counter() - t_settle) * 1e3
 
+    # everything the timed region needs is allocated before the warm-up, so that between the last
+    # warm-up launch and the first timed one the GPU idles only for the synchronize (an idle gap of a
+    # millisecond costs the next launch ~10 % of its time while the clock ramps back up)
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    clk = torch.zeros((3, 128), dtype=torch.int64, device=dev)  # shader clock: timed region, extra legs
     for _ in range(args.warmup):
         render(D)
         exchange(D)
     if pipe is not None:
         pipe.drain()
-    torch.cuda.synchronize(dev)
-
-    # shader clock inside the timed launches (bh_set_clock_probe; rows: timed region, extra legs)
-    clk = torch.zeros((3, 128), dtype=torch.int64, device=dev)
+    # the shader-clock probe counts from the next launch on (bh_set_clock_probe); clk was zeroed above
     if graph is None:
         scene.set_clock_probe(clk[0], CLOCK_STRIDE)
 
     # timed region: K steps = K batches of D frames; barrier + synchronize on both sides; HIP events
     # around every launch on the stream the kernel runs on (kernel duration for the roofline)
-    K = args.steps
     first_timed = launch_no[0]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     if sharded:
         dist.barrier()
     torch.cuda.synchronize(dev)
