@@ -499,13 +499,50 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
             out.px[(size_t)y * out.w + x] = enc(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         });
     } else {
+        // The sample's texel coordinates and weights (sample()'s own arithmetic).  Most pixels of a
+        // same-size pass sample a texel centre (weights 0: the sample is that texel, sample_point),
+        // and a 2:1 downsample the middle of 4 texels (weights 1/2: the exact quad form of TapPlan);
+        // those take short forms, the others the general sampler -- the same bits either way.
+        const bool in = x < out.w && y < out.h;
+        const float u = texcoord(in ? x : 0u, Rw), v = texcoord(in ? y : 0u, Rh);
+        const float tx = sample_coord(u, a.w), ty = sample_coord(v, a.h);
+        const float fx = floorf(tx), fy = floorf(ty);
+        const float fa = tx - fx, fb = ty - fy;
+        const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
+        const int32_t x0 = clampi((int32_t)fx, 0, wm), y0 = clampi((int32_t)fy, 0, hm);
+        const int32_t x1 = clampi((int32_t)fx + 1, 0, wm), y1 = clampi((int32_t)fy + 1, 0, hm);
+        const bool centre = fa == 0.0f && fb == 0.0f;
+        if constexpr (SH == SH_COPY || SH == SH_DOWN) {
+            // a copy of a texel centre stores the texel's own word: enc(dec(t)) == t for every BGRA8 word
+            // (sRGB: every code's decode encodes back to it; alpha: unorm8(k/255) == k --
+            // tests/test_oracle.py::test_srgb_round_trip), so a block of centres needs no tables
+            if (barrier_and(!in || centre)) {
+                if (in) out.px[(size_t)y * out.w + x] = a.px[(size_t)y0 * a.w + (size_t)x0];
+                return;
+            }
+        }
         load_tables(tb, L);
-        if (x >= out.w || y >= out.h) return;
-        const float u = texcoord(x, Rw), v = texcoord(y, Rh);
+        if (!in) return;
         const GlobalSrc A{a, &L};
         F4 r;
-        if constexpr (SH == SH_COPY || SH == SH_DOWN) r = sample(A, u, v);
-        else r = remix(sample(A, u, v), sample(GlobalSrc{b, &L}, u, v));
+        if constexpr (SH == SH_COPY || SH == SH_DOWN) {
+            if (centre) {
+                out.px[(size_t)y * out.w + x] = a.px[(size_t)y0 * a.w + (size_t)x0];
+                return;
+            }
+            if (fa == 0.5f && fb == 0.5f) {
+                // (t * 1/2 + t' * 1/2) == (t + t') * 1/2 for decoded texels, twice: ((t00 + t10) + (t01 + t11)) / 4
+                const F4 q00 = A.at(x0, y0), q10 = A.at(x1, y0), q01 = A.at(x0, y1), q11 = A.at(x1, y1);
+                r = {((q00.r + q10.r) + (q01.r + q11.r)) * 0.25f, ((q00.g + q10.g) + (q01.g + q11.g)) * 0.25f,
+                     ((q00.b + q10.b) + (q01.b + q11.b)) * 0.25f, ((q00.a + q10.a) + (q01.a + q11.a)) * 0.25f};
+            } else {
+                r = sample(A, u, v);
+            }
+        } else {
+            const GlobalSrc B{b, &L};
+            if (centre) r = remix(A.at(x0, y0), B.at(x0, y0));
+            else r = remix(sample(A, u, v), sample(B, u, v));
+        }
         out.px[(size_t)y * out.w + x] = enc(L, r);
     }
 }

@@ -174,6 +174,17 @@ def test_srgb_encode_table_matches_definition_exhaustively():
     assert oracle.srgb_table_mismatches(T) == 0
 
 
+def test_srgb_round_trip():
+    """A Bgra8UnormSrgb store of a decoded texel gives back its byte: the normative encode of the sRGB
+    decode table's entry k is k for every k, and the alpha store unorm8(RN_f32(k / 255)) is k (the
+    bloom's literal copy passes store a texel-centre sample as the texel's own word, bh_bloom.hip
+    pass_kernel)."""
+    lut = oracle.srgb_lut()
+    assert np.array_equal(oracle.srgb_encode(lut.astype(np.float32)).astype(np.int64), np.arange(256))
+    a = np.arange(256, dtype=np.float32) / np.float32(255.0)  # RN_f32(k / 255): the alpha decode
+    assert np.array_equal(np.floor(a.astype(np.float64) * 255.0 + 0.5).astype(np.int64), np.arange(256))
+
+
 def test_exit_tests_on_r_squared_equal_tests_on_r():
     # The kernel's blackout/outside tests (bh_march.hpp step_bf) read r2 = dot(ro, ro) instead of
     # r = RN(sqrt(r2)) (src/black_hole_maybe.wgsl:271-283 compares r with 1):
