@@ -241,6 +241,9 @@ struct FOps {
     __device__ __forceinline__ v3 add2(v3 a, v3 b) {  // a + 2b
         return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
     }
+    __device__ __forceinline__ v3 ro_half(v3 ro, v3 k) {  // ro + 0.5 k
+        return mk(__builtin_fmaf(0.5f, k.x, ro.x), __builtin_fmaf(0.5f, k.y, ro.y), __builtin_fmaf(0.5f, k.z, ro.z));
+    }
     template <int K>
     __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
         const float iq = rsq(q), iq2 = iq * iq;
@@ -331,6 +334,20 @@ struct XOps {
             return mk(__builtin_fmaf(2.0f, b.x, a.x), __builtin_fmaf(2.0f, b.y, a.y), __builtin_fmaf(2.0f, b.z, a.z));
         } else {
             return add(a, smul(2.0f, b));
+        }
+    }
+    // ro + 0.5 k, the RK stage positions of k2 and k3 (:140, :143).  CR: fma(0.5, k, ro), one op per
+    // component instead of two, and the same bits on every step whose guard stays clear:
+    //  * where 0.5 k is exact (|k| >= 2^-125) both forms round ro + 0.5 k once;
+    //  * else |0.5 k| < 2^-126: when |ro_i| >= 2^-100 it is below half an ulp of ro_i and both give ro_i;
+    //    when ro_i is 0 or smaller, the stage position is 0 or below 2^-99, so this stage's numerator
+    //    s * p_i (|s| <= 2^30 on a clear step) is 0 or below DIV_N_MIN and `amin` raises the guard: the
+    //    step re-runs in IEEE ops.
+    __device__ __forceinline__ v3 ro_half(v3 ro, v3 k) {
+        if constexpr (CR) {
+            return mk(__builtin_fmaf(0.5f, k.x, ro.x), __builtin_fmaf(0.5f, k.y, ro.y), __builtin_fmaf(0.5f, k.z, ro.z));
+        } else {
+            return add(ro, smul(0.5f, k));
         }
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
@@ -455,9 +472,9 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const v3 ro_k1 = smul(dt, rd);
     const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r));
     const v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
-    const v3 rd_k2 = smul(dt, X.template accel<2>(add(ro, smul(0.5f, ro_k1)), s));
+    const v3 rd_k2 = smul(dt, X.template accel<2>(X.ro_half(ro, ro_k1), s));
     const v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
-    const v3 rd_k3 = smul(dt, X.template accel<3>(add(ro, smul(0.5f, ro_k2)), s));
+    const v3 rd_k3 = smul(dt, X.template accel<3>(X.ro_half(ro, ro_k2), s));
     const v3 ro_k4 = smul(dt, add(rd, rd_k3));
     const v3 rd_k4 = smul(dt, X.template accel<4>(add(ro, ro_k3), s));
     const v3 dro = X.template div6<0>(add(X.add2(X.add2(ro_k1, ro_k2), ro_k3), ro_k4));
@@ -541,6 +558,9 @@ __device__ __forceinline__ p3 pdiv6(p3 x) {
     const p3 e{pfma(y.xy, bc(6.0f), -x.xy), __builtin_fmaf(y.z, 6.0f, -x.z)};
     return {pfma(-e.xy, bc(R6), y.xy), __builtin_fmaf(-e.z, R6, y.z)};
 }
+__device__ __forceinline__ p3 pro_half(p3 ro, p3 k) {  // ro + 0.5 k, as XOps<true>::ro_half
+    return {pfma(bc(0.5f), k.xy, ro.xy), __builtin_fmaf(0.5f, k.z, ro.z)};
+}
 __device__ __forceinline__ p3 padd2(p3 a, p3 b) {  // a + 2b, as XOps<true>::add2
     return {pfma(bc(2.0f), b.xy, a.xy), __builtin_fmaf(2.0f, b.z, a.z)};
 }
@@ -616,9 +636,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const p3 ro_k1 = psmul(dt, rd);
     const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, G));
     const p3 ro_k2 = psmul(dt, padd(rd, psmul(0.5f, rd_k1)));
-    const p3 rd_k2 = psmul(dt, paccel<2>(padd(ro, psmul(0.5f, ro_k1)), s, G));
+    const p3 rd_k2 = psmul(dt, paccel<2>(pro_half(ro, ro_k1), s, G));
     const p3 ro_k3 = psmul(dt, padd(rd, psmul(0.5f, rd_k2)));
-    const p3 rd_k3 = psmul(dt, paccel<3>(padd(ro, psmul(0.5f, ro_k2)), s, G));
+    const p3 rd_k3 = psmul(dt, paccel<3>(pro_half(ro, ro_k2), s, G));
     const p3 ro_k4 = psmul(dt, padd(rd, rd_k3));
     const p3 rd_k4 = psmul(dt, paccel<4>(padd(ro, ro_k3), s, G));
     const p3 sro = padd(padd2(padd2(ro_k1, ro_k2), ro_k3), ro_k4);
@@ -1206,7 +1226,10 @@ __device__ __forceinline__ void clock_end(unsigned long long* acc, const ClockSt
     const uint32_t t = (uint32_t)__builtin_amdgcn_s_memtime() - c0.t;      // shader clock
     const uint32_t r = (uint32_t)__builtin_amdgcn_s_memrealtime() - c0.r;  // constant 100 MHz
     const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;  // HW_REG_XCC_ID[2:0]
-    if ((threadIdx.x & 63u) == 0u) {
+    // a sample whose ratio is outside 0.5-4 GHz is dropped: a wave saved and restored elsewhere (queue
+    // preemption) reads another XCD's shader counter at its end (seen once: 20 GHz on two XCDs)
+    const bool sane = (uint64_t)t >= 5ull * r && (uint64_t)t <= 40ull * r;
+    if ((threadIdx.x & 63u) == 0u && sane) {
         unsigned long long* p = acc + 16u * x;
         __hip_atomic_fetch_add(p, (unsigned long long)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add(p + 1, (unsigned long long)r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
