@@ -94,6 +94,11 @@ __device__ __forceinline__ float div12(float x) { return div6(x) * 0.5f; }
 // min of |n| would be one op cheaper but cannot tell 0 from tiny: measured 2x slower overall,
 // because every camera-A ray starts on two coordinate planes and its first step then re-runs.)
 constexpr uint32_t KEY_MIN = (0x21800000u << 1) - 1u;  // key(2^-60)
+// The march's acceleration numerators s * p_i are held to the stricter 0 or >= 2^-40 (ACC_N_MIN): then
+// every acceleration component is 0 or >= 2^-100 (Q <= 2^60), which the fma form of the RK stage
+// directions relies on (bh_march.hpp, XOps::rd_half).  Still inside the division core's domain.
+constexpr float ACC_N_MIN = 0x1p-40f;
+constexpr uint32_t KEY_ACC_MIN = (0x2B800000u << 1) - 1u;  // key(2^-40)
 __device__ __forceinline__ uint32_t key(float n) { return (__float_as_uint(n) << 1) - 1u; }
 __device__ __forceinline__ uint32_t kmin3(uint32_t a, uint32_t b, uint32_t c) { return min(min(a, b), c); }
 

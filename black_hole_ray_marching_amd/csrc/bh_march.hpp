@@ -244,6 +244,7 @@ struct FOps {
     __device__ __forceinline__ v3 ro_half(v3 ro, v3 k) {  // ro + 0.5 k
         return mk(__builtin_fmaf(0.5f, k.x, ro.x), __builtin_fmaf(0.5f, k.y, ro.y), __builtin_fmaf(0.5f, k.z, ro.z));
     }
+    __device__ __forceinline__ v3 rd_half(v3 rd, v3 k) { return ro_half(rd, k); }
     template <int K>
     __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
         const float iq = rsq(q), iq2 = iq * iq;
@@ -273,7 +274,8 @@ template <bool CR>
 struct XOps {
     static constexpr bool kCR = CR;
     bool bad = false;
-    // Numerator domain of the division cores: 0 or >= DIV_N_MIN in magnitude.  Zeros are legal (the
+    // Numerator domain of the division cores: 0 or >= DIV_N_MIN in magnitude, held to the stricter
+    // ACC_N_MIN for the acceleration numerators (rd_half's premise).  Zeros are legal (the
     // cores are exact for them) and occur in two places:
     //  * k1's numerators s*ro: camera-A rays start on two coordinate planes.  Checked through
     //    crm::key (zeros map high, tiny values low): one v_lshl_add per value + v_min3_u32;
@@ -341,13 +343,25 @@ struct XOps {
     //  * where 0.5 k is exact (|k| >= 2^-125) both forms round ro + 0.5 k once;
     //  * else |0.5 k| < 2^-126: when |ro_i| >= 2^-100 it is below half an ulp of ro_i and both give ro_i;
     //    when ro_i is 0 or smaller, the stage position is 0 or below 2^-99, so this stage's numerator
-    //    s * p_i (|s| <= 2^30 on a clear step) is 0 or below DIV_N_MIN and `amin` raises the guard: the
+    //    s * p_i (|s| <= 2^30 on a clear step) is 0 or below ACC_N_MIN and `amin` raises the guard: the
     //    step re-runs in IEEE ops.
     __device__ __forceinline__ v3 ro_half(v3 ro, v3 k) {
         if constexpr (CR) {
             return mk(__builtin_fmaf(0.5f, k.x, ro.x), __builtin_fmaf(0.5f, k.y, ro.y), __builtin_fmaf(0.5f, k.z, ro.z));
         } else {
             return add(ro, smul(0.5f, k));
+        }
+    }
+    // rd + 0.5 k, the RK stage directions of ro_k2 and ro_k3 (:139, :142), k = rd_k1 or rd_k2 = dt * a.
+    // CR: fma(0.5, k, rd), exact on every clear step: the acceleration numerators are 0 or >= 2^-40
+    // (ACC_N_MIN, and non-zero for k2) and Q <= 2^60, so a_i is 0 or >= 2^-100, and the guard holds dt
+    // to 0 or |dt| >= 2^-25 (step_bf), so k_i is 0 or >= 2^-125: 0.5 k is exact and both forms round the
+    // same sum once.
+    __device__ __forceinline__ v3 rd_half(v3 rd, v3 k) {
+        if constexpr (CR) {
+            return mk(__builtin_fmaf(0.5f, k.x, rd.x), __builtin_fmaf(0.5f, k.y, rd.y), __builtin_fmaf(0.5f, k.z, rd.z));
+        } else {
+            return add(rd, smul(0.5f, k));
         }
     }
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
@@ -471,9 +485,9 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
     const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r));
-    const v3 ro_k2 = smul(dt, add(rd, smul(0.5f, rd_k1)));
+    const v3 ro_k2 = smul(dt, X.rd_half(rd, rd_k1));
     const v3 rd_k2 = smul(dt, X.template accel<2>(X.ro_half(ro, ro_k1), s));
-    const v3 ro_k3 = smul(dt, add(rd, smul(0.5f, rd_k2)));
+    const v3 ro_k3 = smul(dt, X.rd_half(rd, rd_k2));
     const v3 rd_k3 = smul(dt, X.template accel<3>(X.ro_half(ro, ro_k2), s));
     const v3 ro_k4 = smul(dt, add(rd, rd_k3));
     const v3 rd_k4 = smul(dt, X.template accel<4>(add(ro, ro_k3), s));
@@ -483,8 +497,9 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     if constexpr (Ops::kCR) {
         // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
         // |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds every |s*p_i| <= 2^42.
-        X.bad |= X.kmin < crm::KEY_MIN;
-        X.bad |= !(X.amin >= crm::DIV_N_MIN);
+        X.bad |= X.kmin < crm::KEY_ACC_MIN;
+        X.bad |= !(X.amin >= crm::ACC_N_MIN);
+        X.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);  // rd_half's premise
         X.bad |= !(X.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
         X.bad |= !(fabsf(s) <= 0x1p30f);
     }
@@ -635,9 +650,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const float dt = fminf(dist * 0.9f, a.dtm * r);
     const p3 ro_k1 = psmul(dt, rd);
     const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, G));
-    const p3 ro_k2 = psmul(dt, padd(rd, psmul(0.5f, rd_k1)));
+    const p3 ro_k2 = psmul(dt, pro_half(rd, rd_k1));  // rd + 0.5 k: XOps::rd_half
     const p3 rd_k2 = psmul(dt, paccel<2>(pro_half(ro, ro_k1), s, G));
-    const p3 ro_k3 = psmul(dt, padd(rd, psmul(0.5f, rd_k2)));
+    const p3 ro_k3 = psmul(dt, pro_half(rd, rd_k2));
     const p3 rd_k3 = psmul(dt, paccel<3>(pro_half(ro, ro_k2), s, G));
     const p3 ro_k4 = psmul(dt, padd(rd, rd_k3));
     const p3 rd_k4 = psmul(dt, paccel<4>(padd(ro, ro_k3), s, G));
@@ -645,8 +660,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const p3 srd = padd(padd2(padd2(rd_k1, rd_k2), rd_k3), rd_k4);
     G.amin6 = XOps<true>::absmin3(XOps<true>::absmin3(sro.xy.x, sro.xy.y, sro.z), srd.xy.x, srd.xy.y, srd.z);
     const p3 dro = pdiv6(sro), drd = pdiv6(srd);
-    G.bad |= G.kmin < crm::KEY_MIN;
-    G.bad |= !(G.amin >= crm::DIV_N_MIN);
+    G.bad |= G.kmin < crm::KEY_ACC_MIN;
+    G.bad |= !(G.amin >= crm::ACC_N_MIN);
+    G.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);
     G.bad |= !(G.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
     G.bad |= !(fabsf(s) <= 0x1p30f);
     const float ntr = travelled + dt;
