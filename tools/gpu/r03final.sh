@@ -2,7 +2,7 @@
 # round 3 final validation: the GPU suite, smoke(), the default bench, the driver's command, a 2-rank
 # rehearsal with gather verification, and the bloom chain -- each under its own time limit
 set -o pipefail
-O=gpurun_out/r03final; mkdir -p $O
+O=gpurun_out/${OUT:-r03final}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { echo "smoke failed"; tail -20 $O/smoke.log; exit 1; }
@@ -13,7 +13,7 @@ BH_BENCH_REHEARSAL=1 timeout -k 10 300 python bench.py --gpus 2 --steps 20 --war
 timeout -k 10 120 python tools/bench_bloom.py --steps 200 > $O/bloom.json 2> $O/bloom.err || { echo "bloom failed"; tail -10 $O/bloom.err; exit 1; }
 python - <<'PY'
 import json
-O = "gpurun_out/r03final"
+import os; O = "gpurun_out/" + os.environ.get("OUT", "r03final")
 for n in ("bench_default", "bench_driver_cmd", "rehearsal2"):
     d = json.loads(open(f"{O}/{n}.json").read().strip().splitlines()[-1])
     c = d.get("clock") or {}
