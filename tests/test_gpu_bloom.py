@@ -58,15 +58,19 @@ def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     scene.close()
 
 
-@pytest.mark.parametrize("H,W,levels", [(128, 256, 3), (256, 512, 3), (120, 200, 3)])
-def test_bloom_bitexact_any_alpha(torch_cuda, sky_small, H, W, levels):
+@pytest.mark.parametrize("H,W,levels,sparse", [(128, 256, 3, False), (256, 512, 3, False), (120, 200, 3, False),
+                                               (256, 512, 3, True), (512, 1024, 3, True)])
+def test_bloom_bitexact_any_alpha(torch_cuda, sky_small, H, W, levels, sparse):
     """Inputs with every alpha byte (the march writes 255, but bh_bloom takes any BGRA8 texels): the
     exact fma forms of the standard-plan kernels (acc_scaled, clerp, remix) rest on the products by
-    powers of two being exact for every decoded channel, alpha k/255 included."""
-    rng = np.random.default_rng(W * 3 + H)
+    powers of two being exact for every decoded channel, alpha k/255 included.  `sparse`: alpha 255
+    except at a few scattered texels, so that the final pass runs its opaque-block form (alpha folded)
+    and its general form side by side in one frame."""
+    rng = np.random.default_rng(W * 3 + H + int(sparse))
     col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
-    col[..., 3] = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
-    bo[..., 3] = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
+    for t in (col, bo):
+        a = rng.integers(0, 256, size=(H, W), dtype=np.uint8)
+        t[..., 3] = np.where(rng.random((H, W)) < 0.0005, a, 255) if sparse else a
     scene = bh.Scene(16, 16, sky=sky_small)
     for schedule in (bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL):
         got = _gpu_bloom(torch_cuda, scene, col, bo, levels, schedule)
