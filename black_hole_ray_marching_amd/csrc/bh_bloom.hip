@@ -484,6 +484,100 @@ constexpr int FP_UP = 24;     // staged footprint of a generic up pass (taps wit
 constexpr int FP_Y = 24;      // blur1 at full size: taps within +-3 texels (22 x 22)
 constexpr int FP_FINAL = 44;  // the last up pass at res / 4: taps within +-12 texels (42 x 42)
 
+// ---- separable plan of an 8-tap pass (any frame size) -------------------------------------------
+// A tap's texel coordinate along x depends only on the pixel's column (texcoord(x) + du_i, then
+// sample_coord, floor and the clamps), and along y only on its row.  The host evaluates that arithmetic
+// once per launch shape for every column and row (bh_bloom_sep_plan: the kernel's own f32 operations,
+// no contraction) -- per tap and column the two clamped texel columns and the weight, per tap and row
+// the same -- and the kernel reads them instead of recomputing them per pixel: the general sampler's
+// lerps on the general sampler's texels, the same bits.  Used by the up passes whose TapPlan / Up2Plan
+// proofs fail (frame sizes other than powers of two take the literal schedule).
+// Layout (uint2 = (x0 | x1 << 16, bits of the weight)): [tap][column] for the columns, then [tap][row].
+__device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, const float4& t01, const float4& t11,
+                                        float fa, float fb) {
+    const float ia = 1.0f - fa, ib = 1.0f - fb;  // sample()'s operations in its order
+    F4 q;
+    q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+    q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+    q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+    q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+    return q;
+}
+__global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, const uint2* __restrict__ sep,
+                                           Tex out) {
+    __shared__ Lds L;
+    __shared__ float4 tile[FP_UP * FP_UP];
+    __shared__ uint2 colp[8][16], rowp[8][16];
+    const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
+    const uint32_t tx = threadIdx.x & 15u, ty = threadIdx.x >> 4;
+    const uint32_t x = bx + tx, y = by + ty;
+    const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
+    const Taps k(rx, ry);
+    const Span sx = tap_span(bx, min(bx + 15u, out.w - 1u), Rw, k.du_min(), k.du_max(), a.w);
+    const Span sy = tap_span(by, min(by + 15u, out.h - 1u), Rh, k.dv_min(), k.dv_max(), a.h);
+    const bool staged = sx.n <= FP_UP && sy.n <= FP_UP;  // block-uniform
+    // this block's plan entries: 8 taps x 16 columns, 8 taps x 16 rows (thread t: tap t >> 4 of column
+    // or row t & 15, clamped to the frame)
+    {
+        const uint32_t i = threadIdx.x >> 4, j = threadIdx.x & 15u;
+        if (i < 8u) {
+            colp[i][j] = sep[i * out.w + min(bx + j, out.w - 1u)];
+            rowp[i][j] = sep[8u * out.w + i * out.h + min(by + j, out.h - 1u)];
+        }
+    }
+    constexpr int R = (FP_UP * FP_UP + 255) / 256;
+    uint32_t raw[R];
+    const int32_t n = sx.n * sy.n;
+    if (staged) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                raw[r] = a.px[(size_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
+            }
+        }
+    }
+    load_tables(tb, L);  // after the footprint's loads are issued
+    if (staged) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int32_t i = (int32_t)threadIdx.x + r * 256;
+            if (i < n) {
+                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FP_UP + lx] = make_float4(d.r, d.g, d.b, d.a);
+            }
+        }
+        __syncthreads();
+    }
+    if (x >= out.w || y >= out.h) return;
+    F4 s{0.0f, 0.0f, 0.0f, 0.0f};
+    // the taps over a texel source (staged tile or global), one at a time (the sched barrier and the
+    // empty asm on the sums keep the compiler from hoisting later taps' reads or sinking this tap's work)
+    auto taps = [&](auto fetch) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint2 c = colp[i][tx], r = rowp[i][ty];
+            const int32_t x0 = (int32_t)(c.x & 0xFFFFu), x1 = (int32_t)(c.x >> 16);
+            const int32_t y0 = (int32_t)(r.x & 0xFFFFu), y1 = (int32_t)(r.x >> 16);
+            acc(s, lerp_plan(fetch(x0, y0), fetch(x1, y0), fetch(x0, y1), fetch(x1, y1), __uint_as_float(c.y),
+                             __uint_as_float(r.y)), i);
+            asm volatile("" ::"v"(s.r), "v"(s.g), "v"(s.b), "v"(s.a));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    if (staged) {
+        taps([&](int32_t u, int32_t v) { return tile[(v - sy.lo) * FP_UP + (u - sx.lo)]; });
+    } else {
+        taps([&](int32_t u, int32_t v) {
+            const F4 q = dec(L, a.px[(size_t)v * a.w + u]);
+            return make_float4(q.r, q.g, q.b, q.a);
+        });
+    }
+    out.px[(size_t)y * out.w + x] = enc(L, div12(s));
+}
+
 // One render pass of the reference (literal schedule): 16x16 pixels per 256-thread block.
 template <uint32_t SH>
 __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx, uint32_t ry, uint32_t point, TapPlan P,
@@ -1185,6 +1279,36 @@ int std_tap_plan(const TapPlan& P) {
     return 0;
 }
 
+// The separable plan of an 8-tap pass (see up_sep_kernel): 8 * (ow + oh) uint2 entries into `outp`
+// ((x0 | x1 << 16, weight bits) per tap and column, then per tap and row), from the kernel's own f32
+// arithmetic: texcoord (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset,
+// sample_coord, floor and the clamps.  Texture sides above 65535 do not fit and return false.
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                      uint32_t th, uint32_t rx, uint32_t ry,
+                                                                      uint32_t* outp) {
+    if (tw > 65535u || th > 65535u || tw == 0u || th == 0u) return false;
+    const float hx = 0.5f / (float)rx, hy = 0.5f / (float)ry;
+    auto axis = [](uint32_t on, uint32_t tn, float d, uint32_t* o, uint32_t x) {
+        const float u = ((float)x + 0.5f) / (float)on + d;
+        const float t = h_sample_coord(u, tn);
+        const float f = floorf(t);
+        const int32_t hi = (int32_t)tn - 1;
+        const int32_t a0 = std::min(std::max((int32_t)f, 0), hi), a1 = std::min(std::max((int32_t)f + 1, 0), hi);
+        const float w = t - f;
+        uint32_t wb;
+        std::memcpy(&wb, &w, 4);
+        o[0] = (uint32_t)a0 | (uint32_t)a1 << 16;
+        o[1] = wb;
+    };
+    for (int i = 0; i < 8; ++i) {
+        const float du = (hx * (float)((int)((0x12343210u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        const float dv = (hy * (float)((int)((0x10123432u >> (4 * i)) & 15u) - 2)) * 3.0f;
+        for (uint32_t x = 0; x < ow; ++x) axis(ow, tw, du, outp + 2u * ((size_t)i * ow + x), x);
+        for (uint32_t y = 0; y < oh; ++y) axis(oh, th, dv, outp + 2u * (8u * (size_t)ow + (size_t)i * oh + y), y);
+    }
+    return true;
+}
+
 // bit i: tap i of kawase_upsample.wgsl samples texel centres exactly for every pixel of an
 // ow x oh pass over a tw x th texture with resolution uniform (rx, ry)
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(uint32_t ow, uint32_t oh, uint32_t tw,
@@ -1204,7 +1328,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
                                                                          const uint32_t* codes, const uint32_t* a,
                                                                          uint32_t aw, uint32_t ah, const uint32_t* b,
                                                                          uint32_t rx, uint32_t ry, uint32_t* out,
-                                                                         uint32_t ow, uint32_t oh, hipStream_t s) {
+                                                                         uint32_t ow, uint32_t oh, const uint32_t* sep,
+                                                                         hipStream_t s) {
     const Tables tb{lut, enc, buckets, codes};
     const CTex A{a, aw, ah}, B{b ? b : a, aw, ah};
     const Tex O{out, ow, oh};
@@ -1222,6 +1347,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
             }
             return (int)hipGetLastError();
         }
+    }
+    static const bool no_sep = std::getenv("BH_BLOOM_NO_SEP") != nullptr;  // A/B: the per-pixel sampler
+    if (shader == SH_UP && !P.valid && sep && !no_sep) {
+        hipLaunchKernelGGL(up_sep_kernel, grid_for(ow, oh), dim3(256), 0, s, tb, A, rx, ry,
+                           reinterpret_cast<const uint2*>(sep), O);
+        return (int)hipGetLastError();
     }
     switch (shader) {
         case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;

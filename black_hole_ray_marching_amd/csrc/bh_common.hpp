@@ -217,12 +217,17 @@ extern "C" __attribute__((visibility("hidden"))) void bh_srgb_bucket_table(const
 extern "C" __attribute__((visibility("hidden"))) bool bh_srgb_code_table(const float* T257, uint32_t* E);
 // bh_bloom.hip pass shaders (bh::bloom::Shader)
 constexpr uint32_t bh_bloom_shader_copy = 0, bh_bloom_shader_down = 1, bh_bloom_shader_up = 2, bh_bloom_shader_remix = 3;
+// the separable plan of an 8-tap pass (bh_bloom.hip): 8 * (ow + oh) uint2 entries
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                      uint32_t th, uint32_t rx, uint32_t ry,
+                                                                      uint32_t* outp);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32_t shader, const float* lut,
                                                                          const float* enc, const uint8_t* buckets,
                                                                          const uint32_t* codes, const uint32_t* a,
                                                                          uint32_t aw, uint32_t ah, const uint32_t* b,
                                                                          uint32_t rx, uint32_t ry, uint32_t* out,
-                                                                         uint32_t ow, uint32_t oh, hipStream_t s);
+                                                                         uint32_t ow, uint32_t oh, const uint32_t* sep,
+                                                                         hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
                                                                       const uint8_t* buckets, const uint32_t* codes,
                                                                       const uint32_t* X, uint32_t* Y, uint32_t w,

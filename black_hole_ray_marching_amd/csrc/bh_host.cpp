@@ -3,6 +3,7 @@
 // fails with a status code.
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -62,6 +63,8 @@ struct bh_ctx {
     std::vector<FrameTable> frame_tables;
     // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
     std::vector<uint32_t*> bloom_tex;
+    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; };  // bloom separable plans (sep_plan)
+    std::vector<SepPlan> sep_plans;
     uint64_t bloom_key = ~0ull;
     // shader-clock probe of the march launches (bh_set_clock_probe): device accumulators or null
     unsigned long long* clk = nullptr;
@@ -537,6 +540,7 @@ int bh_destroy(bh_ctx* c) {
         if (o.counters) (void)hipFree(o.counters);
     }
     for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
+    for (auto& p : c->sep_plans) (void)hipFree(p.dev);
     for (auto& t : c->frame_tables) free_frame_table(t);
     delete c;
     return BH_OK;
@@ -577,14 +581,38 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
     return p;
 }
 
+// The separable plan of an up pass of this shape (bh_bloom_sep_plan), on the device, built at its first
+// use and kept with the ctx (a few hundred KiB per shape); NULL if the shape does not fit the plan.
+const uint32_t* sep_plan(bh_ctx* c, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry,
+                         int* err) {
+    const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
+    for (const auto& p : c->sep_plans)
+        if (p.key == key) return p.dev;
+    std::vector<uint32_t> h(16u * ((size_t)ow + oh));
+    if (!bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data())) return nullptr;
+    uint32_t* d = nullptr;
+    hipError_t e = hipMalloc(&d, h.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (d) (void)hipFree(d);
+        *err = hip_fail(e, "bloom separable plan");
+        return nullptr;
+    }
+    c->sep_plans.push_back({key, d});
+    return d;
+}
+
 struct BloomRun {
     bh_ctx* c;
     hipStream_t s;
     int err = 0;
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
+        if (err != 0) return;
+        const uint32_t* sep = sh == bh_bloom_shader_up ? sep_plan(c, ow, oh, aw, ah, res[0], res[1], &err) : nullptr;
         if (err == 0)
-            err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh, s);
+            err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
+                                       sep, s);
     }
 };
 

@@ -43,7 +43,10 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         (32, 2048, 3), (1024, 64, 4), (8, 1024, 2), (64, 16, 3),
                                         # odd widths whose same-size sampling is exact (fused chain): the
                                         # quad kernels' paired stores must not assume 8-byte aligned rows
-                                        (64, 65, 3), (33, 129, 3), (65, 33, 2)])
+                                        (64, 65, 3), (33, 129, 3), (65, 33, 2),
+                                        # literal schedule at a display size and on thin frames: the up
+                                        # passes' separable plan (per-column / per-row taps from the host)
+                                        (1080, 1920, 5), (7, 300, 3), (300, 7, 3)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     """AUTO fuses passes for sizes whose same-size sampling is exact (powers of two) and runs the
     literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes.  Power-of-two
