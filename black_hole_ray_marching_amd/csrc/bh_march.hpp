@@ -291,7 +291,12 @@ struct XOps {
     // one min/max over the squared lengths r^2, |ro - cps|^2 and the k-point dot products -- a range
     // of q that implies Q's -- is 5 VALU fewer again but measured 12 % slower at cap 64 and 512 with
     // the same IEEE re-run count: the compiler then interleaves k3's and k4's rsq/rcp chains; the
-    // max-ilp and iterative-ilp scheduling strategies did not recover it.)
+    // max-ilp and iterative-ilp scheduling strategies did not recover it.  Round 3, with machine
+    // scheduling off: one unsigned v_min3_u32 / v_max3_u32 pool over the bit patterns of r^2, rho^2,
+    // the marker and photon-sphere arguments and the k-point q's, range [2^-16, 2^24] (implies every
+    // root's and Q's domain), 286 -> 280 VALU per step and the same re-run count
+    // (tools/diag_slow.py), measured 3.5 % slower on the headline and 11 % on cap 1000 at one frame
+    // per launch (packed tail); a float pool the same; profiles/r03/ab_pool/.)
     uint32_t kmin;  // k1 numerators (keys)
     float amin;     // k2..k4 numerators
     float amin6;    // x/6 numerators

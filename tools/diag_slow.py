@@ -9,10 +9,12 @@ import black_hole_ray_marching_amd as bh
 lib = bh.load()
 lib.bh_diag_slow_counts.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
 sky = bh.synthetic_sky()
-for cam in ("A", "B"):
-    sc = bh.Scene(4096, 2048, sky=sky, max_iters=512, math=bh.BH_MATH_EXACT)
-    if cam == "B":
-        sc.update(bh.Camera.look_at((0.0, 3.0, -20.0), (0.0, 0.0, 0.0), 4096, 2048))
+from bench import CAMERAS  # noqa: E402
+
+for cam, cap in (("A", 512), ("B", 512), ("C", 1000)):
+    sc = bh.Scene(4096, 2048, sky=sky, max_iters=cap, math=bh.BH_MATH_EXACT)
+    if cam != "A":
+        sc.update(bh.Camera.look_at(*CAMERAS[cam], 4096, 2048))
     col = torch.empty((2048, 4096, 4), dtype=torch.float16, device="cuda")
     nrk = torch.empty((2048, 4096), dtype=torch.int16, device="cuda")
     a, b = C.c_uint32(), C.c_uint32()
@@ -21,5 +23,5 @@ for cam in ("A", "B"):
     torch.cuda.synchronize()
     lib.bh_diag_slow_counts(C.byref(a), C.byref(b))
     steps = int(nrk.cpu().numpy().view("uint16").astype("int64").sum())
-    print(f"camera {cam}: lane-steps total {steps}, slow lane-steps {a.value}, slow wave-steps {b.value}, "
+    print(f"camera {cam} cap {cap}: lane-steps total {steps}, slow lane-steps {a.value}, slow wave-steps {b.value}, "
           f"waves {4096*2048//64}")

@@ -24,4 +24,6 @@ for r in 1 2; do
   run c5_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 5 --steps 20 --warmup 10
   run c2_new_$r base --config 2 --steps 20 --warmup 10
   run c2_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 2 --steps 20 --warmup 10
+  run c1_new_$r base --config 1 --steps 20 --warmup 10
+  run c1_old_$r ${OLDLIB:-tools/variants/noeprio.so} --config 1 --steps 20 --warmup 10
 done
