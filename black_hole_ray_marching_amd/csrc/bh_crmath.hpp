@@ -73,21 +73,19 @@ __device__ __forceinline__ float div_core(float n, const Rcp& R) {
 }
 __device__ __forceinline__ bool div_d_bad(float d) { return !(d >= DIV_D_MIN && d <= DIV_D_MAX); }
 
-// ---- division by 6 ----------------------------------------------------------------------------
-// y = x * RN(1/6); q = y + RN(1/6) * (x - 6y): equals RN(x / 6) for every x whose quotient is not
-// subnormal (exhaustively checked over all 2^32 inputs; the residual is formed negated as in
-// div_core so that x = +-0 gives the IEEE zero).  Callers guarantee x == 0 or |x| >= DIV_N_MIN.
-__device__ __forceinline__ float div6(float x) {
-    constexpr float R6 = 1.0f / 6.0f;
-    const float y = x * R6;
-    const float e = __builtin_fmaf(y, 6.0f, -x);
-    return __builtin_fmaf(-e, R6, y);
-}
-
-// ---- numerator magnitude guard ----------------------------------------------------------------
-// x / 12 = (x / 6) / 2: halving is exact for the normal quotients of the div6 domain, so this is
-// RN(x / 12) wherever div6 is RN(x / 6) (checked exhaustively as selftest op 5).
-__device__ __forceinline__ float div12(float x) { return div6(x) * 0.5f; }
+// ---- division by 6 and by 12 ------------------------------------------------------------------
+// 1/D split as H + L: H = RD_f32(1/D), L = RN_f32(1/D - H) > 0.  x/D = fma(x, H, x*L) rounds
+// x*H + RN(x*L) once; that sum is within 2^-47 relative of x/D, while x/D (x a 24-bit significand over
+// 3 * 2^k) is either exact or at least 1/6 ulp away from every rounding midpoint, so the one rounding
+// is RN(x/D).  Two ops instead of the three of y = x*RN(1/D) plus a residual correction.  Both terms
+// carry x's sign (H, L > 0), so x = +-0 gives the IEEE zero.  Exhaustive: equal to IEEE x/6 and
+// x/12 for every finite x with |x| >= 2^-121 and for +-0 (x*L loses bits below that); the callers'
+// domain is x == 0 or |x| >= DIV_N_MIN (selftest ops 1 and 5 on the GPU over all 2^32 patterns,
+// tools/ubench/div_const.c on the host).
+constexpr float R6_H = 0x1.555554p-3f, R6_L = 0x1.555556p-27f;
+constexpr float R12_H = 0x1.555554p-4f, R12_L = 0x1.555556p-28f;
+__device__ __forceinline__ float div6(float x) { return __builtin_fmaf(x, R6_H, x * R6_L); }
+__device__ __forceinline__ float div12(float x) { return __builtin_fmaf(x, R12_H, x * R12_L); }
 
 // key(n) = 2*bits(|n|) - 1 (mod 2^32): +-0 -> 0xFFFFFFFF, tiny -> small, so key(n) < KEY_MIN iff
 // 0 < |n| < DIV_N_MIN; a running v_min3_u32 over keys needs one compare per step.  (A float

@@ -572,11 +572,8 @@ __device__ __forceinline__ p3 pdiv(p3 n, const crm::Rcp& R) {
     const p3 e{pfma(bc(R.d), y.xy, -n.xy), __builtin_fmaf(R.d, y.z, -n.z)};
     return {pfma(-e.xy, bc(R.r), y.xy), __builtin_fmaf(-e.z, R.r, y.z)};
 }
-__device__ __forceinline__ p3 pdiv6(p3 x) {
-    constexpr float R6 = 1.0f / 6.0f;
-    const p3 y{x.xy * bc(R6), x.z * R6};
-    const p3 e{pfma(y.xy, bc(6.0f), -x.xy), __builtin_fmaf(y.z, 6.0f, -x.z)};
-    return {pfma(-e.xy, bc(R6), y.xy), __builtin_fmaf(-e.z, R6, y.z)};
+__device__ __forceinline__ p3 pdiv6(p3 x) {  // crm::div6 per component
+    return {pfma(x.xy, bc(crm::R6_H), x.xy * bc(crm::R6_L)), crm::div6(x.z)};
 }
 __device__ __forceinline__ p3 pro_half(p3 ro, p3 k) {  // ro + 0.5 k, as XOps<true>::ro_half
     return {pfma(bc(0.5f), k.xy, ro.xy), __builtin_fmaf(0.5f, k.z, ro.z)};
