@@ -431,6 +431,15 @@ struct XOps {
 // written (selects).  `in` and `out` may alias only when BRANCHY = false.
 // Scene flags: a kernel instantiated for one flag set (SF) drops the per-step flag selects.
 constexpr uint32_t SF_DYN = 0xFFFFFFFFu;
+// SF_CAM_OUT (with a fixed flag set only): the frame's camera lies outside the unit sphere, so the
+// blackout test reduces to `!(r > 1)` (march_slot picks the instantiation per wave).  Every ray starts
+// at the camera (:363), so at iteration 0 r > 1, no exit fires and `has_been_outside_eh` becomes true;
+// from then on a ray with !(r > 1) returns black through :280-281 whether or not :273-274's
+// `dot(rd, ro) < 0` holds.  The step then needs neither that product nor the `outside` state (kept
+// at 1): -8 VALU per step.
+constexpr uint32_t SF_CAM_OUT = 0x100u;
+constexpr uint32_t sf_scene(uint32_t sf) { return sf == SF_DYN ? SF_DYN : (sf & BH_SCENE_DEFAULT); }
+constexpr bool sf_cam_out(uint32_t sf) { return sf != SF_DYN && (sf & SF_CAM_OUT) != 0u; }
 
 // r > 1 for r = RN(sqrt(r2)) exactly when r2 > 1 + 2^-23 (step_bf)
 constexpr float R2_GT1 = 0x1.000002p0f;
@@ -442,7 +451,9 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
                                         uint32_t& fate, uint32_t it = 0u) {
-    const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
+    constexpr uint32_t SFS = sf_scene(SF);
+    constexpr bool CO = sf_cam_out(SF);
+    const uint32_t scene_flags = (SFS == SF_DYN) ? a.scene_flags : SFS;
     const v3 ro = in.ro, rd = in.rd;
     const float travelled = in.travelled, s = in.s;
     const uint32_t n_rk = in.n_rk;
@@ -462,16 +473,21 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // selects on the test (s_cselect), but the resulting schedule measured 0.7 % faster than the
     // unconditional form (A/B r01, two pairs).  Forcing a real branch materialises the predicates as
     // integers in VGPRs (+8 VALU): slower.
-    bool ingoing = false;
-    if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = dot(rd, ro) < 0.0f;
-    const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
+    bool blackout;
+    if constexpr (CO) {
+        blackout = bo_on & not_out;  // `outside` is 1 from iteration 0 on (SF_CAM_OUT)
+    } else {
+        bool ingoing = false;
+        if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = dot(rd, ro) < 0.0f;
+        blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
+    }
     float rho2, qm;
     const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
     // the root guards of the enabled terms (a disabled term's value is discarded; a kernel built for
     // one flag set drops its arithmetic entirely)
-    if constexpr (SF == SF_DYN || SF == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
-    else if constexpr (SF == BH_SCENE_DISC) X.sq_arg(rho2);
-    else if constexpr (SF == BH_SCENE_MARKERS) X.sq_arg(qm);
+    if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
+    else if constexpr (SFS == BH_SCENE_DISC) X.sq_arg(rho2);
+    else if constexpr (SFS == BH_SCENE_MARKERS) X.sq_arg(qm);
     const bool surface = ds < MIN_DIST;                                // :286-288
     if constexpr (BRANCHY) {
         if (blackout | surface) {
@@ -512,7 +528,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
     const float ntr = travelled + dt;                                  // :324
     out.s = s;
-    out.outside = not_out ? in.outside : 1u;                           // only read when bo_on
+    out.outside = CO ? 1u : (not_out ? in.outside : 1u);               // only read when bo_on
     const bool escape = ntr > a.max_dist;                              // :325-327
     const bool capped = (UNI ? it : n_rk) + 1u >= a.max_iters;         // loop end (:266)
     if constexpr (BRANCHY) {
@@ -610,7 +626,9 @@ __device__ __forceinline__ p3 paccel(p3 p, float s, PkGuard& G) {
 template <uint32_t SF>
 __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
                                           PkGuard& G, uint32_t& fate) {
-    const uint32_t scene_flags = (SF == SF_DYN) ? a.scene_flags : SF;
+    constexpr uint32_t SFS = sf_scene(SF);
+    constexpr bool CO = sf_cam_out(SF);
+    const uint32_t scene_flags = (SFS == SF_DYN) ? a.scene_flags : SFS;
     const p3 ro = pk(in.ro), rd = pk(in.rd);
     const float travelled = in.travelled, s = in.s;
     const uint32_t n_rk = in.n_rk;
@@ -620,9 +638,14 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const float r = crm::sqrt_core(r2);
     const bool bo_on = a.blackout_eh != 0u;
     const bool not_out = !(r2 > R2_GT1);
-    bool ingoing = false;
-    if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = pdot(rd, ro) < 0.0f;
-    const bool blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
+    bool blackout;
+    if constexpr (CO) {
+        blackout = bo_on & not_out;
+    } else {
+        bool ingoing = false;
+        if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = pdot(rd, ro) < 0.0f;
+        blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
+    }
     // sdf (XOps::sdf): disc from rho^2 = x*x + z*z, markers from the near sphere of each pair
     const float rho2 = sq_xy.x + zz0;
     const float rho = crm::sqrt_core(rho2);
@@ -636,9 +659,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const float m = crm::sqrt_core(qm) - 0.5f;
     const float ds = fminf((scene_flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
                            (scene_flags & BH_SCENE_MARKERS) ? m : __builtin_inff());
-    if constexpr (SF == SF_DYN || SF == BH_SCENE_DEFAULT) G.bad |= crm::sqrt_bad2(rho2, qm);
-    else if constexpr (SF == BH_SCENE_DISC) G.bad |= crm::sqrt_bad(rho2);
-    else if constexpr (SF == BH_SCENE_MARKERS) G.bad |= crm::sqrt_bad(qm);
+    if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) G.bad |= crm::sqrt_bad2(rho2, qm);
+    else if constexpr (SFS == BH_SCENE_DISC) G.bad |= crm::sqrt_bad(rho2);
+    else if constexpr (SFS == BH_SCENE_MARKERS) G.bad |= crm::sqrt_bad(qm);
     const bool surface = ds < MIN_DIST;
     if (blackout | surface) {
         fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
@@ -669,7 +692,7 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     G.bad |= !(fabsf(s) <= 0x1p30f);
     const float ntr = travelled + dt;
     out.s = s;
-    out.outside = not_out ? in.outside : 1u;
+    out.outside = CO ? 1u : (not_out ? in.outside : 1u);
     out.ro = unpk(padd(ro, dro));
     out.rd = unpk(padd(rd, drd));
     out.travelled = ntr;
@@ -1116,6 +1139,56 @@ __device__ __forceinline__ void select_outputs(MarchArgs& a, const FrameArgs& F)
     a.dbg_n_rk = F.dbg_n_rk; a.dbg_fate = F.dbg_fate; a.dbg_steps = F.dbg_steps;
 }
 
+// March one ray to its end (the tile schedule's loop): `fate` and `steps` (RK updates executed).
+template <uint32_t SF>
+__device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& fate,
+                                          uint32_t& steps, uint32_t lane) {
+    // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
+    // writes its input, so no per-step register copies).  The lane's final state is the output
+    // of its last iteration, or its input for the fates decided before the RK update: the one of
+    // st / sb with the larger n_rk, once a lane leaving before the RK update has zeroed the
+    // other's n_rk (it may hold a discarded output of the guarded first pass).  The input of
+    // iteration i holds n_rk = i and the other register i - 1 or (i = 0) the same state, so no
+    // per-step flag records where the state is (-6 VALU per step: headline -0.5 %, A/B r02,
+    // profiles/r02c/ab_inb/).  The trip condition is wave-uniform and each lane's iteration is
+    // predicated: with a divergent loop exit the state would be live out of the loop at a
+    // different iteration per lane, which costs a register copy of every state value per
+    // iteration.  (390 -> 370 VALU per step; with the flag template and the guard pooling
+    // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
+    RayState sb = st;
+    bool alive = true;
+    // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
+    // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
+    constexpr uint32_t TRIP_PAIRS = 3;
+    static_assert(PRIO_ITERS % (2u * TRIP_PAIRS) == 0u, "whole trips");
+    for (uint32_t it = 0; it < PRIO_ITERS && __builtin_amdgcn_ballot_w64(alive) != 0ull; it += 2u * TRIP_PAIRS) {
+#pragma unroll
+        for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
+            if (alive) {
+                if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j)) {
+                    alive = false;
+                    if (fate_before_rk(fate)) sb.n_rk = 0u;
+                }
+            }
+            if (alive) {
+                if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u)) {
+                    alive = false;
+                    if (fate_before_rk(fate)) st.n_rk = 0u;
+                }
+            }
+        }
+    }
+    if (sb.n_rk > st.n_rk) st = sb;
+    steps = st.n_rk;
+    if (alive) {
+        // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
+        // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
+        // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
+        __builtin_amdgcn_s_setprio(2);
+        fate = march_cycles<SF>(a, f, st, steps, hist_lds<0>()[threadIdx.x >> 6], lane);
+    }
+}
+
 // Several frames in one launch (bh_render_frames): dispatch slot s is tile s / n_frames of the order
 // in frame s % n_frames, so every frame's expensive tiles start first and one frame's serial tail
 // overlaps the others' bulk instead of ending the launch alone.  Only frame 0
@@ -1158,49 +1231,13 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
-        // Two iterations per trip, ping-ponging the state between st and sb (march_step_io never
-        // writes its input, so no per-step register copies).  The lane's final state is the output
-        // of its last iteration, or its input for the fates decided before the RK update: the one of
-        // st / sb with the larger n_rk, once a lane leaving before the RK update has zeroed the
-        // other's n_rk (it may hold a discarded output of the guarded first pass).  The input of
-        // iteration i holds n_rk = i and the other register i - 1 or (i = 0) the same state, so no
-        // per-step flag records where the state is (-6 VALU per step: headline -0.5 %, A/B r02,
-        // profiles/r02c/ab_inb/).  The trip condition is wave-uniform and each lane's iteration is
-        // predicated: with a divergent loop exit the state would be live out of the loop at a
-        // different iteration per lane, which costs a register copy of every state value per
-        // iteration.  (390 -> 370 VALU per step; with the flag template and the guard pooling
-        // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
-        RayState sb = st;
-        bool alive = true;
-        // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
-        // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
-        constexpr uint32_t TRIP_PAIRS = 3;
-        static_assert(PRIO_ITERS % (2u * TRIP_PAIRS) == 0u, "whole trips");
-        for (uint32_t it = 0; it < PRIO_ITERS && __builtin_amdgcn_ballot_w64(alive) != 0ull; it += 2u * TRIP_PAIRS) {
-#pragma unroll
-            for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
-                if (alive) {
-                    if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j)) {
-                        alive = false;
-                        if (fate_before_rk(fate)) sb.n_rk = 0u;
-                    }
-                }
-                if (alive) {
-                    if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u)) {
-                        alive = false;
-                        if (fate_before_rk(fate)) st.n_rk = 0u;
-                    }
-                }
-            }
-        }
-        if (sb.n_rk > st.n_rk) st = sb;
-        steps = st.n_rk;
-        if (alive) {
-            // A wave still marching after PRIO_ITERS iterations (~4x the mean step count) holds a
-            // photon-sphere ray that may run to the cap: raise its issue priority so its serial chain
-            // is not stretched by the SIMD's other waves (the frame's tail), and watch for cycles.
-            __builtin_amdgcn_s_setprio(2);
-            fate = march_cycles<SF>(a, f, st, steps, hist_lds<0>()[threadIdx.x >> 6], lane);
+        // the camera outside the unit sphere (wave-uniform; 1.01 leaves room for any rounding of |ro0|^2
+        // against the step's own r^2 > 1 + 2^-23 at iteration 0): the step without the ingoing test
+        if constexpr (SF != SF_DYN) {
+            if (dot(f.ro0, f.ro0) > 1.01f) march_ray<SF | SF_CAM_OUT>(a, f, st, fate, steps, lane);
+            else march_ray<SF>(a, f, st, fate, steps, lane);
+        } else {
+            march_ray<SF>(a, f, st, fate, steps, lane);
         }
     }
     if (valid) {

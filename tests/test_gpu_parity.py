@@ -116,6 +116,32 @@ def test_exact_bitexact(torch_cuda, scene_small, sky_small, cam, W, H, cap, flag
     assert_bitexact(g, o)
 
 
+# cameras on both sides of the unit sphere: the general blackout test (r < 1 and ingoing, or !(r > 1)
+# after having been outside) and the camera-outside step (SF_CAM_OUT) with rays plunging through r = 1
+HORIZON_CASES = [
+    ("F", 64, 48, 128, 3, {}),
+    ("F", 64, 48, 128, 0, {}),
+    ("F", 48, 32, 128, 1, {}),
+    ("F2", 64, 48, 128, 3, {}),
+    ("G", 64, 48, 128, 3, {}),
+    ("G", 64, 48, 128, 0, {}),
+    ("H", 64, 48, 128, 3, {}),
+    ("H", 64, 48, 128, 0, {}),
+    ("H", 64, 48, 128, 3, {"blackout_eh": 0}),
+]
+
+
+@pytest.mark.parametrize("schedule", SCHEDULES)
+@pytest.mark.parametrize("cam,W,H,cap,flags,over", HORIZON_CASES)
+def test_exact_bitexact_camera_at_horizon(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over, schedule):
+    cu, U = camera_uniform(cam, W, H), uniforms(**over)
+    g = gpu_render(torch_cuda, scene_small, cu, U, W, H, cap, flags, bh.BH_MATH_EXACT, schedule=schedule)
+    o = oracle_render(cu, U, sky_small, W, H, cap, flags)
+    assert_bitexact(g, o)
+    fates = np.bincount(o[3].ravel(), minlength=4)
+    assert fates[bh.BH_FATE_ESCAPE] > 0 and (fates[bh.BH_FATE_BLACKOUT] > 0) == (over.get("blackout_eh", 1) != 0)
+
+
 @pytest.mark.parametrize("cam,W,H,cap,flags,over", CASES)
 def test_fast_tolerance(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over):
     cu, U = camera_uniform(cam, W, H), uniforms(**over)
