@@ -1031,6 +1031,12 @@ constexpr uint32_t PRIO_ITERS = 48;
 #ifndef BH_WG_WAVES
 #define BH_WG_WAVES 1u
 #endif
+#ifndef BH_SPW
+#define BH_SPW 1u
+#endif
+#ifndef BH_SPW_STRIDED
+#define BH_SPW_STRIDED 0
+#endif
 
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
 // Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
@@ -1298,15 +1304,29 @@ __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs 
     __shared__ float lut[lds_tables<FMT>()];
     load_tables<FMT, 64u * BH_WG_WAVES>(A, lut);
     __syncthreads();
-    const uint32_t slot = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
-    if (slot >= A.n_tiles * A.n_frames) return;  // wave-uniform
-    // one slot in `stride`, rotated by slot / stride: the dispatcher deals workgroups to the 8 XCDs round
-    // robin, so plain multiples of the stride would all land on one XCD
-    const bool probe = A.clk && ((slot + (slot >> 8)) & A.clk_mask) == 0u;
-    ClockStart c0{0u, 0u};
-    if (probe) c0 = clock_start();
-    march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
-    if (probe) clock_end(A.clk, c0);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
+    const uint32_t n_slots = A.n_tiles * A.n_frames;
+#if BH_SPW > 1
+    // A/B variant: BH_SPW dispatch slots per wave, one after the other (consecutive slots, or with
+    // BH_SPW_STRIDED slot w + k * waves): the wave start-up (tables, arguments) paid once per BH_SPW tiles
+    const uint32_t n_waves = (n_slots + BH_SPW - 1u) / BH_SPW;
+    for (uint32_t k = 0; k < BH_SPW; ++k) {
+        const uint32_t slot = BH_SPW_STRIDED ? w + k * n_waves : w * BH_SPW + k;
+        if (slot >= n_slots) return;  // wave-uniform
+        if (k != 0u) __builtin_amdgcn_s_setprio(0);
+#else
+    {
+        const uint32_t slot = w;
+        if (slot >= n_slots) return;  // wave-uniform
+#endif
+        // one slot in `stride`, rotated by slot / stride: the dispatcher deals workgroups to the 8 XCDs
+        // round robin, so plain multiples of the stride would all land on one XCD
+        const bool probe = A.clk && ((slot + (slot >> 8)) & A.clk_mask) == 0u;
+        ClockStart c0{0u, 0u};
+        if (probe) c0 = clock_start();
+        march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
+        if (probe) clock_end(A.clk, c0);
+    }
 }
 
 // ---- schedule BH_SCHED_PERSISTENT: persistent waves with per-lane refill (A/B option) ------------
@@ -1492,7 +1512,8 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
 // atomic on one word is serialised across the 8 XCDs at ~85 M claims/s)
 template <uint32_t FMT, uint32_t SF>
 inline void launch_tile_schedule(const MarchArgs& a, hipStream_t s) {
-    const uint32_t blocks = (a.n_tiles * a.n_frames + (BH_WG_WAVES - 1u)) / BH_WG_WAVES;
+    const uint32_t waves = (a.n_tiles * a.n_frames + (BH_SPW - 1u)) / BH_SPW;
+    const uint32_t blocks = (waves + (BH_WG_WAVES - 1u)) / BH_WG_WAVES;
     hipLaunchKernelGGL((march_tile_kernel<FMT, SF>), dim3(blocks), dim3(64u * BH_WG_WAVES), 0, s, a);
 }
 
