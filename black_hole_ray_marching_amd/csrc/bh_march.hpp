@@ -436,7 +436,8 @@ constexpr uint32_t SF_DYN = 0xFFFFFFFFu;
 // at the camera (:363), so at iteration 0 r > 1, no exit fires and `has_been_outside_eh` becomes true;
 // from then on a ray with !(r > 1) returns black through :280-281 whether or not :273-274's
 // `dot(rd, ro) < 0` holds.  The step then needs neither that product nor the `outside` state (kept
-// at 1): -8 VALU per step.
+// at 1): -8 VALU per step.  march_slot also requires |s| <= 2^30 on every lane of the wave (the
+// division cores' numerator bound, a per-ray constant), so this step does not re-check it.
 constexpr uint32_t SF_CAM_OUT = 0x100u;
 constexpr uint32_t sf_scene(uint32_t sf) { return sf == SF_DYN ? SF_DYN : (sf & BH_SCENE_DEFAULT); }
 constexpr bool sf_cam_out(uint32_t sf) { return sf != SF_DYN && (sf & SF_CAM_OUT) != 0u; }
@@ -522,7 +523,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         X.bad |= !(X.amin >= crm::ACC_N_MIN);
         X.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);  // rd_half's premise
         X.bad |= !(X.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
-        X.bad |= !(fabsf(s) <= 0x1p30f);
+        if constexpr (!CO) X.bad |= !(fabsf(s) <= 0x1p30f);  // SF_CAM_OUT: checked once per wave
     }
 #endif
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
@@ -689,7 +690,7 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     G.bad |= !(G.amin >= crm::ACC_N_MIN);
     G.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);
     G.bad |= !(G.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
-    G.bad |= !(fabsf(s) <= 0x1p30f);
+    if constexpr (!CO) G.bad |= !(fabsf(s) <= 0x1p30f);
     const float ntr = travelled + dt;
     out.s = s;
     out.outside = CO ? 1u : (not_out ? in.outside : 1u);
@@ -1041,9 +1042,22 @@ constexpr uint32_t PRIO_ITERS = 48;
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
 // Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
 // the centre-out permutation; each wave records its tile's max n_rk for the next frame's order.
+// Max over the wave's 64 lanes, every lane active: an inclusive DPP scan (row_shr 1/2/4/8 within each
+// 16-lane row, then row_bcast:15 and row_bcast:31 across rows) leaves the max in lane 63.  Out-of-range
+// DPP sources read 0, the identity of an unsigned max.  (__shfl_xor: six ds_bpermute round trips and
+// ~36 VALU of index arithmetic.)
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v) {
+    return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false));
+}
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    v = dpp_max_step<0x111>(v);         // row_shr:1
+    v = dpp_max_step<0x112>(v);         // row_shr:2
+    v = dpp_max_step<0x114>(v);         // row_shr:4
+    v = dpp_max_step<0x118>(v);         // row_shr:8
+    v = dpp_max_step<0x142, 0xa>(v);    // row_bcast:15 into rows 1 and 3
+    v = dpp_max_step<0x143, 0xc>(v);    // row_bcast:31 into rows 2 and 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 // ---- cycle fast-forward ----------------------------------------------------------------------------
@@ -1237,10 +1251,12 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
     if (valid) {
-        // the camera outside the unit sphere (wave-uniform; 1.01 leaves room for any rounding of |ro0|^2
-        // against the step's own r^2 > 1 + 2^-23 at iteration 0): the step without the ingoing test
+        // the camera outside the unit sphere (1.01 leaves room for any rounding of |ro0|^2 against the
+        // step's own r^2 > 1 + 2^-23 at iteration 0) and |s| <= 2^30 on every lane: the step without the
+        // ingoing test and the |s| guard (wave-uniform: a scalar branch)
         if constexpr (SF != SF_DYN) {
-            if (dot(f.ro0, f.ro0) > 1.01f) march_ray<SF | SF_CAM_OUT>(a, f, st, fate, steps, lane);
+            const bool out = (dot(f.ro0, f.ro0) > 1.01f) & (__builtin_amdgcn_ballot_w64(!(fabsf(st.s) <= 0x1p30f)) == 0ull);
+            if (__builtin_amdgcn_readfirstlane((int)out)) march_ray<SF | SF_CAM_OUT>(a, f, st, fate, steps, lane);
             else march_ray<SF>(a, f, st, fate, steps, lane);
         } else {
             march_ray<SF>(a, f, st, fate, steps, lane);
