@@ -184,6 +184,24 @@ constexpr uint32_t ORDER_WORDS = 2 * ORDER_BUCKETS + 1;
 __host__ __device__ inline uint32_t cost_bucket(uint32_t c) {
     return c >= 128u ? 0u : c >= 64u ? 1u : c >= 32u ? 2u : c >= 20u ? 3u : c >= 12u ? 4u : 5u;
 }
+
+// Max over the wave's 64 lanes, every lane active: an inclusive DPP scan (row_shr 1/2/4/8 within each
+// 16-lane row, then row_bcast:15 and row_bcast:31 across rows) leaves the max in lane 63.  Out-of-range
+// DPP sources read 0, the identity of an unsigned max.  (__shfl_xor: six ds_bpermute round trips and
+// ~36 VALU of index arithmetic.)
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v) {
+    return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = dpp_max_step<0x111>(v);         // row_shr:1
+    v = dpp_max_step<0x112>(v);         // row_shr:2
+    v = dpp_max_step<0x114>(v);         // row_shr:4
+    v = dpp_max_step<0x118>(v);         // row_shr:8
+    v = dpp_max_step<0x142, 0xa>(v);    // row_bcast:15 into rows 1 and 3
+    v = dpp_max_step<0x143, 0xc>(v);    // row_bcast:31 into rows 2 and 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 }  // namespace bh
 
 // Launchers (defined in the .hip translation units).

@@ -1042,23 +1042,7 @@ constexpr uint32_t PRIO_ITERS = 48;
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
 // Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
 // the centre-out permutation; each wave records its tile's max n_rk for the next frame's order.
-// Max over the wave's 64 lanes, every lane active: an inclusive DPP scan (row_shr 1/2/4/8 within each
-// 16-lane row, then row_bcast:15 and row_bcast:31 across rows) leaves the max in lane 63.  Out-of-range
-// DPP sources read 0, the identity of an unsigned max.  (__shfl_xor: six ds_bpermute round trips and
-// ~36 VALU of index arithmetic.)
-template <int CTRL, int ROW_MASK = 0xf>
-__device__ __forceinline__ uint32_t dpp_max_step(uint32_t v) {
-    return max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false));
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    v = dpp_max_step<0x111>(v);         // row_shr:1
-    v = dpp_max_step<0x112>(v);         // row_shr:2
-    v = dpp_max_step<0x114>(v);         // row_shr:4
-    v = dpp_max_step<0x118>(v);         // row_shr:8
-    v = dpp_max_step<0x142, 0xa>(v);    // row_bcast:15 into rows 1 and 3
-    v = dpp_max_step<0x143, 0xc>(v);    // row_bcast:31 into rows 2 and 3
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
+// wave_max_u32: bh_common.hpp
 
 // ---- cycle fast-forward ----------------------------------------------------------------------------
 // One loop iteration is a pure function of (ro, rd, travelled, outside) (s and the uniforms are
@@ -1255,7 +1239,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
         // step's own r^2 > 1 + 2^-23 at iteration 0) and |s| <= 2^30 on every lane: the step without the
         // ingoing test and the |s| guard (wave-uniform: a scalar branch)
         if constexpr (SF != SF_DYN) {
-            const bool out = (dot(f.ro0, f.ro0) > 1.01f) & (__builtin_amdgcn_ballot_w64(!(fabsf(st.s) <= 0x1p30f)) == 0ull);
+            const bool out = (dot(f.ro0, f.ro0) > 1.01f) && (__builtin_amdgcn_ballot_w64(!(fabsf(st.s) <= 0x1p30f)) == 0ull);
             if (__builtin_amdgcn_readfirstlane((int)out)) march_ray<SF | SF_CAM_OUT>(a, f, st, fate, steps, lane);
             else march_ray<SF>(a, f, st, fate, steps, lane);
         } else {

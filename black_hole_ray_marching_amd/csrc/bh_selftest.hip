@@ -39,6 +39,7 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 //       `count` random (y, x) pairs seeded by base: random directions, random magnitudes, and the
 //       special values (+-0, axes, diagonals, tiny); ex[0..3] of a mismatch = y, x, got, want
 // op 9: the unit-vector pairs of op 8 (10 of every 16); counts how many the core hands to the fallback
+// op 11: wave_max_u32 (DPP scan) against a serial max, `count` rounds per wave
 // op 7: div_core over EVERY pair of significands (n, d) in [1, 2)^2 with d's 23 fraction bits in
 //       [base, base + count / 2^23): all 2^23 numerators per denominator (the full 2^46 square is
 //       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
@@ -46,6 +47,23 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
                                                       unsigned long long* cnt, uint32_t* ex, const float* T,
                                                       const uint8_t* B, const uint32_t* E) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    if (op == 11) {
+        // wave_max_u32 (bh_common.hpp, the DPP row scan of the tile costs) against a serial max over
+        // the wave's lanes read one by one: `count` rounds of random values per wave (full waves: the
+        // block is 256 threads), seeded by base; magnitudes from 0 to 2^32 - 1, often shared maxima
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        for (uint64_t r = 0; r < count; ++r) {
+            const uint64_t h = mix64((base + r) * 0x9E3779B97F4A7C15ull ^ ((w << 6) | lane));
+            uint32_t v = (uint32_t)h >> ((h >> 32) & 31u);
+            if (((h >> 40) & 7u) == 0u) v &= 0xFFu;
+            const uint32_t got = wave_max_u32(v);
+            uint32_t want = 0;
+            for (int l = 0; l < 64; ++l) want = max(want, (uint32_t)__builtin_amdgcn_readlane((int)v, l));
+            if (lane == 0u && got != want) record(cnt, ex, (uint32_t)w, (uint32_t)r, got, want);
+        }
+        return;
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
         if (op == 0) {
             const uint32_t bits = (uint32_t)(base + i);
@@ -149,7 +167,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 10 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 11 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;

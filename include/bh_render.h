@@ -342,7 +342,9 @@ int bh_srgb_encode_table(float* out257);
  * [base, base + count/2^23); op 8: the shading's f32-rounded atan2 (short f64 core + library fallback)
  * against (float)atan2((double)y, (double)x) on `count` random (y, x) pairs seeded by base; op 9:
  * the number of those pairs the core hands to the fallback; op 10: the bloom chain's code-table form of
- * the sRGB encoder against op 4's over bit patterns [base, base+count)).  *out_mismatches = number of differing results;
+ * the sRGB encoder against op 4's over bit patterns [base, base+count); op 11: the march kernel's
+ * wave-wide max of the tile costs (DPP scan) against a serial max, `count` random rounds per wave
+ * seeded by base).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

@@ -97,3 +97,10 @@ def test_atan2_core_fallback_is_rare(lib):
     n = 1 << 28
     m, _ = run(lib, 9, 7, n)
     assert m < n * 10 // 16 * 1e-5, m
+
+
+def test_wave_max_dpp(lib):
+    # the tile-cost reduction of the march kernel (bh_common.hpp wave_max_u32: DPP row_shr / row_bcast
+    # scan) against a serial max over the 64 lanes, 64 rounds of random values on every wave of the grid
+    m, ex = run(lib, 11, 0x5EED, 64)
+    assert m == 0, ex
