@@ -121,7 +121,8 @@ template <bool A1 = false>
 __device__ __forceinline__ F4 dec(const Lds& L, uint32_t t) {
     return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : L.alut[t >> 24]};
 }
-__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// lo <= hi: one v_med3_i32
+__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return min(max(v, lo), hi); }
 
 __device__ __forceinline__ uint32_t unorm8(float a) {
     // branch-free: the conversion of an out-of-range a is discarded by the selects

@@ -133,13 +133,16 @@ struct Ray {
     uint32_t fate;
 };
 
+// x, y clamped to the texture; 32-bit element index (bh_create: at most 2^30 texels), so the gather
+// address is one 32-bit multiply-add and one 64-bit shift-add
 __device__ __forceinline__ uint32_t texel_u32(const MarchArgs& a, int32_t x, int32_t y) {
-    return a.sky[(size_t)y * a.sky_w + (size_t)x];
+    return a.sky[(uint32_t)y * a.sky_w + (uint32_t)x];
 }
 __device__ __forceinline__ v3 decode(const float* lut, uint32_t t) {
     return mk(lut[t & 0xffu], lut[(t >> 8) & 0xffu], lut[(t >> 16) & 0xffu]);
 }
-__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+// lo <= hi: one v_med3_i32
+__device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return min(max(v, lo), hi); }
 
 // textureSampleLevel(t_diffuse, s_diffuse, uv, 0) on Rgba8UnormSrgb, mag=Linear, clamp-to-edge
 // (src/texture.rs:41,62-70): decode texels, then bilinear with fp32 weights.
@@ -147,8 +150,9 @@ __device__ __forceinline__ v3 sample_sky(const MarchArgs& a, const float* lut, f
     if (u != u || v != v) return decode(lut, texel_u32(a, 0, 0));  // Q8
     float tx = u * (float)a.sky_w - 0.5f;
     float ty = v * (float)a.sky_h - 0.5f;
-    tx = fminf(fmaxf(tx, -1.0f), (float)a.sky_w);
-    ty = fminf(fmaxf(ty, -1.0f), (float)a.sky_h);
+    // fminf(fmaxf(t, -1), n) for the non-NaN t here: one v_med3_f32
+    tx = __builtin_amdgcn_fmed3f(tx, -1.0f, (float)a.sky_w);
+    ty = __builtin_amdgcn_fmed3f(ty, -1.0f, (float)a.sky_h);
     float fx0 = floorf(tx), fy0 = floorf(ty);
     float fa = tx - fx0, fb = ty - fy0;
     int32_t x0 = (int32_t)fx0, y0 = (int32_t)fy0;
@@ -1015,8 +1019,9 @@ __device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab
     write_pixel<FMT>(a, tab, idx, col, n_rk, fate, n_rk);
 }
 
-__device__ __forceinline__ size_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
-    return (a.layout != BH_LAYOUT_ROWMAJOR) ? (size_t)t * 64u + lane : (size_t)py * a.width + px;
+// 32-bit pixel index: width, height <= 65536 (bh_render), so py * W + px < 2^32; a shard holds < 2^24 tiles
+__device__ __forceinline__ uint32_t out_index(const MarchArgs& a, uint32_t t, uint32_t lane, uint32_t px, uint32_t py) {
+    return (a.layout != BH_LAYOUT_ROWMAJOR) ? t * 64u + lane : py * a.width + px;
 }
 
 // Iterations after which a still-marching wave raises its issue priority (the frame's tail: measured
