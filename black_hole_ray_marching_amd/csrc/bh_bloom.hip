@@ -165,7 +165,7 @@ struct GlobalSrc {
     static constexpr bool kA1 = false;
     CTex t;
     const Lds* L;
-    __device__ __forceinline__ F4 at(int32_t x, int32_t y) const { return dec(*L, t.px[(size_t)y * t.w + x]); }
+    __device__ __forceinline__ F4 at(int32_t x, int32_t y) const { return dec(*L, t.px[(uint32_t)y * t.w + x]); }
 };
 template <int FP>
 struct TileSrc {
@@ -180,9 +180,10 @@ struct TileSrc {
 };
 
 // clamp-to-edge bilinear of decoded texels at texcoord (u, v) (oracle: sample)
+// (t is never NaN: texcoords come from pixel indices) fminf(fmaxf(t, -1), n) as one v_med3_f32
 __device__ __forceinline__ float sample_coord(float u, uint32_t n) {
     const float t = u * (float)n - 0.5f;
-    return fminf(fmaxf(t, -1.0f), (float)n);
+    return __builtin_amdgcn_fmed3f(t, -1.0f, (float)n);
 }
 template <class Src>
 __device__ __forceinline__ F4 sample(const Src& src, float u, float v) {
@@ -415,7 +416,7 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
                 const int32_t ly = ty + 16 * a, lx = tx + 16 * b;
                 raw[a][b] = 0xFF000000u;
                 if (ly < ny && lx < nx)
-                    raw[a][b] = t.px[(size_t)clampi(y0 + ly, 0, hm) * t.w + clampi(x0 + lx, 0, wm)];
+                    raw[a][b] = t.px[(uint32_t)clampi(y0 + ly, 0, hm) * t.w + clampi(x0 + lx, 0, wm)];
             }
         load_tables(tb, L);
 #pragma unroll
@@ -455,7 +456,7 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
             const int32_t i = (int32_t)threadIdx.x + r * 256;
             if (i < n) {
                 const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-                raw[r] = t.px[(size_t)(sy.lo + ly) * t.w + (sx.lo + lx)];
+                raw[r] = t.px[(uint32_t)(sy.lo + ly) * t.w + (sx.lo + lx)];
             }
         }
         load_tables(tb, L);
@@ -535,7 +536,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
             const int32_t i = (int32_t)threadIdx.x + r * 256;
             if (i < n) {
                 const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-                raw[r] = a.px[(size_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
+                raw[r] = a.px[(uint32_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
             }
         }
     }
@@ -572,11 +573,11 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
         taps([&](int32_t u, int32_t v) { return tile[(v - sy.lo) * FP_UP + (u - sx.lo)]; });
     } else {
         taps([&](int32_t u, int32_t v) {
-            const F4 q = dec(L, a.px[(size_t)v * a.w + u]);
+            const F4 q = dec(L, a.px[(uint32_t)v * a.w + u]);
             return make_float4(q.r, q.g, q.b, q.a);
         });
     }
-    out.px[(size_t)y * out.w + x] = enc(L, div12(s));
+    out.px[(uint32_t)y * out.w + x] = enc(L, div12(s));
 }
 
 // One render pass of the reference (literal schedule): 16x16 pixels per 256-thread block.
@@ -591,7 +592,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
         const Taps k(rx, ry);
         with_source<FP_UP>(tb, a, L, tile, k, out.w, out.h, Rw, Rh, P, [&](const auto& src) {
             if (x >= out.w || y >= out.h) return;
-            out.px[(size_t)y * out.w + x] = enc(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
+            out.px[(uint32_t)y * out.w + x] = enc(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
         });
     } else {
         // The sample's texel coordinates and weights (sample()'s own arithmetic).  Most pixels of a
@@ -612,7 +613,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
             // (sRGB: every code's decode encodes back to it; alpha: unorm8(k/255) == k --
             // tests/test_oracle.py::test_srgb_round_trip), so a block of centres needs no tables
             if (barrier_and(!in || centre)) {
-                if (in) out.px[(size_t)y * out.w + x] = a.px[(size_t)y0 * a.w + (size_t)x0];
+                if (in) out.px[(uint32_t)y * out.w + x] = a.px[(uint32_t)y0 * a.w + (uint32_t)x0];
                 return;
             }
         }
@@ -622,7 +623,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
         F4 r;
         if constexpr (SH == SH_COPY || SH == SH_DOWN) {
             if (centre) {
-                out.px[(size_t)y * out.w + x] = a.px[(size_t)y0 * a.w + (size_t)x0];
+                out.px[(uint32_t)y * out.w + x] = a.px[(uint32_t)y0 * a.w + (uint32_t)x0];
                 return;
             }
             if (fa == 0.5f && fb == 0.5f) {
@@ -638,7 +639,7 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
             if (centre) r = remix(A.at(x0, y0), B.at(x0, y0));
             else r = remix(sample(A, u, v), sample(B, u, v));
         }
-        out.px[(size_t)y * out.w + x] = enc(L, r);
+        out.px[(uint32_t)y * out.w + x] = enc(L, r);
     }
 }
 
@@ -652,7 +653,7 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
     with_source<FP_Y>(tb, X, L, tile, k, Y.w, Y.h, Rw, Rh, P, [&](const auto& src) {
         if (x >= Y.w || y >= Y.h) return;
         const F4 b1 = quant(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
-        Y.px[(size_t)y * Y.w + x] = enc(L, remix(src.at((int32_t)x, (int32_t)y), b1));
+        Y.px[(uint32_t)y * Y.w + x] = enc(L, remix(src.at((int32_t)x, (int32_t)y), b1));
     });
 }
 
@@ -698,7 +699,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
-            if (ly < ny) raw[r] = X.px[(size_t)clampi(y0 + ly, 0, hm) * X.w + clampi(x0 + lx, 0, wm)];
+            if (ly < ny) raw[r] = X.px[(uint32_t)clampi(y0 + ly, 0, hm) * X.w + clampi(x0 + lx, 0, wm)];
         }
         load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
 #pragma unroll
@@ -729,11 +730,11 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
                 c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
             }
             if (full) {
-                *reinterpret_cast<uint2*>(Y.px + (size_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
+                *reinterpret_cast<uint2*>(Y.px + (uint32_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
             } else {
 #pragma unroll
                 for (int a = 0; a < 2; ++a)
-                    if (x + a < Y.w && y + b < Y.h) Y.px[(size_t)(y + b) * Y.w + x + a] = c[a];
+                    if (x + a < Y.w && y + b < Y.h) Y.px[(uint32_t)(y + b) * Y.w + x + a] = c[a];
             }
         }
     };
@@ -780,7 +781,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
     const Taps k(rx, ry);
     // the pixel's own Y and col texels: loaded before the footprint and the tables, used last
     const bool in = x < out.w && y < out.h;
-    const size_t i = (size_t)y * out.w + x;
+    const uint32_t i = (uint32_t)y * out.w + x;
     const uint32_t yv = in ? Y.px[i] : 0u, cv = in ? col.px[i] : 0u;
     with_source<FP_FINAL, true, STD>(
         tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P,
@@ -833,7 +834,7 @@ __device__ __forceinline__ void stage_final_dma(const CTex& U, uint32_t t, uint3
         const int32_t i = r * 256 + (int32_t)threadIdx.x;
         if (r * 256 + (int32_t)(threadIdx.x & ~63u) < F::NN) {  // wave-uniform: whole 64-word runs
             const int32_t ly = min(i, F::NN - 1) / F::NX, lx = min(i, F::NN - 1) - ly * F::NX;
-            const uint32_t* g = U.px + (size_t)clampi(y0 + ly, 0, hm) * U.w + clampi(x0 + lx, 0, wm);
+            const uint32_t* g = U.px + (uint32_t)clampi(y0 + ly, 0, hm) * U.w + clampi(x0 + lx, 0, wm);
             __builtin_amdgcn_global_load_lds(g, buf + r * 256 + (threadIdx.x & ~63u), 4, 0, 0);
         }
     }
@@ -857,7 +858,7 @@ bloom_final_pkernel(Tables tb, CTex col, CTex Y, CTex U0, TapPlan P, Tex out, ui
         int32_t x, y;
         pix(t, x, y);
         const bool in = x < (int32_t)out.w && y < (int32_t)out.h;
-        const size_t i = in ? (size_t)y * out.w + (size_t)x : 0;
+        const uint32_t i = in ? (uint32_t)y * out.w + (uint32_t)x : 0;
         yv = Y.px[i];
         cv = col.px[i];
     };
@@ -889,7 +890,7 @@ bloom_final_pkernel(Tables tb, CTex col, CTex Y, CTex U0, TapPlan P, Tex out, ui
             const PlanSrc<F::NX, true, STD> src{U0, cur, x0, y0, &P, &L, x, y};
             const F4 b3 = quant(L, up8(src, Taps(1u, 1u), 0.0f, 0.0f, 0u));
             const F4 z = quant(L, remix(dec(L, yv), b3));
-            out.px[(size_t)y * out.w + (size_t)x] = enc(L, remix(dec(L, cv), z));
+            out.px[(uint32_t)y * out.w + (uint32_t)x] = enc(L, remix(dec(L, cv), z));
         }
         yv = yn;
         cv = cn;
@@ -1026,7 +1027,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
             const int32_t i = (int32_t)threadIdx.x + r * 256;
             if (i < n) {
                 const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-                raw[r] = a.px[(size_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
+                raw[r] = a.px[(uint32_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
             }
         }
         load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
@@ -1054,7 +1055,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
             const float u = texcoord(px, Rw), v = texcoord(py, Rh);
             const F4 r = staged ? up8(TileSrc<FP_UPQ>{a, tile, sx.lo, sy.lo}, k, u, v, point)
                                 : up8(GlobalSrc{a, &L}, k, u, v, point);
-            out.px[(size_t)py * out.w + px] = enc(L, r);
+            out.px[(uint32_t)py * out.w + px] = enc(L, r);
         }
         return;
     }
@@ -1081,7 +1082,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
         uint2 w;
         w.x = enc(L, div12(s[b][0]));
         w.y = enc(L, div12(s[b][1]));
-        *reinterpret_cast<uint2*>(out.px + (size_t)(y + b) * out.w + x) = w;  // x even: 8-byte aligned
+        *reinterpret_cast<uint2*>(out.px + (uint32_t)(y + b) * out.w + x) = w;  // x even: 8-byte aligned
     }
 }
 

@@ -622,7 +622,9 @@ extern "C" {
 
 int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint32_t H, uint32_t levels,
              uint32_t schedule, void* out, void* stream) {
-    if (!c || !col || !blackout || !out || W == 0 || H == 0 || levels < 1 || levels > 12 || schedule > BH_BLOOM_LITERAL)
+    // W, H <= 65536 as bh_render: the bloom kernels index texels with 32 bits (y * w + x < 2^32)
+    if (!c || !col || !blackout || !out || W == 0 || H == 0 || W > 65536u || H > 65536u || levels < 1 || levels > 12 ||
+        schedule > BH_BLOOM_LITERAL)
         return BH_ERR_INVALID_ARG;
     hipError_t e;
     DeviceScope dev(c->device);

@@ -259,8 +259,8 @@ int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* ca
 
 /* Bloom::render (src/bloom.rs:53-71): the reference's Kawase bloom + remix chain over the scene's two
  * targets, on BGRA8-sRGB images (bh_render with BH_OUT_BGRA8_SRGB): `col` (full_image_input),
- * `blackout` (blackout_input) -> `out` (the surface), all width x height, row-major, device memory.
- * `levels` = the Bloom's level count (src/state.rs:125 uses 3; 1..12).  Scratch textures live in
+ * `blackout` (blackout_input) -> `out` (the surface), all width x height (1..65536 each, as bh_render),
+ * row-major, device memory.  `levels` = the Bloom's level count (src/state.rs:125 uses 3; 1..12).  Scratch textures live in
  * the context (allocated at the first call for a size).  `schedule`: BH_BLOOM_AUTO fuses passes
  * whenever that gives identical bytes (always for power-of-two sizes), BH_BLOOM_LITERAL runs the
  * reference's render passes one by one.  Asynchronous on `hip_stream`. */

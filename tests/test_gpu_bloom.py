@@ -112,6 +112,9 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
         scene.bloom(t, t, t, levels=0)
     with pytest.raises(bh.BhError):
         scene.bloom(t, t, t, schedule=7)
+    big = torch_cuda.zeros((1, 65537, 4), dtype=torch_cuda.uint8, device="cuda")
+    with pytest.raises(bh.BhError):  # width, height <= 65536: the kernels index texels with 32 bits
+        scene.bloom(big, big, big, width=65537, height=1)
     scene.close()
 
 
