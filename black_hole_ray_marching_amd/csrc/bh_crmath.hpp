@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t kmin3(uint32_t a, uint32_t b, uint32_t c) { 
 // (RN-accurate quotient), and atan(u) = u + u^3 P(u^2) with an 11-term Chebyshev fit on
 // [0, tan^2(pi/8)] (approximation error 2^-57, f64 evaluation ~2^-53; tools/atan2_coefs.py).  Its
 // relative error is below 2^-50, so RN_f32(A) equals RN_f32 of any f64 atan2 within an ulp of the
-// true angle unless A lies within 2^-45 |A| of an f32 rounding midpoint: atan2_near_mid flags those
+// true angle unless A lies within 128 f64 ulps of an f32 rounding midpoint: `near` flags those
 // (and zeros, tiny and non-finite cases) for the caller's fallback to the library call.
 constexpr double ATAN_P[11] = {-0x1.3a31b1c0fd3b7p-6, 0x1.4162c02b1dda3p-5, -0x1.a0999c632b6edp-5,
                                0x1.dfe6497e96323p-5, -0x1.10fa77b1a6d57p-4, 0x1.3b1263064f6b9p-4,
@@ -149,13 +149,15 @@ __device__ __forceinline__ Atan2 atan2_core(float yf, float xf) {
     a = __builtin_signbit(x) ? PI_F64 - a : a;
     a = __builtin_copysign(a, y);
     const float f = (float)a;
-    // distance of A to the nearest f32 rounding midpoints around f (half an ulp of f; a quarter on the
-    // side below a power of two), exact in f64 (Sterbenz)
-    const double d = fabs(a - (double)f);
-    const double h = __builtin_ldexp(1.0, __builtin_amdgcn_frexp_expf(f) - 25);
-    const double tol = fabs(a) * 0x1p-45;
-    const bool near = (x != x) || (y != y) || !(mx > 0.0 && mx < 0x1p200) || !(fabs(a) >= 0x1p-120) ||
-                      fabs(d - h) <= tol || fabs(d - 0.5 * h) <= tol;
+    // Distance of A to the nearest f32 rounding midpoint, in f64 ulps of A: for a normal f32 result the
+    // conversion keeps A's top 24 significand bits and rounds on the low 29, so every midpoint of A's
+    // binade -- including the one below a power of two the result may round up to -- sits at low29 =
+    // 2^28.  Flag |low29 - 2^28| <= 128 ulps (>= 2^-46 |A|; the core's error is below 2^-50 |A|, 8 ulps,
+    // the library's below an ulp): one integer compare instead of the f64 distance arithmetic (frexp,
+    // ldexp, three f64 subtractions).
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint64_t, a) & 0x1FFFFFFFu;
+    const bool mid = lo - (0x10000000u - 128u) <= 256u;
+    const bool near = (x != x) || (y != y) || !(mx > 0.0 && mx < 0x1p200) || !(fabs(a) >= 0x1p-120) || mid;
     return {f, near};
 }
 
