@@ -32,6 +32,7 @@ touches a GPU) and exits non-zero unless all N ranks finish; the ranks never fal
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
@@ -102,6 +103,10 @@ def parse(argv=None):
                         "own tiles cross no link): 'calibrate' (default: the fastest of a few candidates, measured "
                         "before the warm-up), 'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain "
                         "(tx + 3ty) %% N interleave")
+    p.add_argument("--deadline-s", type=float, default=900.0,
+                   help="self-launched N>1 run: stop every rank and exit non-zero after this many seconds")
+    p.add_argument("--pg-timeout-s", type=float, default=120.0,
+                   help="torch.distributed process-group timeout (init and every collective)")
     p.add_argument("--plumbing", action="store_true",
                    help="no GPU: the N-rank launch, gather pipeline and RGBM unpack on CPU (gloo) with "
                         "synthetic shards (tests only; prints no measurement)")
@@ -138,11 +143,27 @@ def _free_port() -> int:
     return port
 
 
-def launch_ranks(n: int, argv: list[str]) -> int:
+def _stop(procs, live, grace_s: float = 10.0) -> None:
+    """SIGTERM the live ranks (by PID), then SIGKILL whatever is still running after `grace_s`."""
+    for q in live:
+        procs[q].terminate()
+    end = time.monotonic() + grace_s
+    for q in live:
+        try:
+            procs[q].wait(timeout=max(0.0, end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            procs[q].kill()
+            procs[q].wait()
+
+
+def launch_ranks(n: int, argv: list[str], deadline_s: float) -> int:
     """Start this script as N ranks (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env, as
     torchrun sets them) and wait for all of them.  The parent never touches a GPU (it does not even
     import torch), so the children are plain fork+exec of an uninitialised process.  If any rank
-    fails, the others are terminated (by PID) and the exit status is non-zero."""
+    fails, the others are terminated (by PID) and the exit status is non-zero.  If the ranks have not
+    all finished `deadline_s` after the start (a wedged collective, a hung rank), every rank is stopped
+    and the launcher prints one {"error": ...} line and exits non-zero: a hang costs the deadline, not
+    the driver's whole time limit."""
     port = _free_port()
     procs = []
     for r in range(n):
@@ -151,6 +172,7 @@ def launch_ranks(n: int, argv: list[str]) -> int:
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve()), *argv], env=env))
     rc = 0
     live = set(range(n))
+    t_end = time.monotonic() + deadline_s
     while live:
         for r in sorted(live):
             c = procs[r].poll()
@@ -160,8 +182,13 @@ def launch_ranks(n: int, argv: list[str]) -> int:
             if c != 0 and rc == 0:
                 rc = c if c > 0 else 1
                 print(f"bench: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr)
-                for q in live:
-                    procs[q].terminate()
+                _stop(procs, live)
+                live.clear()
+        if live and time.monotonic() > t_end:
+            print(json.dumps({"error": f"deadline: ranks {sorted(live)} of {n} still running after {deadline_s:.0f} s; "
+                                       "all ranks stopped", "n_gpus": n}), flush=True)
+            _stop(procs, live)
+            return 124
         time.sleep(0.05)
     return rc
 
@@ -216,9 +243,12 @@ def plumbing(args, rank: int, n: int) -> int:
 
     from black_hole_ray_marching_amd import multigpu
     if n > 1:
-        dist.init_process_group("gloo")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.pg_timeout_s))
     if os.environ.get("BH_PLUMBING_FAIL_RANK") == str(rank):  # test hook: a rank that dies mid-run
         raise SystemExit(f"plumbing: rank {rank} failing on request")
+    if os.environ.get("BH_PLUMBING_HANG_RANK") == str(rank):  # test hook: a rank that hangs mid-run
+        while True:
+            time.sleep(1.0)
     W, H = (args.width or 100), (args.height or 52)
     weights = root_weights(args, n)
     stride = multigpu.packed_stride(W, H, n, weights)
@@ -284,7 +314,7 @@ def main() -> int:
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        return launch_ranks(args.gpus, argv)
+        return launch_ranks(args.gpus, argv, args.deadline_s)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -315,10 +345,13 @@ def main() -> int:
     if sharded:
         if args.rccl_dry_run and "MASTER_ADDR" not in os.environ:
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1")
+        # an explicit timeout: a wedged rendezvous or collective on the 8-rank node raises instead of
+        # waiting forever (the launcher's deadline stops what it cannot)
+        pg_timeout = datetime.timedelta(seconds=args.pg_timeout_s)
         if rehearsal:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         if dist.get_world_size() != n:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {n}")
 

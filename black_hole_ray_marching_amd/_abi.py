@@ -21,6 +21,7 @@ BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
 BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM = 0, 1, 2, 3
 BH_ORDER_STATES = 32
+BH_BLOOM_SETS = 4
 BH_MAX_FRAMES = 256
 BH_SCHED_TILE, BH_SCHED_PAIR, BH_SCHED_PERSISTENT = 0, 1, 2
 BH_SCHED_FLAG_STATIC_ORDER = 0x100
@@ -29,7 +30,7 @@ BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled bu
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
 
@@ -112,6 +113,7 @@ SIGNATURES = {
                            C.c_void_p, C.c_void_p]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
     "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "bh_graph_release": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None

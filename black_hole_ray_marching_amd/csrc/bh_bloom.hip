@@ -580,6 +580,71 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
     out.px[(uint32_t)y * out.w + x] = enc(L, div12(s));
 }
 
+// ---- remixes of the chain at any proven-identity size (general fused schedule) ----------------------
+// On frames whose same-size passes are identities on stored texels (the host's same_size_identity, e.g.
+// 1920x1080, 1280x720) the copies vanish, but a remix still SAMPLES its two inputs: at the few columns
+// and rows where t = RN(RN((x + 0.5) / n) * n) - 0.5 misses x, the sample mixes in a neighbour with a tiny
+// weight before the two samples are added, and that sum can round to another byte than the texels' sum.
+// So these kernels sample every input through the same-size plan (bh_bloom_same_plan: per column and per
+// row the two clamped texels and the weight, sample()'s own arithmetic) -- a pixel whose column and row
+// are exact (weights 1 / 0) reads its own texel, which is that sample bit for bit.
+// Plan layout: (x0 | x1 << 16, weight bits) per column [0, w), then per row [w, w + h).
+template <bool A1 = false>
+__device__ __forceinline__ F4 sample_same(const Lds& L, CTex t, uint2 cx, uint2 cy) {
+    const int32_t x0 = (int32_t)(cx.x & 0xFFFFu), y0 = (int32_t)(cy.x & 0xFFFFu);
+    const float fa = __uint_as_float(cx.y), fb = __uint_as_float(cy.y);
+    const uint32_t r0 = (uint32_t)y0 * t.w;
+    if (fa == 0.0f && fb == 0.0f) return dec<A1>(L, t.px[r0 + (uint32_t)x0]);
+    const int32_t x1 = (int32_t)(cx.x >> 16), y1 = (int32_t)(cy.x >> 16);
+    const uint32_t r1 = (uint32_t)y1 * t.w;
+    const F4 a = dec<A1>(L, t.px[r0 + (uint32_t)x0]), b = dec<A1>(L, t.px[r0 + (uint32_t)x1]);
+    const F4 c = dec<A1>(L, t.px[r1 + (uint32_t)x0]), d = dec<A1>(L, t.px[r1 + (uint32_t)x1]);
+    return lerp_plan(make_float4(a.r, a.g, a.b, a.a), make_float4(b.r, b.g, b.b, b.a), make_float4(c.r, c.g, c.b, c.a),
+                     make_float4(d.r, d.g, d.b, d.a), fa, fb);
+}
+// out = remix(A, B) (remix.wgsl:22-24) with both inputs sampled through the plan
+__global__ void __launch_bounds__(256) remix_plan_kernel(Tables tb, CTex A, CTex B, const uint2* __restrict__ plan,
+                                                         Tex out) {
+    __shared__ Lds L;
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
+    const bool in = x < out.w && y < out.h;
+    const uint2 cx = plan[in ? x : 0u], cy = plan[out.w + (in ? y : 0u)];
+    load_tables(tb, L);
+    if (!in) return;
+    out.px[y * out.w + x] = enc(L, remix(sample_same(L, A, cx, cy), sample_same(L, B, cx, cy)));
+}
+// The chain's last two remixes: out = remix(col, F), F = q(remix(Y, Bt)) -- F is a texture of the
+// reference (final_in1), so where the plan samples F between texels the lane evaluates F at each texel
+// it weighs (at most 4, each sampling Y and Bt through the plan again).
+__global__ void __launch_bounds__(256) remix2_plan_kernel(Tables tb, CTex col, CTex Y, CTex Bt,
+                                                          const uint2* __restrict__ plan, Tex out) {
+    __shared__ Lds L;
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
+    const bool in = x < out.w && y < out.h;
+    const uint2 cx = plan[in ? x : 0u], cy = plan[out.w + (in ? y : 0u)];
+    load_tables(tb, L);
+    if (!in) return;
+    auto F = [&](uint32_t u, uint32_t v) {  // texel (u, v) of final_in1, decoded
+        const uint2 px = plan[u], py = plan[out.w + v];
+        return quant(L, remix(sample_same(L, Y, px, py), sample_same(L, Bt, px, py)));
+    };
+    const float fa = __uint_as_float(cx.y), fb = __uint_as_float(cy.y);
+    const uint32_t x0 = cx.x & 0xFFFFu, x1 = cx.x >> 16, y0 = cy.x & 0xFFFFu, y1 = cy.x >> 16;
+    F4 f;
+    if (fa == 0.0f && fb == 0.0f) {
+        f = F(x0, y0);
+    } else {
+        // the lerp of sample(): a texel whose weight is 0 enters as t * 0 == 0 for any finite t >= 0,
+        // so it is not evaluated
+        const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
+        const bool ex = fa != 0.0f, ey = fb != 0.0f;
+        const F4 a = F(x0, y0), b = ex ? F(x1, y0) : z, c = ey ? F(x0, y1) : z, d = ex && ey ? F(x1, y1) : z;
+        f = lerp_plan(make_float4(a.r, a.g, a.b, a.a), make_float4(b.r, b.g, b.b, b.a), make_float4(c.r, c.g, c.b, c.a),
+                      make_float4(d.r, d.g, d.b, d.a), fa, fb);
+    }
+    out.px[y * out.w + x] = enc(L, remix(sample_same(L, col, cx, cy), f));
+}
+
 // One render pass of the reference (literal schedule): 16x16 pixels per 256-thread block.
 template <uint32_t SH>
 __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx, uint32_t ry, uint32_t point, TapPlan P,
@@ -1311,6 +1376,46 @@ extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t
     return true;
 }
 
+// The same-size plan of a w x h frame (remix_plan_kernel): per column, then per row, the two clamped
+// texels and the weight of a sample at the pixel's own texcoord ((x + 0.5) / n, sample_coord, floor).
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_plan(uint32_t w, uint32_t h, uint32_t* outp) {
+    if (w > 65535u || h > 65535u || w == 0u || h == 0u) return false;
+    auto axis = [](uint32_t n, uint32_t x, uint32_t* o) {
+        const float t = h_sample_coord(((float)x + 0.5f) / (float)n, n);
+        const float f = floorf(t), wgt = t - f;
+        const int32_t hi = (int32_t)n - 1;
+        const int32_t a0 = std::min(std::max((int32_t)f, 0), hi), a1 = std::min(std::max((int32_t)f + 1, 0), hi);
+        o[0] = (uint32_t)a0 | (uint32_t)a1 << 16;
+        std::memcpy(&o[1], &wgt, 4);
+    };
+    for (uint32_t x = 0; x < w; ++x) axis(w, x, outp + 2u * x);
+    for (uint32_t y = 0; y < h; ++y) axis(h, y, outp + 2u * ((size_t)w + y));
+    return true;
+}
+
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(const float* lut, const float* enc,
+                                                                               const uint8_t* buckets,
+                                                                               const uint32_t* codes, const uint32_t* a,
+                                                                               const uint32_t* b, const uint32_t* plan,
+                                                                               uint32_t* out, uint32_t w, uint32_t h,
+                                                                               hipStream_t s) {
+    hipLaunchKernelGGL(remix_plan_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
+                       CTex{a, w, h}, CTex{b, w, h}, reinterpret_cast<const uint2*>(plan), Tex{out, w, h});
+    return (int)hipGetLastError();
+}
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan(const float* lut, const float* enc,
+                                                                                const uint8_t* buckets,
+                                                                                const uint32_t* codes,
+                                                                                const uint32_t* col, const uint32_t* Y,
+                                                                                const uint32_t* Bt, const uint32_t* plan,
+                                                                                uint32_t* out, uint32_t w, uint32_t h,
+                                                                                hipStream_t s) {
+    hipLaunchKernelGGL(remix2_plan_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
+                       CTex{col, w, h}, CTex{Y, w, h}, CTex{Bt, w, h}, reinterpret_cast<const uint2*>(plan),
+                       Tex{out, w, h});
+    return (int)hipGetLastError();
+}
+
 // bit i: tap i of kawase_upsample.wgsl samples texel centres exactly for every pixel of an
 // ow x oh pass over a tw x th texture with resolution uniform (rx, ry)
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(uint32_t ow, uint32_t oh, uint32_t tw,
@@ -1325,6 +1430,16 @@ extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_point_mask(ui
     return m;
 }
 
+// Whether bh_launch_bloom_pass runs an up pass of this shape with up_sep_kernel (neither the TapPlan nor
+// the Up2Plan form applies): only then does the host build the shape's separable plan (bh_bloom_sep_plan).
+static const bool g_no_up2 = std::getenv("BH_BLOOM_NO_UP2") != nullptr;  // A/B: the general up pass
+static const bool g_no_sep = std::getenv("BH_BLOOM_NO_SEP") != nullptr;  // A/B: the per-pixel sampler
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_up_uses_sep(uint32_t ow, uint32_t oh, uint32_t aw,
+                                                                         uint32_t ah, uint32_t rx, uint32_t ry) {
+    if (g_no_sep || tap_plan(ow, oh, aw, ah, rx, ry).valid) return false;
+    return g_no_up2 || !up2_plan(ow, oh, aw, ah, rx, ry).valid;
+}
+
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32_t shader, const float* lut,
                                                                          const float* enc, const uint8_t* buckets,
                                                                          const uint32_t* codes, const uint32_t* a,
@@ -1337,8 +1452,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     const Tex O{out, ow, oh};
     const TapPlan P = shader == SH_UP ? tap_plan(ow, oh, aw, ah, rx, ry) : TapPlan{};
     const uint32_t pm = shader == SH_UP && !P.valid ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
-    static const bool no_up2 = std::getenv("BH_BLOOM_NO_UP2") != nullptr;  // A/B: the general up pass
-    if (shader == SH_UP && !P.valid && !no_up2) {
+    if (shader == SH_UP && !P.valid && !g_no_up2) {
         const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
         if (Q.valid) {
             const dim3 g((ow + 31u) / 32u, (oh + 31u) / 32u);
@@ -1350,8 +1464,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
             return (int)hipGetLastError();
         }
     }
-    static const bool no_sep = std::getenv("BH_BLOOM_NO_SEP") != nullptr;  // A/B: the per-pixel sampler
-    if (shader == SH_UP && !P.valid && sep && !no_sep) {
+    if (shader == SH_UP && !P.valid && sep && !g_no_sep) {
         hipLaunchKernelGGL(up_sep_kernel, grid_for(ow, oh), dim3(256), 0, s, tb, A, rx, ry,
                            reinterpret_cast<const uint2*>(sep), O);
         return (int)hipGetLastError();

@@ -239,6 +239,24 @@ constexpr uint32_t bh_bloom_shader_copy = 0, bh_bloom_shader_down = 1, bh_bloom_
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                       uint32_t th, uint32_t rx, uint32_t ry,
                                                                       uint32_t* outp);
+// the same-size plan of a w x h frame (bh_bloom.hip): (w + h) uint2 entries; the plan remixes
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_plan(uint32_t w, uint32_t h, uint32_t* outp);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(const float* lut, const float* enc,
+                                                                               const uint8_t* buckets,
+                                                                               const uint32_t* codes, const uint32_t* a,
+                                                                               const uint32_t* b, const uint32_t* plan,
+                                                                               uint32_t* out, uint32_t w, uint32_t h,
+                                                                               hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan(const float* lut, const float* enc,
+                                                                                const uint8_t* buckets,
+                                                                                const uint32_t* codes,
+                                                                                const uint32_t* col, const uint32_t* Y,
+                                                                                const uint32_t* Bt, const uint32_t* plan,
+                                                                                uint32_t* out, uint32_t w, uint32_t h,
+                                                                                hipStream_t s);
+// whether bh_launch_bloom_pass runs an up pass of this shape from its separable plan (bh_bloom.hip)
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_up_uses_sep(uint32_t ow, uint32_t oh, uint32_t aw,
+                                                                         uint32_t ah, uint32_t rx, uint32_t ry);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32_t shader, const float* lut,
                                                                          const float* enc, const uint8_t* buckets,
                                                                          const uint32_t* codes, const uint32_t* a,

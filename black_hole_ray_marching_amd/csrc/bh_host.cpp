@@ -3,6 +3,7 @@
 // fails with a status code.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <array>
 #include <atomic>
 #include <cmath>
@@ -61,11 +62,21 @@ struct bh_ctx {
         std::vector<bh::FrameArgs> last;              // what the table holds once the stream's copies ran
     };
     std::vector<FrameTable> frame_tables;
-    // post-processing (bh_bloom) scratch textures, keyed by (width, height, levels)
-    std::vector<uint32_t*> bloom_tex;
-    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; };  // bloom separable plans (sep_plan)
-    std::vector<SepPlan> sep_plans;
-    uint64_t bloom_key = ~0ull;
+    // post-processing (bh_bloom) scratch: one set of textures per (width, height, levels), with the
+    // separable plans of its up passes (sep_plan).  Graph contract as the order states: a set used under
+    // stream capture is never evicted (bh_graph_release clears the mark); others are evicted least
+    // recently used beyond BH_BLOOM_SETS.
+    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; };
+    struct BloomScratch {
+        uint64_t key = 0;
+        std::vector<uint32_t*> tex;
+        std::vector<SepPlan> sep_plans;
+        uint32_t prepared = 0;   // bit s: schedule s ran once outside capture (every plan it uses exists)
+        bool captured = false;
+        uint64_t last_use = 0;
+    };
+    std::vector<BloomScratch> blooms;
+    uint64_t bloom_clock = 0;
     // shader-clock probe of the march launches (bh_set_clock_probe): device accumulators or null
     unsigned long long* clk = nullptr;
     uint32_t clk_mask = 0;
@@ -83,6 +94,18 @@ struct bh_partition {
 };
 static std::atomic<uint64_t> g_partition_serial{0};
 static void free_frame_table(bh_ctx::FrameTable& t);
+static void free_bloom_scratch(bh_ctx::BloomScratch& b) {
+    for (uint32_t* t : b.tex) (void)hipFree(t);
+    for (auto& p : b.sep_plans) (void)hipFree(p.dev);
+    b.tex.clear();
+    b.sep_plans.clear();
+}
+// True when `s` is capturing -- or when the runtime cannot say (e.g. the legacy stream while another
+// stream captures in global mode): the callers then refuse to allocate, which a capture would not survive.
+static bool stream_capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
 
 namespace {
 
@@ -539,8 +562,7 @@ int bh_destroy(bh_ctx* c) {
         if (o.order) (void)hipFree(o.order);
         if (o.counters) (void)hipFree(o.counters);
     }
-    for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
-    for (auto& p : c->sep_plans) (void)hipFree(p.dev);
+    for (auto& b : c->blooms) free_bloom_scratch(b);
     for (auto& t : c->frame_tables) free_frame_table(t);
     delete c;
     return BH_OK;
@@ -550,15 +572,75 @@ int bh_destroy(bh_ctx* c) {
 
 namespace {
 
-// A same-size pass samples texel centres exactly iff u = RN((x+0.5)/n), RN(u*n) - 0.5 == x for every
-// x < n (then the bilinear weights are exactly 0/1: the pass is the identity on stored texels).
+// A same-size pass (copy, the blur's same-size downsample, a remix input: n texels sampled at n pixels)
+// is the identity on stored texels when every pixel's bilinear sample encodes back to its own texel's
+// byte.  Along one axis pixel x samples texels x0, x1 = clamp(floor(t)), clamp(floor(t) + 1) with
+// weights 1 - fa, fa (t = RN(RN((x + 0.5) / n) * n) - 0.5, sample()'s arithmetic); where t == x the
+// weights are exactly 1 and 0, elsewhere (e.g. 51 of 1920 columns, 42 of 1080 rows) t misses x by a few
+// ulps and the weight on the other texel is tiny but not 0.  Every rounding of the 2-D lerp is monotone
+// in each texel (weights >= 0), so with texel (x, y) = D the result lies between the lerp with every
+// other texel 0 and with every other texel 1 (the largest decoded value); when both bounds encode to D's
+// own byte for every byte value, every weight class of the two axes and both channel kinds (sRGB colour,
+// linear alpha k/255), the pass returns its input's bytes whatever the other texels are.  Powers of two
+// (t == x everywhere) pass trivially.
+struct AxisClass {
+    float ia, fa;  // the weights on texels x0 and x1
+    bool d0, d1;   // x0 == x, x1 == x
+    bool operator==(const AxisClass& o) const { return ia == o.ia && fa == o.fa && d0 == o.d0 && d1 == o.d1; }
+};
+bool same_size_axis(uint32_t n, std::vector<AxisClass>& cls) {
+    cls.clear();
+    const int32_t hi = (int32_t)n - 1;
+    for (uint32_t x = 0; x < n; ++x) {
+        const float u = ((float)x + 0.5f) / (float)n;
+        const float t = fminf(fmaxf(u * (float)n - 0.5f, -1.0f), (float)n);
+        const float f = floorf(t);
+        const float fa = t - f;
+        const int32_t x0 = std::min(std::max((int32_t)f, 0), hi), x1 = std::min(std::max((int32_t)f + 1, 0), hi);
+        const AxisClass c{1.0f - fa, fa, x0 == (int32_t)x, x1 == (int32_t)x};
+        if (!c.d0 && !c.d1) return false;
+        if (std::find(cls.begin(), cls.end(), c) == cls.end()) cls.push_back(c);
+    }
+    return true;
+}
+uint8_t unorm8_ref(float a) {
+    if (!(a > 0.0f)) return 0;
+    if (a >= 1.0f) return 255;
+    return (uint8_t)std::floor((double)a * 255.0 + 0.5);
+}
+// Every pixel of a same-size pass samples its own texel centre exactly (t == x): weights 1 and 0, the
+// sample is the texel itself, before any quantisation (powers of two).
 bool same_size_exact(uint32_t n) {
     for (uint32_t x = 0; x < n; ++x) {
         const float u = ((float)x + 0.5f) / (float)n;
-        const float t = u * (float)n - 0.5f;
-        if (t != (float)x) return false;
+        if (u * (float)n - 0.5f != (float)x) return false;
     }
     return true;
+}
+bool same_size_identity(uint32_t w, uint32_t h) {
+    static thread_local std::vector<std::pair<uint64_t, bool>> memo;
+    const uint64_t key = (uint64_t)w << 32 | h;
+    for (const auto& m : memo)
+        if (m.first == key) return m.second;
+    std::vector<AxisClass> cx, cy;
+    bool ok = same_size_axis(w, cx) && same_size_axis(h, cy);
+    float lut[256];
+    srgb_lut(lut);
+    for (const AxisClass& X : cx)
+        for (const AxisClass& Y : cy)
+            for (int kind = 0; kind < 2 && ok; ++kind)
+                for (int b = 0; b < 256 && ok; ++b) {
+                    const float D = kind == 0 ? lut[b] : (float)b / 255.0f;
+                    for (float O : {0.0f, 1.0f}) {
+                        const float t00 = X.d0 && Y.d0 ? D : O, t10 = X.d1 && Y.d0 ? D : O;
+                        const float t01 = X.d0 && Y.d1 ? D : O, t11 = X.d1 && Y.d1 ? D : O;
+                        const float r = (t00 * X.ia + t10 * X.fa) * Y.ia + (t01 * X.ia + t11 * X.fa) * Y.fa;
+                        if ((kind == 0 ? srgb_encode_ref(r) : unorm8_ref(r)) != b) ok = false;
+                    }
+                }
+    if (memo.size() >= 16) memo.erase(memo.begin());
+    memo.push_back({key, ok});
+    return ok;
 }
 
 struct BloomPlan {
@@ -582,14 +664,23 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 }
 
 // The separable plan of an up pass of this shape (bh_bloom_sep_plan), on the device, built at its first
-// use and kept with the ctx (a few hundred KiB per shape); NULL if the shape does not fit the plan.
-const uint32_t* sep_plan(bh_ctx* c, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry,
-                         int* err) {
+// use and kept with the scratch set (16 B per column and row); NULL if the shape does not fit the plan.
+// A capturing call never builds one (bh_bloom refuses a set not prepared outside capture).
+const uint32_t* sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th,
+                         uint32_t rx, uint32_t ry, int* err) {
     const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
-    for (const auto& p : c->sep_plans)
+    for (const auto& p : b->sep_plans)
         if (p.key == key) return p.dev;
-    std::vector<uint32_t> h(16u * ((size_t)ow + oh));
-    if (!bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data())) return nullptr;
+    if (capturing) {
+        *err = (int)hipErrorStreamCaptureUnsupported;
+        return nullptr;
+    }
+    // rx == 0: the same-size plan of the remixes (bh_bloom_same_plan), one tap
+    std::vector<uint32_t> h((rx ? 16u : 2u) * ((size_t)ow + oh));
+    if (!(rx ? bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data()) : bh_bloom_same_plan(ow, oh, h.data()))) {
+        *err = (int)hipErrorInvalidValue;
+        return nullptr;
+    }
     uint32_t* d = nullptr;
     hipError_t e = hipMalloc(&d, h.size() * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
@@ -598,18 +689,22 @@ const uint32_t* sep_plan(bh_ctx* c, uint32_t ow, uint32_t oh, uint32_t tw, uint3
         *err = hip_fail(e, "bloom separable plan");
         return nullptr;
     }
-    c->sep_plans.push_back({key, d});
+    b->sep_plans.push_back({key, d});
     return d;
 }
 
 struct BloomRun {
     bh_ctx* c;
+    bh_ctx::BloomScratch* B;
+    bool capturing;
     hipStream_t s;
     int err = 0;
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
         if (err != 0) return;
-        const uint32_t* sep = sh == bh_bloom_shader_up ? sep_plan(c, ow, oh, aw, ah, res[0], res[1], &err) : nullptr;
+        const uint32_t* sep = sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1])
+                                  ? sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err)
+                                  : nullptr;
         if (err == 0)
             err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
                                        sep, s);
@@ -631,31 +726,60 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;
     const BloomPlan P = bloom_plan(W, H, levels);
-    const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) &&
-                       same_size_exact(P.res[levels - 1][0]) && same_size_exact(P.res[levels - 1][1]);
+    // AUTO: the fused chain when every same-size sample is exact (powers of two); the general fused chain
+    // when they are proven identities on stored texels (same_size_identity: the copies vanish, the remixes
+    // still sample through the same-size plan); else the literal pass list
+    const uint32_t wl = P.res[levels - 1][0], hl = P.res[levels - 1][1];
+    const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) && same_size_exact(wl) &&
+                       same_size_exact(hl);
+    const bool general = schedule == BH_BLOOM_AUTO && !fused && same_size_identity(W, H) && same_size_identity(wl, hl);
     // scratch: [0, 3*levels) copy_in / remix_in0 / remix_in1 (full), then blur_in, final_in1 (full),
     // then down[levels], up[levels] at res[l]
     const uint64_t key = ((uint64_t)W << 40) ^ ((uint64_t)H << 16) ^ levels;
-    if (c->bloom_key != key) {
-        for (uint32_t* t : c->bloom_tex) (void)hipFree(t);
-        c->bloom_tex.clear();
-        c->bloom_key = ~0ull;
-        const size_t full = (size_t)W * H * 4u;
-        for (uint32_t i = 0; i < 3u * levels + 2u; ++i) {
-            uint32_t* t = nullptr;
-            if ((e = hipMalloc(&t, full)) != hipSuccess) return hip_fail(e, "hipMalloc(bloom)");
-            c->bloom_tex.push_back(t);
+    const bool capturing = stream_capturing(s);
+    bh_ctx::BloomScratch* B = nullptr;
+    for (auto& b : c->blooms)
+        if (b.key == key) B = &b;
+    if (capturing) {
+        // graph contract: nothing is allocated or uploaded under capture, and a set a graph uses is kept
+        if (!B || !(B->prepared & (1u << schedule))) {
+            g_last_error = "bh_bloom: the first call of a (size, levels, schedule) allocates; run it once before "
+                           "capturing it into a graph";
+            return BH_ERR_UNSUPPORTED;
         }
-        for (uint32_t k = 0; k < 2; ++k)
-            for (uint32_t l = 0; l < levels; ++l) {
-                uint32_t* t = nullptr;
-                if ((e = hipMalloc(&t, (size_t)P.res[l][0] * P.res[l][1] * 4u)) != hipSuccess)
-                    return hip_fail(e, "hipMalloc(bloom)");
-                c->bloom_tex.push_back(t);
-            }
-        c->bloom_key = key;
+        B->captured = true;
     }
-    uint32_t** T = c->bloom_tex.data();
+    if (!B) {
+        bh_ctx::BloomScratch n;
+        n.key = key;
+        auto alloc = [&](size_t bytes) {
+            uint32_t* t = nullptr;
+            if ((e = hipMalloc(&t, bytes)) == hipSuccess) n.tex.push_back(t);
+            return e == hipSuccess;
+        };
+        bool ok = true;
+        for (uint32_t i = 0; ok && i < 3u * levels + 2u; ++i) ok = alloc((size_t)W * H * 4u);
+        for (uint32_t k = 0; ok && k < 2; ++k)
+            for (uint32_t l = 0; ok && l < levels; ++l) ok = alloc((size_t)P.res[l][0] * P.res[l][1] * 4u);
+        if (!ok) {
+            free_bloom_scratch(n);
+            return e == hipErrorOutOfMemory ? BH_ERR_OUT_OF_MEMORY : hip_fail(e, "hipMalloc(bloom)");
+        }
+        if (c->blooms.size() >= BH_BLOOM_SETS) {  // evict the least recently used set no graph holds
+            size_t v = c->blooms.size();
+            for (size_t i = 0; i < c->blooms.size(); ++i)
+                if (!c->blooms[i].captured && (v == c->blooms.size() || c->blooms[i].last_use < c->blooms[v].last_use))
+                    v = i;
+            if (v < c->blooms.size()) {
+                free_bloom_scratch(c->blooms[v]);
+                c->blooms.erase(c->blooms.begin() + (long)v);
+            }
+        }
+        c->blooms.push_back(std::move(n));
+        B = &c->blooms.back();
+    }
+    B->last_use = ++c->bloom_clock;
+    uint32_t** T = B->tex.data();
     uint32_t **copy_in = T, **remix_in0 = T + levels, **remix_in1 = T + 2 * levels;
     uint32_t* blur_in = T[3 * levels];
     uint32_t* final_in1 = T[3 * levels + 1];
@@ -664,10 +788,10 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     const uint32_t* C = (const uint32_t*)col;
     uint32_t* O = (uint32_t*)out;
     const uint32_t full[2] = {W, H};
-    BloomRun R{c, s};
+    BloomRun R{c, B, capturing, s};
     const uint32_t L = levels - 1;
     if (fused) {
-        // same-size passes are identities (same_size_exact): see bh_bloom.hip
+        // same-size passes are identities (same_size_identity): see bh_bloom.hip
         const uint32_t* S = X;
         if (levels > 1) {
             if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
@@ -688,6 +812,36 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         }
         if (R.err == 0)
             R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, c->enc_e, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
+    } else if (general) {
+        // general fused chain (same-size passes are identities, see bloom_plan_remixes in bh_bloom.hip):
+        // U1 = up(X) at full size, Y = remix(X, U1) through the same-size plan, the blur's downsamples
+        // and upsamples from Y, B = its last up pass, out = remix(col, q(remix(Y, B))) through the plan
+        const uint32_t* plan = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
+        const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
+        if (levels > 1) {
+            uint32_t* U1 = remix_in1[0];
+            R.pass(bh_bloom_shader_up, X, W, H, nullptr, full, U1, W, H);
+            if (R.err == 0)
+                R.err = bh_launch_bloom_remix_plan(c->lut, c->enc, c->enc_b, c->enc_e, X, U1, plan, copy_in[1], W, H, s);
+            S = copy_in[1];
+        }
+        const uint32_t* dn = S;
+        for (uint32_t l = 1; l < levels; ++l) {
+            R.pass(bh_bloom_shader_down, dn, P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1], down[l],
+                   P.res[l][0], P.res[l][1]);
+            dn = down[l];
+        }
+        const uint32_t* u_src = dn;
+        for (uint32_t l = 0; l + 1 < levels; ++l) {
+            const uint32_t ti = levels - l - 2;
+            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
+                   P.res[ti][0], P.res[ti][1]);
+            u_src = up[ti];
+        }
+        uint32_t* Bt = remix_in1[L];
+        R.pass(bh_bloom_shader_up, u_src, W, H, nullptr, P.res[L], Bt, W, H);
+        if (R.err == 0)
+            R.err = bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, C, S, Bt, plan, O, W, H, s);
     } else {
         // literal: the reference's render passes in order (oracle/bh_bloom_oracle.c, bho_bloom)
         if ((e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)
@@ -718,6 +872,14 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         (void)blur_in;
     }
     if (R.err != 0) return hip_fail((hipError_t)R.err, "bloom launch");
+    if (!capturing) B->prepared |= 1u << schedule;
+    return BH_OK;
+}
+
+int bh_graph_release(bh_ctx* c) {
+    if (!c) return BH_ERR_INVALID_ARG;
+    for (auto& o : c->orders) o.captured = false;
+    for (auto& b : c->blooms) b.captured = false;
     return BH_OK;
 }
 
@@ -756,8 +918,7 @@ static void free_frame_table(bh_ctx::FrameTable& t) {
 // order and march kernels that read it.  *dev receives the table.
 static int stage_frame_table(bh_ctx* c, hipStream_t s, const bh::FrameArgs* frames, uint32_t n,
                              const bh::FrameArgs** dev) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    if (stream_capturing(s)) {
         g_last_error = "bh_render_frames: more than 32 frames per call cannot be captured into a graph";
         return BH_ERR_UNSUPPORTED;
     }
@@ -977,9 +1138,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     bh_ctx::OrderState* os = nullptr;
     if (sched == BH_SCHED_TILE && !(d->schedule & BH_SCHED_FLAG_STATIC_ORDER)) {
         // temporal order of this (geometry, shard, stream): allocated at its first render only
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        const bool capturing = hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
-        int st = order_state(c, d, nt, s, capturing, &os);
+        int st = order_state(c, d, nt, s, stream_capturing(s), &os);
         if (st != BH_OK) return st;
         if (!os->valid) {
             // all costs 0 (one bucket, the uncounted last) and an empty histogram: consistent

@@ -268,6 +268,7 @@ class Scene:
         if getattr(self, "_ctx", None):
             self.lib.bh_destroy(self._ctx)
             self._ctx = None
+        self._clock_acc = None
 
     def __del__(self) -> None:
         try:
@@ -376,6 +377,14 @@ class Scene:
         if acc is not None:
             _check_size(acc, 128 * 8, "acc", "set_clock_probe")
         check(self.lib.bh_set_clock_probe(self._ctx, _ptr(acc), stride), "bh_set_clock_probe")
+        # the armed ctx holds acc's raw pointer: keep the tensor alive until disarmed (or close), so the
+        # caching allocator cannot hand its memory to another tensor while march launches add into it
+        self._clock_acc = acc
+
+    def graph_release(self) -> None:
+        """bh_graph_release: unpin the order states and bloom scratch sets that stream captures marked
+        (call it after destroying every graph captured from this scene)."""
+        check(self.lib.bh_graph_release(self._ctx), "bh_graph_release")
 
     def bloom(self, col, blackout, out, *, levels: int = 3, schedule: int = 0, width: int | None = None,
               height: int | None = None, stream=None) -> None:

@@ -37,7 +37,13 @@
  * and may be captured into a hipGraph.  Those buffers are never freed or moved before bh_destroy
  * while a graph may use them: a key rendered under stream capture is never evicted.  Other keys are
  * evicted least-recently-used beyond BH_ORDER_STATES (when every key has been captured the ctx keeps
- * more instead).  Renders of one ctx on different streams with the TILE or PAIR schedule use
+ * more instead).  bh_bloom keeps one scratch set per (size, levels) under the same contract: the first
+ * call of a (size, levels, schedule) allocates and must not be captured (BH_ERR_UNSUPPORTED on a
+ * capturing stream), a set used under capture is never freed, others are evicted least-recently-used
+ * beyond BH_BLOOM_SETS.  A stream whose capture status the runtime cannot report (e.g. the legacy
+ * stream while another stream captures globally) counts as capturing.  Captured states stay pinned
+ * until bh_destroy, or until bh_graph_release (call it once the graphs that used them are destroyed).
+ * Renders of one ctx on different streams with the TILE or PAIR schedule use
  * different order state and no other shared scratch, so they may run concurrently (frames in flight);
  * the PERSISTENT schedule (shared work counters) and bh_bloom (shared scratch textures) must not run
  * concurrently with themselves on one ctx.  One bh_ctx per device; a ctx is not thread-safe, distinct
@@ -53,10 +59,12 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 6
+#define BH_ABI_VERSION 7
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
+/* bh_bloom scratch sets (size x levels) one ctx keeps (see above). */
+#define BH_BLOOM_SETS 4
 
 typedef enum {
     BH_OK = 0,
@@ -261,13 +269,19 @@ int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* ca
  * targets, on BGRA8-sRGB images (bh_render with BH_OUT_BGRA8_SRGB): `col` (full_image_input),
  * `blackout` (blackout_input) -> `out` (the surface), all width x height (1..65536 each, as bh_render),
  * row-major, device memory.  `levels` = the Bloom's level count (src/state.rs:125 uses 3; 1..12).  Scratch textures live in
- * the context (allocated at the first call for a size).  `schedule`: BH_BLOOM_AUTO fuses passes
- * whenever that gives identical bytes (always for power-of-two sizes), BH_BLOOM_LITERAL runs the
+ * the context (allocated at the first call for a size; graph contract above).  `schedule`: BH_BLOOM_AUTO
+ * fuses passes whenever that gives identical bytes (the host proves the chain's same-size samples are
+ * identities on stored texels: powers of two, 1920x1080, 1280x720, ...), BH_BLOOM_LITERAL runs the
  * reference's render passes one by one.  Asynchronous on `hip_stream`. */
 #define BH_BLOOM_AUTO    0u
 #define BH_BLOOM_LITERAL 1u
 int bh_bloom(bh_ctx* ctx, const void* col_bgra8, const void* blackout_bgra8, uint32_t width, uint32_t height,
              uint32_t levels, uint32_t schedule, void* out_bgra8, void* hip_stream);
+
+/* Graph contract (see the top of this file): unpin every order state and bloom scratch set that a
+ * capture marked, so that LRU eviction may free them again.  Call it only after destroying every HIP
+ * graph captured from this ctx (their kernels read and write those buffers). */
+int bh_graph_release(bh_ctx* ctx);
 
 /* Number of 8x8 tiles owned by `shard_index` of `shard_count` in a width x height frame. */
 int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count);

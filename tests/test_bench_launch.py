@@ -43,6 +43,29 @@ def test_self_launch_fails_loudly_when_a_rank_fails():
     assert all(d.get("gather_verified_bit_exact") is not True for d in lines)
 
 
+def test_self_launch_deadline_stops_a_hung_rank():
+    """A rank that hangs (not one that exits) must not hold the run for the driver's whole limit: the
+    launcher's deadline stops every rank and prints one {"error": ...} line."""
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e["BH_PLUMBING_HANG_RANK"] = "1"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--plumbing", "--steps", "3",
+                        "--deadline-s", "25", "--pg-timeout-s", "600"],
+                       capture_output=True, text=True, timeout=120, env=e, cwd=str(ROOT))
+    assert r.returncode != 0
+    errs = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"error"')]
+    assert len(errs) == 1 and "deadline" in errs[0]["error"], r.stdout[-2000:]
+    assert not any(x.startswith('{"metric"') for x in r.stdout.splitlines())
+
+
+def test_process_group_timeout_ends_a_wedged_collective():
+    """With the deadline out of the way, the process group's own timeout ends the wait of the rank
+    blocked in the gather on the hung peer: it raises, exits non-zero, and the launcher stops the rest."""
+    rc, lines, _ = _bench("--gpus", "2", "--plumbing", "--steps", "3", "--deadline-s", "600", "--pg-timeout-s", "8",
+                          env={"BH_PLUMBING_HANG_RANK": "1"}, timeout=180)
+    assert rc != 0
+    assert all(d.get("gather_verified_bit_exact") is not True for d in lines)
+
+
 def test_world_size_mismatch_is_refused():
     rc, lines, err = _bench("--gpus", "2", "--plumbing", env={"WORLD_SIZE": "3", "RANK": "0"})
     assert rc != 0 and not lines

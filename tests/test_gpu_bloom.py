@@ -44,12 +44,15 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # odd widths whose same-size sampling is exact (fused chain): the
                                         # quad kernels' paired stores must not assume 8-byte aligned rows
                                         (64, 65, 3), (33, 129, 3), (65, 33, 2),
-                                        # literal schedule at a display size and on thin frames: the up
-                                        # passes' separable plan (per-column / per-row taps from the host)
-                                        (1080, 1920, 5), (7, 300, 3), (300, 7, 3)])
+                                        # display sizes (config 2's frame; the reference's 1280x720 window,
+                                        # src/lib.rs:60-61): same-size passes proven identities, so AUTO
+                                        # fuses them; the up passes take the separable plan (per-column /
+                                        # per-row taps from the host); also thin frames
+                                        (1080, 1920, 3), (720, 1280, 3), (1080, 1920, 5), (7, 300, 3), (300, 7, 3)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
-    """AUTO fuses passes for sizes whose same-size sampling is exact (powers of two) and runs the
-    literal pass list otherwise (200x120, 53x37); both must give the oracle's bytes.  Power-of-two
+    """AUTO fuses the chain when its same-size passes are provably identities on stored texels (the
+    host's same_size_identity: every size here, powers of two trivially) and runs the literal pass list
+    otherwise; LITERAL always runs the pass list.  Both must give the oracle's bytes.  Power-of-two
     sizes also take the 8-tap passes' TapPlan form (constant-offset taps) and the 2:1 up passes'
     Up2Plan form (per-parity offsets and weights), up to the full 4096x2048 frame."""
     rng = np.random.default_rng(W * 7 + H + levels)
@@ -128,4 +131,40 @@ def test_bloom_matches_golden(torch_cuda, sky_small, path, schedule):
     scene = bh.Scene(16, 16, sky=sky_small)
     got = _gpu_bloom(torch_cuda, scene, z["col"], z["blackout"], int(z["levels"][0]), schedule)
     assert np.array_equal(got, z["out"])
+    scene.close()
+
+
+def test_bloom_graph_contract(torch_cuda, sky_small):
+    """Graph contract of bh_bloom (include/bh_render.h): the first call of a (size, levels, schedule)
+    allocates and is refused on a capturing stream; a captured chain's scratch set survives any number of
+    other sizes (beyond BH_BLOOM_SETS) and its replay writes the same bytes as a direct call."""
+    torch = torch_cuda
+    rng = np.random.default_rng(11)
+    H, W = 72, 136  # not a power of two: the fused chain's up passes run from separable plans
+    col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
+    c, b = torch.from_numpy(col).cuda(), torch.from_numpy(bo).cuda()
+    out = torch.zeros_like(c)
+    scene = bh.Scene(16, 16, sky=sky_small)
+    s = torch.cuda.Stream()
+    scene.bloom(c, b, out, width=W, height=H, stream=s)  # allocates this key's scratch and plans
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        with pytest.raises(bh.BhError):  # a new size under capture: refused, nothing launched
+            scene.bloom(c, b, out, width=W - 8, height=H, stream=s)
+        with pytest.raises(bh.BhError):  # the same size with a schedule not run before: refused
+            scene.bloom(c, b, out, width=W, height=H, schedule=bh.BH_BLOOM_LITERAL, stream=s)
+        scene.bloom(c, b, out, width=W, height=H, stream=s)
+    for k in range(bh.BH_BLOOM_SETS + 2):  # other sizes: evict every set no graph holds
+        w = W - 8 * (k + 1)
+        scene.bloom(c, b, torch.zeros_like(c), width=w, height=H, stream=s)
+    torch.cuda.synchronize()
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.bloom(col, bo, 3))
+    del g
+    scene.graph_release()
+    scene.bloom(c, b, torch.zeros_like(c), width=W - 64, height=H, stream=s)  # may evict it now
+    torch.cuda.synchronize()
     scene.close()

@@ -487,7 +487,10 @@ def test_clock_probe_samples_the_march_without_changing_it(torch_cuda, sky_small
     torch.cuda.synchronize()
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     c = bh.clock_mhz(acc.cpu().numpy())
-    assert c["waves"] == (W // 8) * (H // 8) // 16, c
+    # clock_end drops a sample whose tick ratio is implausible (a wave preempted and restored on another
+    # XCD): most sampled waves count, none beyond the sampled slots
+    expected = (W // 8) * (H // 8) // 16
+    assert 0.9 * expected <= c["waves"] <= expected, c
     assert 300.0 < c["mhz"] < 3500.0, c
     with pytest.raises(bh.BhError):
         scene.set_clock_probe(acc, 3)  # stride must be a power of two
