@@ -103,6 +103,9 @@ def parse(argv=None):
                         "own tiles cross no link): 'calibrate' (default: the fastest of a few candidates, measured "
                         "before the warm-up), 'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain "
                         "(tx + 3ty) %% N interleave")
+    p.add_argument("--transport", choices=["auto", "rgbm", "rgbm14"], default="auto",
+                   help="N>1 shard layout: BH_LAYOUT_TILES_RGBM (6.125 B/pixel of RGBA16F) or BH_LAYOUT_TILES_RGBM14 "
+                        "(5.375: the fp16 channels in [0, 1] take 14 bits); auto = rgbm14 for rgba16f")
     p.add_argument("--deadline-s", type=float, default=900.0,
                    help="self-launched N>1 run: stop every rank and exit non-zero after this many seconds")
     p.add_argument("--pg-timeout-s", type=float, default=120.0,
@@ -252,7 +255,8 @@ def plumbing(args, rank: int, n: int) -> int:
     W, H = (args.width or 100), (args.height or 52)
     weights = root_weights(args, n)
     stride = multigpu.packed_stride(W, H, n, weights)
-    tb = multigpu.rgbm_tile_bytes(1)
+    p14 = args.transport != "rgbm"  # the frame is RGBA16F
+    tb = multigpu.RGBM14_TILE_BYTES if p14 else multigpu.rgbm_tile_bytes(1)
     yy, xx = np.mgrid[0:H, 0:W]
 
     def frame(i):
@@ -264,7 +268,10 @@ def plumbing(args, rank: int, n: int) -> int:
     ok = []
 
     def on_frame(i, gathered):
-        col, bo = multigpu.unpack_rgbm_numpy(gathered.numpy(), W, H, n, stride, np.float16, 1.0, weights)
+        if p14:
+            col, bo = multigpu.unpack_rgbm14_numpy(gathered.numpy(), W, H, n, stride, weights)
+        else:
+            col, bo = multigpu.unpack_rgbm_numpy(gathered.numpy(), W, H, n, stride, np.float16, 1.0, weights)
         want, zero = frame(i)
         want_bo = want.copy()
         want_bo[zero, :3] = 0
@@ -274,13 +281,15 @@ def plumbing(args, rank: int, n: int) -> int:
     pipe = multigpu.GatherPipeline(lambda: torch.zeros((stride, tb), dtype=torch.uint8), rank, n, on_frame)
     for i in range(args.steps):
         c, z = frame(i)
-        pipe.buffer(i).copy_(torch.from_numpy(multigpu.pack_rgbm_numpy(c, z, rank, n, stride, weights)))
+        pack = multigpu.pack_rgbm14_numpy if p14 else multigpu.pack_rgbm_numpy
+        pipe.buffer(i).copy_(torch.from_numpy(pack(c, z, rank, n, stride, weights)))
         pipe.submit(i)
     pipe.drain()
     world = dist.get_world_size() if n > 1 else 1
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Mpix/s", "n_gpus": n, "steps": args.steps,
                           "data": "plumbing (CPU, gloo, synthetic RGBM shards; no GPU, not a measurement)",
+                          "transport": "rgbm14" if p14 else "rgbm",
                           "world_size": world, "backend": dist.get_backend() if n > 1 else None,
                           "partition_weights": weights,
                           "frames_checked": len(ok), "gather_verified_bit_exact": bool(ok) and all(ok)}))
@@ -398,7 +407,12 @@ def main() -> int:
         pipe = None
         batches = [scene.prepare_frames(cols, bos, fmt=fmt, schedule=sched, **shard)]
     else:
-        tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+        p14 = args.transport == "rgbm14" or (args.transport == "auto" and fmt == bh.BH_OUT_RGBA16F)
+        if p14 and fmt != bh.BH_OUT_RGBA16F:
+            raise SystemExit("--transport rgbm14 packs rgba16f only")
+        layout = bh.BH_LAYOUT_TILES_RGBM14 if p14 else bh.BH_LAYOUT_TILES_RGBM
+        ufmt = fmt | bh.BH_UNPACK_RGBM14 if p14 else fmt  # the unpack's format argument
+        tb = bh.tile_bytes(layout, fmt)
         frame_cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         frame_bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         side = torch.cuda.Stream(dev)
@@ -414,7 +428,7 @@ def main() -> int:
                 self.part = bh.Partition(W, H, weights, device=local) if weights else None
                 self.stride = max(self.part.counts) if self.part else multigpu.packed_stride(W, H, n)
                 self.my_tiles = self.part.counts[rank] if self.part else bh.shard_tile_count(W, H, rank, n)
-                self.shard = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_index=rank, shard_count=n)
+                self.shard = dict(layout=layout, shard_index=rank, shard_count=n)
                 if self.part:
                     self.shard["partition"] = self.part
                 self.launch_frames = {}
@@ -431,10 +445,10 @@ def main() -> int:
                 for f in range(self.launch_frames.pop(i)):
                     if self.part:
                         bh.tiles_unpack_rgbm_partition(gathered[f * st:], frame_cols[f], frame_bos[f], self.part, D * st,
-                                                       fmt, stream=torch.cuda.current_stream(dev),
+                                                       ufmt, stream=torch.cuda.current_stream(dev),
                                                        rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
                     else:
-                        bh.tiles_unpack_rgbm(gathered[f * st:], frame_cols[f], frame_bos[f], W, H, n, D * st, fmt,
+                        bh.tiles_unpack_rgbm(gathered[f * st:], frame_cols[f], frame_bos[f], W, H, n, D * st, ufmt,
                                              stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
 
             def step(self, k):  # one untimed batch (render + exchange), k = its pipeline index
@@ -693,8 +707,9 @@ def main() -> int:
                             f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}"
                             + (f" orbiting {args.orbit_deg} deg/frame" if args.camera_path == "orbit" else "") + ", "
                             f"{args.fmt} col+blackout, {args.math} math, {D} frames per step"
-                            + ("" if not sharded else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of RGBM shards "
-                                                  "(RGB planes + blackout mask) to rank 0 overlapped with the next "
+                            + ("" if not sharded else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of "
+                                                  f"{'RGBM14' if p14 else 'RGBM'} shards "
+                                                  "(RGB + blackout mask) to rank 0 overlapped with the next "
                                                   "batch, rank 0 unpacks col and blackout_col"),
                 "baseline_config": args.config or None,
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
@@ -755,6 +770,8 @@ def main() -> int:
         if sharded:
             result["world_size"] = dist.get_world_size()
             result["backend"] = dist.get_backend()
+            result["transport"] = {"layout": "rgbm14" if p14 else "rgbm", "tile_bytes": tb,
+                                   "bytes_per_pixel": round(tb / 64.0, 4)}
             result["per_rank_s"] = [round(x, 6) for x in per_rank]
             result["ranks"] = ranks
             result["partition_calibration"] = calibration

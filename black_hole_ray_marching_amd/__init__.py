@@ -5,7 +5,7 @@ The compute path is libbh_render.so (hand-written HIP for gfx950 behind the C AB
 include/bh_render.h); this package is the host-side mirror of the reference's Scene/Camera API.
 """
 from ._abi import (BH_BLOOM_AUTO, BH_BLOOM_LITERAL, BH_FATE_BLACKOUT, BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_LAYOUT_ROWMAJOR,
-                   BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_ORDER_STATES, BH_BLOOM_SETS, BH_MAX_FRAMES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_BGRA8_SRGB, BH_OUT_RGBA16F,
+                   BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_LAYOUT_TILES_RGBM14, BH_UNPACK_RGBM14, BH_ORDER_STATES, BH_BLOOM_SETS, BH_MAX_FRAMES, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_BGRA8_SRGB, BH_OUT_RGBA16F,
                    BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BH_SCHED_FLAG_STATIC_ORDER, BH_SCHED_FLAG_ISSUE_ORDER, BH_SCHED_FLAG_LATENCY, BH_SCHED_PAIR, BH_SCHED_PERSISTENT, BH_SCHED_TILE,
                    BYTES_PER_PIXEL,
                    BhError, load)

@@ -19,7 +19,8 @@ BH_BLOOM_AUTO, BH_BLOOM_LITERAL = 0, 1
 BH_MATH_EXACT, BH_MATH_FAST = 0, 1
 BH_SCENE_DISC, BH_SCENE_MARKERS = 1, 2
 BH_SCENE_DEFAULT = 3
-BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM = 0, 1, 2, 3
+BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_LAYOUT_TILES_RGBM14 = 0, 1, 2, 3, 4
+BH_UNPACK_RGBM14 = 0x100  # format flag of the RGBM unpacks: the shards are BH_LAYOUT_TILES_RGBM14
 BH_ORDER_STATES = 32
 BH_BLOOM_SETS = 4
 BH_MAX_FRAMES = 256

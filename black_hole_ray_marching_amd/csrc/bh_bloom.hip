@@ -488,16 +488,30 @@ constexpr int FP_FINAL = 44;  // the last up pass at res / 4: taps within +-12 t
 
 // ---- separable plan of an 8-tap pass (any frame size) -------------------------------------------
 // A tap's texel coordinate along x depends only on the pixel's column (texcoord(x) + du_i, then
-// sample_coord, floor and the clamps), and along y only on its row.  The host evaluates that arithmetic
-// once per launch shape for every column and row (bh_bloom_sep_plan: the kernel's own f32 operations,
-// no contraction) -- per tap and column the two clamped texel columns and the weight, per tap and row
-// the same -- and the kernel reads them instead of recomputing them per pixel: the general sampler's
-// lerps on the general sampler's texels, the same bits.  Used by the up passes whose TapPlan / Up2Plan
-// proofs fail (frame sizes other than powers of two take the literal schedule).
-// Layout (uint2 = (x0 | x1 << 16, bits of the weight)): [tap][column] for the columns, then [tap][row].
+// sample_coord and floor), and along y only on its row.  The host evaluates that arithmetic once per
+// launch shape for every column and row (bh_bloom_sep_plan: the kernel's own f32 operations, no
+// contraction) and the kernel reads it instead of recomputing it per pixel: the general sampler's lerps
+// on the general sampler's texels, the same bits.  Used by the up passes whose TapPlan / Up2Plan proofs
+// fail (frame sizes other than powers of two).
+// Entry per tap and column (then per tap and row): the UNCLAMPED floor f of the sampler's coordinate t
+// (t clamped to [-1, n] as sample_coord does, so f is in [-1, n]) and the weights fa = t - f,
+// ia = 1 - fa.  The block stages its footprint with clamp-to-edge addressing -- tile entry (ly, lx)
+// holds texel (clamp(lo_y + ly), clamp(lo_x + lx)) -- so sample()'s texels clamp(f) and clamp(f + 1)
+// are tile entries f - lo and f + 1 - lo: a tap's four reads are one base offset plus 0, 1, FP, FP + 1.
+struct SepEntry { int32_t f; float fa, ia; int32_t pad; };
+static_assert(sizeof(SepEntry) == 16, "one ds_read_b128 per entry");
+
+// Epilogues of the separable up pass.  PLAIN: out = q(up8).  Y (the general fused chain's first stage,
+// source X): U = q(up8(X)) to `aux` for every pixel, and Y = q(X + 0.5 U) to `out` for the pixels whose
+// column and row sample exactly (same-size plan weight 0; the rest: fixup_kernel).  FINAL (source U0
+// = the blur's last up input, res = res[L]): B = q(up8(U0)) to `aux`, and for exact pixels
+// out = q(col + 0.5 q(Y + 0.5 B)) (own0 = col, own1 = Y).
+enum SepEpi : uint32_t { EPI_PLAIN = 0, EPI_Y = 1, EPI_FINAL = 2 };
+
+// bilinear of texels (t00, t10, t01, t11) with weights (fa, fb): sample()'s operations in its order
 __device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, const float4& t01, const float4& t11,
                                         float fa, float fb) {
-    const float ia = 1.0f - fa, ib = 1.0f - fb;  // sample()'s operations in its order
+    const float ia = 1.0f - fa, ib = 1.0f - fb;
     F4 q;
     q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
     q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
@@ -505,79 +519,125 @@ __device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, co
     q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
     return q;
 }
-__global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, const uint2* __restrict__ sep,
-                                           Tex out) {
+template <int FP, bool A1>
+__device__ __forceinline__ F4 lerp_sep(const float4* T, int32_t o, const SepEntry& c, const SepEntry& r) {
+    const float4 t00 = T[o], t10 = T[o + 1];
+    const float4 t01 = T[o + FP], t11 = T[o + FP + 1];
+    const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;    // sample()'s operations in its order
+    F4 q;
+    q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+    q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+    q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+    // an opaque block's texels all have alpha 1.0, and then every tap's alpha is exactly 1.0:
+    // RN(ia + fa) == 1 for fa in [0, 1) and ia = RN(1 - fa) (|ia + fa - 1| <= 2^-25), likewise along y
+    q.a = A1 ? 1.0f : (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+    return q;
+}
+
+// FP: the staged footprint's side; FS: the tile's row stride in float4, a multiple of 16 (see FS_YQ: in a
+// same-size pass lane l reads column ~l & 15 of row ~l >> 4)
+template <int FP, uint32_t EPI, int FS = (FP + 15) / 16 * 16>
+__global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, const SepEntry* __restrict__ sep, Tex out, CTex own0,
+                                           CTex own1, const uint2* __restrict__ same, Tex aux) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_UP * FP_UP];
-    __shared__ uint2 colp[8][16], rowp[8][16];
+    __shared__ float4 tile[FP * FS];
+    __shared__ SepEntry colp[8][16], rowp[8][16];
     const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
+    const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t tx = threadIdx.x & 15u, ty = threadIdx.x >> 4;
     const uint32_t x = bx + tx, y = by + ty;
-    const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
-    const Taps k(rx, ry);
-    const Span sx = tap_span(bx, min(bx + 15u, out.w - 1u), Rw, k.du_min(), k.du_max(), a.w);
-    const Span sy = tap_span(by, min(by + 15u, out.h - 1u), Rh, k.dv_min(), k.dv_max(), a.h);
-    const bool staged = sx.n <= FP_UP && sy.n <= FP_UP;  // block-uniform
-    // this block's plan entries: 8 taps x 16 columns, 8 taps x 16 rows (thread t: tap t >> 4 of column
-    // or row t & 15, clamped to the frame)
+    const bool in = x < ow && y < oh;
+    // the block's footprint: floors are monotone in the column (row), so the taps' floors at the first
+    // and last column bound it (scalar loads: block-uniform addresses)
+    const uint32_t xl = min(bx + 15u, ow - 1u), yl = min(by + 15u, oh - 1u);
+    int32_t lo_x = INT_MAX, hi_x = INT_MIN, lo_y = INT_MAX, hi_y = INT_MIN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        lo_x = min(lo_x, sep[i * ow + bx].f);
+        hi_x = max(hi_x, sep[i * ow + xl].f);
+        lo_y = min(lo_y, sep[8u * ow + i * oh + by].f);
+        hi_y = max(hi_y, sep[8u * ow + i * oh + yl].f);
+    }
+    const int32_t nx = hi_x - lo_x + 2, ny = hi_y - lo_y + 2;  // floor .. floor + 1
+    // the host sizes FP for the launch (bh_bloom_sep_plan's extent); a larger block footprint never
+    // occurs, and would read the clamped tile edge rather than outside it
+    // this block's plan entries, as tile offsets: thread t < 128 column entry (t >> 4, t & 15), else row
     {
-        const uint32_t i = threadIdx.x >> 4, j = threadIdx.x & 15u;
-        if (i < 8u) {
-            colp[i][j] = sep[i * out.w + min(bx + j, out.w - 1u)];
-            rowp[i][j] = sep[8u * out.w + i * out.h + min(by + j, out.h - 1u)];
+        const uint32_t i = (threadIdx.x >> 4) & 7u, j = threadIdx.x & 15u;
+        if (threadIdx.x < 128u) {
+            SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
+            e.f -= lo_x;
+            colp[i][j] = e;
+        } else {
+            SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
+            e.f = (e.f - lo_y) * FS;
+            rowp[i][j] = e;
         }
     }
-    constexpr int R = (FP_UP * FP_UP + 255) / 256;
+    // own texels of the epilogue, loaded before the footprint and the tables, used last
+    const uint32_t pix = (in ? y : 0u) * ow + (in ? x : 0u);
+    uint32_t o0 = 0xFF000000u, o1 = 0xFF000000u;
+    bool exact = false;
+    if constexpr (EPI != EPI_PLAIN) {
+        o0 = own0.px[pix];
+        if constexpr (EPI == EPI_FINAL) o1 = own1.px[pix];
+        exact = in && same[in ? x : 0u].y == 0u && same[ow + (in ? y : 0u)].y == 0u;
+    }
+    constexpr int R = (FP * FP + 255) / 256;
     uint32_t raw[R];
-    const int32_t n = sx.n * sy.n;
-    if (staged) {
+    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
+    const int32_t cx = min(nx, FP), cy = min(ny, FP);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int32_t i = (int32_t)threadIdx.x + r * 256;
-            if (i < n) {
-                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-                raw[r] = a.px[(uint32_t)(sy.lo + ly) * a.w + (sx.lo + lx)];
-            }
-        }
+    for (int r = 0; r < R; ++r) {
+        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
+        raw[r] = 0xFF000000u;
+        if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
     }
-    load_tables(tb, L);  // after the footprint's loads are issued
-    if (staged) {
+    load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
+    uint32_t m = min(o0, o1);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int32_t i = (int32_t)threadIdx.x + r * 256;
-            if (i < n) {
-                const int32_t ly = i / sx.n, lx = i - ly * sx.n;
-                const F4 d = dec(L, raw[r]);
-                tile[ly * FP_UP + lx] = make_float4(d.r, d.g, d.b, d.a);
-            }
+    for (int r = 0; r < R; ++r) {
+        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
+        if (ly < cy) {
+            const F4 d = dec(L, raw[r]);
+            tile[ly * FS + lx] = make_float4(d.r, d.g, d.b, d.a);
         }
-        __syncthreads();
+        m = min(m, raw[r]);
     }
-    if (x >= out.w || y >= out.h) return;
-    F4 s{0.0f, 0.0f, 0.0f, 0.0f};
-    // the taps over a texel source (staged tile or global), one at a time (the sched barrier and the
-    // empty asm on the sums keep the compiler from hoisting later taps' reads or sinking this tap's work)
-    auto taps = [&](auto fetch) {
+    // every staged texel (and every own texel) opaque: alpha 1.0 throughout, its arithmetic folds away
+    const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+    if (!in) return;
+    auto run = [&](auto A1c) {
+        constexpr bool A1 = decltype(A1c)::value;
+        F4 s{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const uint2 c = colp[i][tx], r = rowp[i][ty];
-            const int32_t x0 = (int32_t)(c.x & 0xFFFFu), x1 = (int32_t)(c.x >> 16);
-            const int32_t y0 = (int32_t)(r.x & 0xFFFFu), y1 = (int32_t)(r.x >> 16);
-            acc(s, lerp_plan(fetch(x0, y0), fetch(x1, y0), fetch(x0, y1), fetch(x1, y1), __uint_as_float(c.y),
-                             __uint_as_float(r.y)), i);
+            // one tap at a time (the sched barrier and the empty asm on the sums keep the compiler from
+            // hoisting later taps' reads or sinking this tap's work)
+            const SepEntry c = colp[i][tx], r = rowp[i][ty];
+            acc(s, lerp_sep<FS, A1>(tile, c.f + r.f, c, r), i);
             asm volatile("" ::"v"(s.r), "v"(s.g), "v"(s.b), "v"(s.a));
             __builtin_amdgcn_sched_barrier(0);
         }
+        const F4 u = div12(s);
+        if constexpr (EPI == EPI_PLAIN) {
+            out.px[pix] = enc(L, u);
+        } else {
+            const uint32_t ue = enc(L, u);
+            aux.px[pix] = ue;
+            if (exact) {
+                const F4 uq = dec<A1>(L, ue);
+                if constexpr (EPI == EPI_Y) {
+                    out.px[pix] = enc(L, remix(dec<A1>(L, o0), uq));
+                } else {
+                    const F4 z = quant<A1>(L, remix(dec<A1>(L, o1), uq));
+                    out.px[pix] = enc(L, remix(dec<A1>(L, o0), z));
+                }
+            }
+        }
     };
-    if (staged) {
-        taps([&](int32_t u, int32_t v) { return tile[(v - sy.lo) * FP_UP + (u - sx.lo)]; });
-    } else {
-        taps([&](int32_t u, int32_t v) {
-            const F4 q = dec(L, a.px[(uint32_t)v * a.w + u]);
-            return make_float4(q.r, q.g, q.b, q.a);
-        });
-    }
-    out.px[(uint32_t)y * out.w + x] = enc(L, div12(s));
+    if (a1) run(std::true_type{});
+    else run(std::false_type{});
 }
 
 // ---- remixes of the chain at any proven-identity size (general fused schedule) ----------------------
@@ -643,6 +703,50 @@ __global__ void __launch_bounds__(256) remix2_plan_kernel(Tables tb, CTex col, C
                       make_float4(d.r, d.g, d.b, d.a), fa, fb);
     }
     out.px[y * out.w + x] = enc(L, remix(sample_same(L, col, cx, cy), f));
+}
+
+// The pixels the fused epilogues of up_sep_kernel skip: every pixel of a column or row whose same-size
+// sample is inexact.  `list` = the n_cols inexact columns, then the n_rows inexact rows; thread i
+// covers pixel i of the columns' pixels (all rows), then of the rows' pixels (all columns but the
+// listed ones).  EPI_Y: out = remix(S(A), S(B)) (A = X, B = U1); EPI_FINAL: out = remix(S(A), S(F)),
+// F = q(remix(S(B), S(C))) (A = col, B = Y, C = B-texture) -- remix_plan_kernel's / remix2_plan_kernel's
+// per-pixel arithmetic.
+template <uint32_t EPI>
+__global__ void __launch_bounds__(256) fixup_kernel(Tables tb, CTex A, CTex B, CTex C, const uint2* __restrict__ plan,
+                                                    const uint32_t* __restrict__ list, uint32_t n_cols, uint32_t n_rows,
+                                                    Tex out) {
+    __shared__ Lds L;
+    load_tables(tb, L);
+    const uint32_t W = out.w, H = out.h;
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x, nc = (uint64_t)n_cols * H;
+    uint32_t x, y;
+    if (i < nc) {
+        x = list[i / H];
+        y = (uint32_t)(i % H);
+    } else {
+        const uint64_t j = i - nc;
+        if (j >= (uint64_t)n_rows * W) return;
+        y = list[n_cols + j / W];
+        x = (uint32_t)(j % W);
+        if (plan[x].y != 0u) return;  // an inexact column: its pixels are the first part's
+    }
+    const uint2 cx = plan[x], cy = plan[W + y];
+    if constexpr (EPI == EPI_Y) {
+        out.px[y * W + x] = enc(L, remix(sample_same(L, A, cx, cy), sample_same(L, B, cx, cy)));
+    } else {
+        auto F = [&](uint32_t u, uint32_t v) {
+            const uint2 px = plan[u], py = plan[W + v];
+            return quant(L, remix(sample_same(L, B, px, py), sample_same(L, C, px, py)));
+        };
+        const float fa = __uint_as_float(cx.y), fb = __uint_as_float(cy.y);
+        const uint32_t x0 = cx.x & 0xFFFFu, x1 = cx.x >> 16, y0 = cy.x & 0xFFFFu, y1 = cy.x >> 16;
+        const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
+        const bool ex = fa != 0.0f, ey = fb != 0.0f;
+        const F4 a = F(x0, y0), b = ex ? F(x1, y0) : z, c = ey ? F(x0, y1) : z, d = ex && ey ? F(x1, y1) : z;
+        const F4 f = lerp_plan(make_float4(a.r, a.g, a.b, a.a), make_float4(b.r, b.g, b.b, b.a),
+                               make_float4(c.r, c.g, c.b, c.a), make_float4(d.r, d.g, d.b, d.a), fa, fb);
+        out.px[y * W + x] = enc(L, remix(sample_same(L, A, cx, cy), f));
+    }
 }
 
 // One render pass of the reference (literal schedule): 16x16 pixels per 256-thread block.
@@ -727,13 +831,21 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
 // four pixels (14 LDS reads per pixel instead of 21 at 4096x2048), each pixel reduced exactly as
 // up8(PlanSrc) does.  HX / HY: the tap's half flags.
 constexpr int FP_YQ = 40;  // 32 + the taps' reach (38 at 4096x2048)
+// The tile's row stride in float4: a multiple of 16 (256 B, all 64 banks), so that the quad loops'
+// ds_read_b128 -- lane l reads column l & 15 of row l >> 4, and the instruction's lane groups {0-3, 12-15,
+// 20-27}, {4-11, 16-19, 28-31}, ... take two rows each -- touch 16 distinct 4-bank slots per group (a
+// 40-float4 stride puts row 1's columns 4-11 on the slots of row 0's 12-15 and 0-3: 2-way conflicts).
+#ifndef BH_BLOOM_FS_YQ
+#define BH_BLOOM_FS_YQ 48
+#endif
+constexpr int FS_YQ = BH_BLOOM_FS_YQ;
 template <int HX, int HY>
 __device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2]) {
     float4 t[2 + HY][2 + HX];
 #pragma unroll
     for (int r = 0; r < 2 + HY; ++r)
 #pragma unroll
-        for (int c = 0; c < 2 + HX; ++c) t[r][c] = T[r * FP_YQ + c];
+        for (int c = 0; c < 2 + HX; ++c) t[r][c] = T[r * FS_YQ + c];
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -753,7 +865,7 @@ __device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2])
 template <int STD>
 __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_YQ * FP_YQ];
+    __shared__ float4 tile[FP_YQ * FS_YQ];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;  // the footprint, clamp-to-edge
     {
@@ -772,14 +884,14 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
             if (ly < ny) {
                 const F4 d = dec(L, raw[r]);
-                tile[ly * FP_YQ + lx] = make_float4(d.r, d.g, d.b, d.a);
+                tile[ly * FS_YQ + lx] = make_float4(d.r, d.g, d.b, d.a);
             }
         }
     }
     __syncthreads();
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     if (x >= Y.w || y >= Y.h) return;
-    const int32_t base = ((int32_t)y - y0) * FP_YQ + ((int32_t)x - x0);
+    const int32_t base = ((int32_t)y - y0) * FS_YQ + ((int32_t)x - x0);
     F4 s[2][2];
     // Y = X + 0.5 q(blur1 / 12) per pixel of the quad; both pixels of each quad row in one 8-byte store:
     // inside the frame, and rows 8-byte aligned (even width; x is even); else one word per pixel
@@ -791,7 +903,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const F4 b1 = quant(L, div12(s[b][a]));
-                const float4 v = tile[base + b * FP_YQ + a];  // the pixel's own texel
+                const float4 v = tile[base + b * FS_YQ + a];  // the pixel's own texel
                 c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
             }
             if (full) {
@@ -807,7 +919,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
         // the standard plan: constant offsets and halves, one tap at a time (see quad_taps_std)
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const float4* T = tile + (base + fdiv8(STD * tap_m(1, i)) * FP_YQ + fdiv8(STD * tap_m(0, i)));
+            const float4* T = tile + (base + fdiv8(STD * tap_m(1, i)) * FS_YQ + fdiv8(STD * tap_m(0, i)));
             switch ((fmod8(STD * tap_m(0, i)) == 4 ? 1 : 0) | (fmod8(STD * tap_m(1, i)) == 4 ? 2 : 0)) {
                 case 0: yquad_tap<0, 0>(T, i, s); break;
                 case 1: yquad_tap<1, 0>(T, i, s); break;
@@ -821,7 +933,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     } else {
 #pragma unroll 1
         for (int i = 0; i < 8; i++) {
-            const float4* T = tile + (base + P.oy[i] * FP_YQ + P.ox[i]);
+            const float4* T = tile + (base + P.oy[i] * FS_YQ + P.ox[i]);
             switch (((P.hx >> i) & 1u) | ((P.hy >> i) & 1u) << 1) {  // launch-uniform
                 case 0: yquad_tap<0, 0>(T, i, s); break;
                 case 1: yquad_tap<1, 0>(T, i, s); break;
@@ -1070,11 +1182,16 @@ __device__ __forceinline__ void quad_taps_std(const float4* base, F4 (&s)[2][2],
 // outermost blocks (and footprints over FP) take the general sampler per pixel.  STD: 0 = the runtime
 // plan P, else the standard plan A = STD (P still gives the interior).
 constexpr int FP_UPQ = 28;  // footprint of 16 texels + the taps' reach (24 at 4096x2048)
+// row stride in float4, a multiple of 16 for the quad reads' lane groups (see FS_YQ)
+#ifndef BH_BLOOM_FS_UPQ
+#define BH_BLOOM_FS_UPQ 32
+#endif
+constexpr int FS_UPQ = BH_BLOOM_FS_UPQ;
 template <int STD>
 __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P,
                                         Tex out) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_UPQ * FP_UPQ];
+    __shared__ float4 tile[FP_UPQ * FS_UPQ];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
@@ -1102,7 +1219,7 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
             if (i < n) {
                 const int32_t ly = i / sx.n, lx = i - ly * sx.n;
                 const F4 d = dec(L, raw[r]);
-                tile[ly * FP_UPQ + lx] = make_float4(d.r, d.g, d.b, d.a);
+                tile[ly * FS_UPQ + lx] = make_float4(d.r, d.g, d.b, d.a);
             }
         }
         __syncthreads();
@@ -1118,27 +1235,27 @@ __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t
         for (int j = 0; j < 4; ++j) {
             const uint32_t px = x + (j & 1), py = y + (j >> 1);
             const float u = texcoord(px, Rw), v = texcoord(py, Rh);
-            const F4 r = staged ? up8(TileSrc<FP_UPQ>{a, tile, sx.lo, sy.lo}, k, u, v, point)
+            const F4 r = staged ? up8(TileSrc<FS_UPQ>{a, tile, sx.lo, sy.lo}, k, u, v, point)
                                 : up8(GlobalSrc{a, &L}, k, u, v, point);
             out.px[(uint32_t)py * out.w + px] = enc(L, r);
         }
         return;
     }
     F4 s[2][2];
-    const int32_t base = ((int32_t)(y >> 1) - sy.lo) * FP_UPQ + ((int32_t)(x >> 1) - sx.lo);
+    const int32_t base = ((int32_t)(y >> 1) - sy.lo) * FS_UPQ + ((int32_t)(x >> 1) - sx.lo);
     if constexpr (STD != 0) {
-        quad_taps_std<FP_UPQ, STD>(tile + base, s, std::make_integer_sequence<int, 8>{});
+        quad_taps_std<FS_UPQ, STD>(tile + base, s, std::make_integer_sequence<int, 8>{});
     } else {
         // rolled (the plan read by scalar loads; unrolled, the taps' LDS reads are hoisted together)
 #pragma unroll 1
         for (int i = 0; i < 8; i++) {
-            const float4* T = tile + (base + P.oy[0][i] * FP_UPQ + P.ox[0][i]);
+            const float4* T = tile + (base + P.oy[0][i] * FS_UPQ + P.ox[0][i]);
             const uint32_t d = (uint32_t)(P.ox[1][i] - P.ox[0][i]) | (uint32_t)(P.oy[1][i] - P.oy[0][i]) << 1;
             switch (d) {  // wave-uniform
-                case 0: quad_tap<FP_UPQ, 0, 0>(T, P, i, s); break;
-                case 1: quad_tap<FP_UPQ, 1, 0>(T, P, i, s); break;
-                case 2: quad_tap<FP_UPQ, 0, 1>(T, P, i, s); break;
-                default: quad_tap<FP_UPQ, 1, 1>(T, P, i, s); break;
+                case 0: quad_tap<FS_UPQ, 0, 0>(T, P, i, s); break;
+                case 1: quad_tap<FS_UPQ, 1, 0>(T, P, i, s); break;
+                case 2: quad_tap<FS_UPQ, 0, 1>(T, P, i, s); break;
+                default: quad_tap<FS_UPQ, 1, 1>(T, P, i, s); break;
             }
         }
     }
@@ -1346,34 +1463,97 @@ int std_tap_plan(const TapPlan& P) {
     return 0;
 }
 
-// The separable plan of an 8-tap pass (see up_sep_kernel): 8 * (ow + oh) uint2 entries into `outp`
-// ((x0 | x1 << 16, weight bits) per tap and column, then per tap and row), from the kernel's own f32
-// arithmetic: texcoord (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset,
-// sample_coord, floor and the clamps.  Texture sides above 65535 do not fit and return false.
-extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
-                                                                      uint32_t th, uint32_t rx, uint32_t ry,
-                                                                      uint32_t* outp) {
-    if (tw > 65535u || th > 65535u || tw == 0u || th == 0u) return false;
+// The separable plan of an 8-tap pass (see SepEntry / up_sep_kernel): 8 * (ow + oh) entries of 4 words
+// into `outp` (per tap and column, then per tap and row), from the kernel's own f32 arithmetic: texcoord
+// (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset, sample_coord and
+// floor.  Returns the largest 16x16 block footprint along either axis (the staged tile's side), or -1
+// (texture sides above 65535).
+extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                     uint32_t th, uint32_t rx, uint32_t ry,
+                                                                     uint32_t* outp) {
+    if (tw > 65535u || th > 65535u || tw == 0u || th == 0u || ow == 0u || oh == 0u) return -1;
     const float hx = 0.5f / (float)rx, hy = 0.5f / (float)ry;
-    auto axis = [](uint32_t on, uint32_t tn, float d, uint32_t* o, uint32_t x) {
-        const float u = ((float)x + 0.5f) / (float)on + d;
-        const float t = h_sample_coord(u, tn);
-        const float f = floorf(t);
-        const int32_t hi = (int32_t)tn - 1;
-        const int32_t a0 = std::min(std::max((int32_t)f, 0), hi), a1 = std::min(std::max((int32_t)f + 1, 0), hi);
-        const float w = t - f;
-        uint32_t wb;
-        std::memcpy(&wb, &w, 4);
-        o[0] = (uint32_t)a0 | (uint32_t)a1 << 16;
-        o[1] = wb;
+    auto axis = [](uint32_t on, uint32_t tn, float d, uint32_t x, uint32_t* o) {
+        const float t = h_sample_coord(((float)x + 0.5f) / (float)on + d, tn);
+        const float f = floorf(t), fa = t - f, ia = 1.0f - fa;
+        const int32_t fi = (int32_t)f;
+        std::memcpy(&o[0], &fi, 4);
+        std::memcpy(&o[1], &fa, 4);
+        std::memcpy(&o[2], &ia, 4);
+        o[3] = 0u;
     };
+    auto fl = [&](size_t e) { int32_t v; std::memcpy(&v, outp + 4u * e, 4); return v; };
     for (int i = 0; i < 8; ++i) {
         const float du = (hx * (float)((int)((0x12343210u >> (4 * i)) & 15u) - 2)) * 3.0f;
         const float dv = (hy * (float)((int)((0x10123432u >> (4 * i)) & 15u) - 2)) * 3.0f;
-        for (uint32_t x = 0; x < ow; ++x) axis(ow, tw, du, outp + 2u * ((size_t)i * ow + x), x);
-        for (uint32_t y = 0; y < oh; ++y) axis(oh, th, dv, outp + 2u * (8u * (size_t)ow + (size_t)i * oh + y), y);
+        for (uint32_t x = 0; x < ow; ++x) axis(ow, tw, du, x, outp + 4u * ((size_t)i * ow + x));
+        for (uint32_t y = 0; y < oh; ++y) axis(oh, th, dv, y, outp + 4u * (8u * (size_t)ow + (size_t)i * oh + y));
     }
-    return true;
+    int ext = 0;
+    for (int ax = 0; ax < 2; ++ax) {
+        const uint32_t n = ax ? oh : ow;
+        const size_t base = ax ? 8u * (size_t)ow : 0u;
+        for (uint32_t b = 0; b < n; b += 16u) {
+            const uint32_t l = std::min(b + 15u, n - 1u);
+            int32_t lo = INT_MAX, hi = INT_MIN;
+            for (int i = 0; i < 8; ++i) {
+                lo = std::min(lo, fl(base + (size_t)i * n + b));
+                hi = std::max(hi, fl(base + (size_t)i * n + l));
+            }
+            ext = std::max(ext, hi - lo + 2);
+        }
+    }
+    return ext;
+}
+
+// The staged tile side of up_sep_kernel for a plan's footprint extent, or 0 (too large: the general pass)
+static int sep_tile(int ext) { return ext <= 0 ? 0 : ext <= 24 ? 24 : ext <= 44 ? 44 : 0; }
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
+                                                                        const uint8_t* buckets, const uint32_t* codes,
+                                                                        const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                        const uint32_t* sep, int ext, uint32_t epi,
+                                                                        const uint32_t* own0, const uint32_t* own1,
+                                                                        const uint32_t* same, uint32_t* out, uint32_t* aux,
+                                                                        uint32_t ow, uint32_t oh, hipStream_t s) {
+    const Tables tb{lut, enc, buckets, codes};
+    const CTex A{a, aw, ah}, O0{own0 ? own0 : a, ow, oh}, O1{own1 ? own1 : a, ow, oh};
+    const SepEntry* P = reinterpret_cast<const SepEntry*>(sep);
+    const uint2* S = reinterpret_cast<const uint2*>(same);
+    const Tex O{out, ow, oh}, X{aux ? aux : out, ow, oh};
+    const dim3 g = grid_for(ow, oh);
+#define BH_SEP(FP, E) hipLaunchKernelGGL((up_sep_kernel<FP, E>), g, dim3(256), 0, s, tb, A, P, O, O0, O1, S, X)
+    const int fp = sep_tile(ext);
+    if (fp == 24) {
+        if (epi == EPI_Y) BH_SEP(24, EPI_Y); else if (epi == EPI_FINAL) BH_SEP(24, EPI_FINAL); else BH_SEP(24, EPI_PLAIN);
+    } else if (fp == 44) {
+        if (epi == EPI_Y) BH_SEP(44, EPI_Y); else if (epi == EPI_FINAL) BH_SEP(44, EPI_FINAL); else BH_SEP(44, EPI_PLAIN);
+    } else {
+        return (int)hipErrorInvalidValue;
+    }
+#undef BH_SEP
+    return (int)hipGetLastError();
+}
+
+// The fix-up pass of a fused epilogue (fixup_kernel): `list` = n_cols columns then n_rows rows
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const float* lut, const float* enc,
+                                                                          const uint8_t* buckets, const uint32_t* codes,
+                                                                          uint32_t epi, const uint32_t* a, const uint32_t* b,
+                                                                          const uint32_t* c, const uint32_t* same,
+                                                                          const uint32_t* list, uint32_t n_cols,
+                                                                          uint32_t n_rows, uint32_t* out, uint32_t w,
+                                                                          uint32_t h, hipStream_t s) {
+    const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
+    if (n == 0) return 0;
+    const Tables tb{lut, enc, buckets, codes};
+    const dim3 g((uint32_t)((n + 255u) / 256u));
+    const uint2* S = reinterpret_cast<const uint2*>(same);
+    if (epi == EPI_Y)
+        hipLaunchKernelGGL(fixup_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{b, w, h}, S, list,
+                           n_cols, n_rows, Tex{out, w, h});
+    else
+        hipLaunchKernelGGL(fixup_kernel<EPI_FINAL>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{c, w, h}, S,
+                           list, n_cols, n_rows, Tex{out, w, h});
+    return (int)hipGetLastError();
 }
 
 // The same-size plan of a w x h frame (remix_plan_kernel): per column, then per row, the two clamped
@@ -1446,7 +1626,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
                                                                          uint32_t aw, uint32_t ah, const uint32_t* b,
                                                                          uint32_t rx, uint32_t ry, uint32_t* out,
                                                                          uint32_t ow, uint32_t oh, const uint32_t* sep,
-                                                                         hipStream_t s) {
+                                                                         int sep_ext, hipStream_t s) {
     const Tables tb{lut, enc, buckets, codes};
     const CTex A{a, aw, ah}, B{b ? b : a, aw, ah};
     const Tex O{out, ow, oh};
@@ -1464,10 +1644,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
             return (int)hipGetLastError();
         }
     }
-    if (shader == SH_UP && !P.valid && sep && !g_no_sep) {
-        hipLaunchKernelGGL(up_sep_kernel, grid_for(ow, oh), dim3(256), 0, s, tb, A, rx, ry,
-                           reinterpret_cast<const uint2*>(sep), O);
-        return (int)hipGetLastError();
+    if (shader == SH_UP && !P.valid && sep && sep_tile(sep_ext) != 0 && !g_no_sep) {
+        return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, sep, sep_ext, EPI_PLAIN, nullptr, nullptr, nullptr,
+                                   out, nullptr, ow, oh, s);
     }
     switch (shader) {
         case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;

@@ -235,10 +235,26 @@ extern "C" __attribute__((visibility("hidden"))) void bh_srgb_bucket_table(const
 extern "C" __attribute__((visibility("hidden"))) bool bh_srgb_code_table(const float* T257, uint32_t* E);
 // bh_bloom.hip pass shaders (bh::bloom::Shader)
 constexpr uint32_t bh_bloom_shader_copy = 0, bh_bloom_shader_down = 1, bh_bloom_shader_up = 2, bh_bloom_shader_remix = 3;
-// the separable plan of an 8-tap pass (bh_bloom.hip): 8 * (ow + oh) uint2 entries
-extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
-                                                                      uint32_t th, uint32_t rx, uint32_t ry,
-                                                                      uint32_t* outp);
+// the separable plan of an 8-tap pass (bh_bloom.hip): 8 * (ow + oh) entries of 4 words; returns the largest
+// block footprint side (or -1)
+extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                     uint32_t th, uint32_t rx, uint32_t ry,
+                                                                     uint32_t* outp);
+// an up pass from its separable plan with an epilogue (bh_bloom.hip SepEpi: 0 plain, 1 Y, 2 final)
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
+                                                                        const uint8_t* buckets, const uint32_t* codes,
+                                                                        const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                        const uint32_t* sep, int ext, uint32_t epi,
+                                                                        const uint32_t* own0, const uint32_t* own1,
+                                                                        const uint32_t* same, uint32_t* out, uint32_t* aux,
+                                                                        uint32_t ow, uint32_t oh, hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const float* lut, const float* enc,
+                                                                          const uint8_t* buckets, const uint32_t* codes,
+                                                                          uint32_t epi, const uint32_t* a, const uint32_t* b,
+                                                                          const uint32_t* c, const uint32_t* same,
+                                                                          const uint32_t* list, uint32_t n_cols,
+                                                                          uint32_t n_rows, uint32_t* out, uint32_t w,
+                                                                          uint32_t h, hipStream_t s);
 // the same-size plan of a w x h frame (bh_bloom.hip): (w + h) uint2 entries; the plan remixes
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_plan(uint32_t w, uint32_t h, uint32_t* outp);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(const float* lut, const float* enc,
@@ -262,7 +278,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
                                                                          const uint32_t* codes, const uint32_t* a,
                                                                          uint32_t aw, uint32_t ah, const uint32_t* b,
                                                                          uint32_t rx, uint32_t ry, uint32_t* out,
-                                                                         uint32_t ow, uint32_t oh, const uint32_t* sep,
+                                                                         uint32_t ow, uint32_t oh, const uint32_t* sep, int sep_ext,
                                                                          hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
                                                                       const uint8_t* buckets, const uint32_t* codes,

@@ -35,6 +35,15 @@ __device__ __forceinline__ float sqrt_core(float x) {
     const float r = __builtin_fmaf(-s, s, x);
     return __builtin_fmaf(r, h, s);
 }
+// the same, also handing back the v_rsq estimate y it refined (rcp_from_rsq seeds a reciprocal from it)
+struct SqrtY { float s, y; };
+__device__ __forceinline__ SqrtY sqrt_core_y(float x) {
+    const float y = __builtin_amdgcn_rsqf(x);
+    const float s = x * y;
+    const float h = 0.5f * y;
+    const float r = __builtin_fmaf(-s, s, x);
+    return {__builtin_fmaf(r, h, s), y};
+}
 // unsafe iff x is outside [2^-96, FLT_MAX] (0, +inf and NaN included)
 __device__ __forceinline__ bool sqrt_bad(float x) { return !(x >= SQRT_MIN && x <= SQRT_MAX); }
 // the same for two values (one v_min + one v_max + two compares)
@@ -65,6 +74,17 @@ __device__ __forceinline__ Rcp rcp_refined(float d) {
     const float e = __builtin_fmaf(-d, r, 1.0f);
     r = __builtin_fmaf(e, r, r);
     return {d, r};
+}
+// RN(1/Q) of rd_derivative's denominator Q = RN(RN(q*q) * sqrt(q)) without a second transcendental:
+// y = v_rsq(q) (the square-root core's own estimate) gives the seed z = (y^2)^2 * y ~ q^-2.5 (three
+// multiplies, 6 issue cycles, where v_rcp takes 8 and blocks the SIMD's vector issue for all of them:
+// tools/ubench/trans_mix.hip), within ~2^-20 of 1/Q; one refinement r = z + z(1 - Qz) lands within
+// ~2^-40 of 1/Q before its rounding.  Equal to rcp_refined(Q).r = RN(1/Q) for EVERY q whose Q passes
+// div_d_bad (selftest op 12, exhaustive over q in [2^-17, 2^25)), so every quotient is unchanged.
+__device__ __forceinline__ Rcp rcp_from_rsq(float Q, float y) {
+    const float y2 = y * y, y4 = y2 * y2, z = y4 * y;
+    const float e = __builtin_fmaf(-Q, z, 1.0f);
+    return {Q, __builtin_fmaf(e, z, z)};
 }
 __device__ __forceinline__ float div_core(float n, const Rcp& R) {
     const float y = n * R.r;

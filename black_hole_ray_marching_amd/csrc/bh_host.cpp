@@ -66,7 +66,8 @@ struct bh_ctx {
     // separable plans of its up passes (sep_plan).  Graph contract as the order states: a set used under
     // stream capture is never evicted (bh_graph_release clears the mark); others are evicted least
     // recently used beyond BH_BLOOM_SETS.
-    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; };
+    // ext: the largest block footprint side (up passes); nc, nr: the inexact columns / rows (same plan)
+    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; int ext; uint32_t nc, nr; };
     struct BloomScratch {
         uint64_t key = 0;
         std::vector<uint32_t*> tex;
@@ -664,33 +665,50 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 }
 
 // The separable plan of an up pass of this shape (bh_bloom_sep_plan), on the device, built at its first
-// use and kept with the scratch set (16 B per column and row); NULL if the shape does not fit the plan.
-// A capturing call never builds one (bh_bloom refuses a set not prepared outside capture).
-const uint32_t* sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th,
-                         uint32_t rx, uint32_t ry, int* err) {
+// use and kept with the scratch set (64 B per column and row); NULL if the shape does not fit the plan.
+// rx == 0: the same-size plan of the remixes (bh_bloom_same_plan, 8 B per column and row) followed by the
+// list of its inexact columns, then rows (the fused epilogues' fix-up pixels).  A capturing call never
+// builds one (bh_bloom refuses a set not prepared outside capture).
+const bh_ctx::SepPlan* sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw,
+                                uint32_t th, uint32_t rx, uint32_t ry, int* err) {
     const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
     for (const auto& p : b->sep_plans)
-        if (p.key == key) return p.dev;
+        if (p.key == key) return &p;
     if (capturing) {
         *err = (int)hipErrorStreamCaptureUnsupported;
         return nullptr;
     }
-    // rx == 0: the same-size plan of the remixes (bh_bloom_same_plan), one tap
-    std::vector<uint32_t> h((rx ? 16u : 2u) * ((size_t)ow + oh));
-    if (!(rx ? bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data()) : bh_bloom_same_plan(ow, oh, h.data()))) {
+    bh_ctx::SepPlan P{key, nullptr, 0, 0u, 0u};
+    std::vector<uint32_t> h;
+    if (rx) {
+        h.resize(32u * ((size_t)ow + oh));
+        P.ext = bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data());
+    } else {
+        h.resize(2u * ((size_t)ow + oh));
+        P.ext = bh_bloom_same_plan(ow, oh, h.data()) ? 1 : -1;
+        std::vector<uint32_t> cols, rows;
+        for (uint32_t x = 0; x < ow; ++x)
+            if (h[2u * x + 1u] != 0u) cols.push_back(x);
+        for (uint32_t y = 0; y < oh; ++y)
+            if (h[2u * ((size_t)ow + y) + 1u] != 0u) rows.push_back(y);
+        P.nc = (uint32_t)cols.size();
+        P.nr = (uint32_t)rows.size();
+        h.insert(h.end(), cols.begin(), cols.end());
+        h.insert(h.end(), rows.begin(), rows.end());
+    }
+    if (P.ext < 0) {
         *err = (int)hipErrorInvalidValue;
         return nullptr;
     }
-    uint32_t* d = nullptr;
-    hipError_t e = hipMalloc(&d, h.size() * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemcpy(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    hipError_t e = hipMalloc(&P.dev, h.size() * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemcpy(P.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
-        if (d) (void)hipFree(d);
+        if (P.dev) (void)hipFree(P.dev);
         *err = hip_fail(e, "bloom separable plan");
         return nullptr;
     }
-    b->sep_plans.push_back({key, d});
-    return d;
+    b->sep_plans.push_back(P);
+    return &b->sep_plans.back();
 }
 
 struct BloomRun {
@@ -702,12 +720,12 @@ struct BloomRun {
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
         if (err != 0) return;
-        const uint32_t* sep = sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1])
-                                  ? sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err)
-                                  : nullptr;
+        const bh_ctx::SepPlan* sp = sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1])
+                                        ? sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err)
+                                        : nullptr;
         if (err == 0)
             err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
-                                       sep, s);
+                                       sp ? sp->dev : nullptr, sp ? sp->ext : 0, s);
     }
 };
 
@@ -813,16 +831,39 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         if (R.err == 0)
             R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, c->enc_e, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
     } else if (general) {
-        // general fused chain (same-size passes are identities, see bloom_plan_remixes in bh_bloom.hip):
-        // U1 = up(X) at full size, Y = remix(X, U1) through the same-size plan, the blur's downsamples
-        // and upsamples from Y, B = its last up pass, out = remix(col, q(remix(Y, B))) through the plan
-        const uint32_t* plan = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
+        // general fused chain (same-size passes are identities, same_size_identity): U1 = up(X) at full
+        // size, Y = remix(X, U1) through the same-size plan, the blur's downsamples and upsamples from Y,
+        // B = its last up pass, out = remix(col, q(remix(Y, B))) through the plan.  The two full-size
+        // up passes with a separable plan carry the remixes as epilogues for the pixels whose column and
+        // row sample exactly (bh_bloom.hip up_sep_kernel, EPI_Y / EPI_FINAL) and a fix-up pass covers the
+        // inexact columns and rows; other plans run the plain pass and the plan remix kernels.
+        const bh_ctx::SepPlan* same = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
+        const uint32_t* plan = same ? same->dev : nullptr;
+        const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
+        // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
+        // fix-up of the inexact pixels -- or the plain pass and the remix kernel
+        auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
+                            uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
+            if (R.err != 0) return;
+            const bh_ctx::SepPlan* sp = bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1])
+                                            ? sep_plan(B, capturing, W, H, sw, sh, res[0], res[1], &R.err)
+                                            : nullptr;
+            if (R.err != 0) return;
+            if (sp && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, sp->dev, sp->ext, epi, own0,
+                                          own1, plan, dst, aux, W, H, s) == 0) {
+                R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
+                                              plan, list, same->nc, same->nr, dst, W, H, s);
+                return;
+            }
+            R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);
+            if (R.err != 0) return;
+            R.err = epi == 1u ? bh_launch_bloom_remix_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, aux, plan, dst, W, H, s)
+                              : bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, own1, aux, plan, dst,
+                                                            W, H, s);
+        };
         const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
         if (levels > 1) {
-            uint32_t* U1 = remix_in1[0];
-            R.pass(bh_bloom_shader_up, X, W, H, nullptr, full, U1, W, H);
-            if (R.err == 0)
-                R.err = bh_launch_bloom_remix_plan(c->lut, c->enc, c->enc_b, c->enc_e, X, U1, plan, copy_in[1], W, H, s);
+            fused_up(1u, X, W, H, full, remix_in1[0], X, nullptr, copy_in[1]);
             S = copy_in[1];
         }
         const uint32_t* dn = S;
@@ -838,10 +879,8 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
                    P.res[ti][0], P.res[ti][1]);
             u_src = up[ti];
         }
-        uint32_t* Bt = remix_in1[L];
-        R.pass(bh_bloom_shader_up, u_src, W, H, nullptr, P.res[L], Bt, W, H);
-        if (R.err == 0)
-            R.err = bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, C, S, Bt, plan, O, W, H, s);
+        const uint32_t uw = levels > 1 ? P.res[0][0] : W, uh = levels > 1 ? P.res[0][1] : H;  // up[0] is W x H
+        fused_up(2u, u_src, uw, uh, P.res[L], remix_in1[L], C, S, O);
     } else {
         // literal: the reference's render passes in order (oracle/bh_bloom_oracle.c, bho_bloom)
         if ((e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)
@@ -1055,7 +1094,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     if (!d->out_col) return BH_ERR_INVALID_ARG;
     if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
     if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
-    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGBM) return BH_ERR_INVALID_ARG;
+    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGBM14) return BH_ERR_INVALID_ARG;
     if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER | BH_SCHED_FLAG_ISSUE_ORDER | BH_SCHED_FLAG_LATENCY))) return BH_ERR_INVALID_ARG;
     if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
     if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
@@ -1064,8 +1103,13 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
         if (!descs[i].out_col || !same_launch(d, &descs[i])) return BH_ERR_INVALID_ARG;
         if (!screen_tri_default(&cams[i])) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
     }
-    if (d->layout == BH_LAYOUT_TILES_RGBM && (d->schedule & 0xFFu) == BH_SCHED_PERSISTENT) {
-        g_last_error = "BH_LAYOUT_TILES_RGBM needs the tile or pair schedule";
+    if ((d->layout == BH_LAYOUT_TILES_RGBM || d->layout == BH_LAYOUT_TILES_RGBM14) &&
+        (d->schedule & 0xFFu) == BH_SCHED_PERSISTENT) {
+        g_last_error = "BH_LAYOUT_TILES_RGBM(14) needs the tile or pair schedule";
+        return BH_ERR_UNSUPPORTED;
+    }
+    if (d->layout == BH_LAYOUT_TILES_RGBM14 && d->format != BH_OUT_RGBA16F) {
+        g_last_error = "BH_LAYOUT_TILES_RGBM14 packs RGBA16F only";
         return BH_ERR_UNSUPPORTED;
     }
     if (n_frames > 1u && (d->schedule & 0xFFu) != BH_SCHED_TILE) {  // one launch per frame
@@ -1187,6 +1231,11 @@ int bh_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t heig
     return BH_OK;
 }
 
+// an RGBM unpack's format: a bh_out_format, or BH_OUT_RGBA16F | BH_UNPACK_RGBM14
+static bool unpack_format_ok(uint32_t format) {
+    return format <= BH_OUT_BGRA8_SRGB || format == (BH_OUT_RGBA16F | BH_UNPACK_RGBM14);
+}
+
 int bh_tiles_unpack_rgb_rows(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
                              uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight, void* stream) {
     if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
@@ -1209,7 +1258,7 @@ int bh_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo, uint32_t w
                          uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
                          void* stream) {
     if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
-    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    if (!unpack_format_ok(format)) return BH_ERR_INVALID_ARG;
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
             return BH_ERR_INVALID_ARG;
@@ -1321,7 +1370,7 @@ int64_t bh_partition_tile_count(const bh_partition* P, uint32_t shard_index) {
 int bh_tiles_unpack_rgbm_partition(const void* packed, void* out, void* out_bo, const bh_partition* P,
                                    uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
                                    void* stream) {
-    if (!packed || !out || !P || format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    if (!packed || !out || !P || !unpack_format_ok(format)) return BH_ERR_INVALID_ARG;
     for (uint32_t k = 0; k < P->shard_count; ++k)
         if (P->count[k] > shard_stride_tiles) return BH_ERR_INVALID_ARG;
     int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, P->width, P->height, P->shard_count, shard_stride_tiles,
@@ -1337,6 +1386,7 @@ int64_t bh_tile_bytes(uint32_t layout, uint32_t format) {
         case BH_LAYOUT_TILES: return 64 * bpp;
         case BH_LAYOUT_TILES_RGB: return 48 * bpp;
         case BH_LAYOUT_TILES_RGBM: return 48 * bpp + 8;
+        case BH_LAYOUT_TILES_RGBM14: return format == BH_OUT_RGBA16F ? 344 : BH_ERR_UNSUPPORTED;
         default: return BH_ERR_INVALID_ARG;
     }
 }

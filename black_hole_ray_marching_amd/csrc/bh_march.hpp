@@ -22,6 +22,10 @@
 #ifndef BH_FAST
 #error "define BH_FAST to 0 or 1"
 #endif
+// rd_derivative's reciprocal RN(1/Q) from the root's own v_rsq (crm::rcp_from_rsq) instead of a v_rcp of Q
+#ifndef BH_RCP_SEED
+#define BH_RCP_SEED 1
+#endif
 
 namespace bh {
 namespace BH_NS {
@@ -249,8 +253,9 @@ struct FOps {
         return mk(__builtin_fmaf(0.5f, k.x, ro.x), __builtin_fmaf(0.5f, k.y, ro.y), __builtin_fmaf(0.5f, k.z, ro.z));
     }
     __device__ __forceinline__ v3 rd_half(v3 rd, v3 k) { return ro_half(rd, k); }
+    __device__ __forceinline__ float sqrt_y(float x, float&) { return __builtin_amdgcn_sqrtf(x); }
     template <int K>
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float) {
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float, float = 0.0f) {
         const float iq = rsq(q), iq2 = iq * iq;
         return muls(p, s * (iq2 * iq2 * iq));
     }
@@ -323,6 +328,16 @@ struct XOps {
         if constexpr (CR) return crm::sqrt_core(x);
         else return __builtin_sqrtf(x);
     }
+    // sqrt(x), and (CR) the v_rsq estimate the core refined: rd_derivative's reciprocal is seeded from it
+    __device__ __forceinline__ float sqrt_y(float x, float& y) {
+        if constexpr (CR) {
+            const crm::SqrtY r = crm::sqrt_core_y(x);
+            y = r.y;
+            return r.s;
+        } else {
+            return __builtin_sqrtf(x);
+        }
+    }
     __device__ __forceinline__ void sq_args(float a, float b) {
         if constexpr (CR) bad |= crm::sqrt_bad2(a, b);
     }
@@ -376,8 +391,10 @@ struct XOps {
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
     // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
     // K = 1..4: the RK stage (k1's numerators may be zeros, see above)
+    // y: v_rsq(q) from the root of q (sqrt_y), the seed of RN(1/Q) (crm::rcp_from_rsq; BH_RCP_SEED 0:
+    // a v_rcp of Q instead)
     template <int K>
-    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq) {
+    __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq, float y) {
         const float Q = (q * q) * sq;
         const float nx = s * p.x, ny = s * p.y, nz = s * p.z;
         if constexpr (CR) {
@@ -385,7 +402,7 @@ struct XOps {
             if constexpr (K == 1) kmin = crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz));
             else if constexpr (K == 2) amin = absmin3(nx, ny, nz);
             else amin = absmin3(amin, nx, ny, nz);
-            const crm::Rcp R = crm::rcp_refined(Q);
+            const crm::Rcp R = BH_RCP_SEED ? crm::rcp_from_rsq(Q, y) : crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
         } else {
             return mk(nx / Q, ny / Q, nz / Q);
@@ -394,7 +411,9 @@ struct XOps {
     template <int K>
     __device__ __forceinline__ v3 accel(v3 p, float s) {
         const float q = dot(p, p);
-        return accel_qs<K>(p, s, q, sqrt(q));
+        float y = 0.0f;
+        const float sq = sqrt_y(q, y);
+        return accel_qs<K>(p, s, q, sq, y);
     }
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
@@ -463,7 +482,8 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const float travelled = in.travelled, s = in.s;
     const uint32_t n_rk = in.n_rk;
     const float r2 = dot(ro, ro);
-    const float r = X.sqrt(r2);                                        // :271
+    float y1 = 0.0f;                                                   // v_rsq(r2): k1's reciprocal seed
+    const float r = X.sqrt_y(r2, y1);                                  // :271
     // :272-283: blackout if (r < 1 and rd.ro < 0), or if !(r > 1) and the ray was outside before;
     // r > 1 sets `outside`.  Bitwise (not short-circuit) logic: lane masks, no branches.
     // The tests read r^2: for r = RN(sqrt(r2)),  r < 1  <=>  r2 < 1  and  r > 1  <=>  r2 > 1 + 2^-23
@@ -510,7 +530,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
-    const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r));
+    const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r, y1));
     const v3 ro_k2 = smul(dt, X.rd_half(rd, rd_k1));
     const v3 rd_k2 = smul(dt, X.template accel<2>(X.ro_half(ro, ro_k1), s));
     const v3 ro_k3 = smul(dt, X.rd_half(rd, rd_k2));
@@ -611,19 +631,20 @@ struct PkGuard {
 
 // rd_derivative as XOps<true>::accel_qs<K>
 template <int K>
-__device__ __forceinline__ p3 paccel_qs(p3 p, float s, float q, float sq, PkGuard& G) {
+__device__ __forceinline__ p3 paccel_qs(p3 p, float s, float q, float sq, float y, PkGuard& G) {
     const float Q = (q * q) * sq;
     const p3 n = psmul(s, p);
     G.bad |= crm::div_d_bad(Q);
     if constexpr (K == 1) G.kmin = crm::kmin3(crm::key(n.xy.x), crm::key(n.xy.y), crm::key(n.z));
     else if constexpr (K == 2) G.amin = XOps<true>::absmin3(n.xy.x, n.xy.y, n.z);
     else G.amin = XOps<true>::absmin3(G.amin, n.xy.x, n.xy.y, n.z);
-    return pdiv(n, crm::rcp_refined(Q));
+    return pdiv(n, BH_RCP_SEED ? crm::rcp_from_rsq(Q, y) : crm::rcp_refined(Q));
 }
 template <int K>
 __device__ __forceinline__ p3 paccel(p3 p, float s, PkGuard& G) {
     const float q = pdot(p, p);
-    return paccel_qs<K>(p, s, q, crm::sqrt_core(q), G);
+    const crm::SqrtY sy = crm::sqrt_core_y(q);
+    return paccel_qs<K>(p, s, q, sy.s, sy.y, G);
 }
 
 // step_bf<true, XOps<true>, SF> with packed pairs (see above): same contract (`out` is not written for
@@ -640,7 +661,8 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const f2 sq_xy = ro.xy * ro.xy;                 // x*x, y*y
     const float zz0 = ro.z * ro.z;
     const float r2 = (sq_xy.x + sq_xy.y) + zz0;     // dot(ro, ro)
-    const float r = crm::sqrt_core(r2);
+    const crm::SqrtY sy1 = crm::sqrt_core_y(r2);
+    const float r = sy1.s;
     const bool bo_on = a.blackout_eh != 0u;
     const bool not_out = !(r2 > R2_GT1);
     bool blackout;
@@ -679,7 +701,7 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     const float dist = fminf(ds, dps);
     const float dt = fminf(dist * 0.9f, a.dtm * r);
     const p3 ro_k1 = psmul(dt, rd);
-    const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, G));
+    const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, sy1.y, G));
     const p3 ro_k2 = psmul(dt, pro_half(rd, rd_k1));  // rd + 0.5 k: XOps::rd_half
     const p3 rd_k2 = psmul(dt, paccel<2>(pro_half(ro, ro_k1), s, G));
     const p3 ro_k3 = psmul(dt, pro_half(rd, rd_k2));
@@ -982,6 +1004,28 @@ __device__ __forceinline__ void store_px_planar(void* base, size_t idx, v3 c, co
 template <uint32_t FMT>
 constexpr uint32_t rgbm_tile_elems() { return 192u + 8u / (FMT == BH_OUT_RGBA32F ? 4u : FMT == BH_OUT_RGBA16F ? 2u : 1u); }
 
+// BH_LAYOUT_TILES_RGBM14 store (include/bh_render.h): the RGBA16F channels, each an fp16 in [0, 1] (bits
+// 14-15 zero), as 64 words r | g << 14 | (b & 0xF) << 28, 64 bytes (b >> 4) & 0xFF, the wave's ballots of
+// b's bits 12 and 13, and the blackout mask word -- 86 words per tile.  Every active lane of the wave
+// must hold a pixel of the same tile (as for RGBM); its first active lane stores the three 64-bit words.
+__device__ __forceinline__ void store_rgbm14(void* base, size_t idx, v3 c, bool zero) {
+    const uint32_t r = __half_as_ushort(__float2half_rn(c.x)), g = __half_as_ushort(__float2half_rn(c.y));
+    const uint32_t b = __half_as_ushort(__float2half_rn(c.z));
+    uint32_t* W = reinterpret_cast<uint32_t*>(base) + (idx >> 6) * 86u;
+    const uint32_t e = (uint32_t)idx & 63u;
+    W[e] = r | (g << 14) | (b << 28);
+    reinterpret_cast<uint8_t*>(W + 64)[e] = (uint8_t)(b >> 4);
+    const uint64_t m12 = __builtin_amdgcn_ballot_w64(((b >> 12) & 1u) != 0u);
+    const uint64_t m13 = __builtin_amdgcn_ballot_w64(((b >> 13) & 1u) != 0u);
+    const uint64_t mz = __builtin_amdgcn_ballot_w64(zero);
+    if (e == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec())) {
+        uint64_t* M = reinterpret_cast<uint64_t*>(W + 80);
+        M[0] = m12;
+        M[1] = m13;
+        M[2] = mz;
+    }
+}
+
 // fs_main output (:365-369): col, blackout_col = dot(col,col) < 1 ? 0 : col, debug counters.
 // BH_LAYOUT_TILES_RGBM: every active lane of the calling wave must hold a pixel of the same tile
 // (true of the tile and pair schedules, bh_render rejects the others): the wave's ballot of the
@@ -1004,6 +1048,11 @@ __device__ __forceinline__ void write_pixel(const MarchArgs& a, const float* tab
             const size_t w = ((idx >> 6) * TE + 192u) * CB / 8u;  // the mask word (8-byte aligned)
             reinterpret_cast<uint64_t*>(a.out_col)[w] = m;
             if (a.out_blackout) reinterpret_cast<uint64_t*>(a.out_blackout)[w] = m;
+        }
+    } else if (a.layout == BH_LAYOUT_TILES_RGBM14) {
+        if constexpr (FMT == BH_OUT_RGBA16F) {  // bh_render admits this layout for RGBA16F only
+            store_rgbm14(a.out_col, idx, col, zero);
+            if (a.out_blackout) store_rgbm14(a.out_blackout, idx, bo, zero);
         }
     } else {
         store_px<FMT>(a.out_col, idx, col, tab + 256);
@@ -1203,9 +1252,25 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
 // overlaps the others' bulk instead of ending the launch alone.  Only frame 0
 // records the tile costs for the next launch's order (the histogram must count each tile once).
 //
+// BH_DIAG_PHASES (diagnostic builds only, tools/probe_phases.py): a clock-probed wave also adds the shader
+// cycles of its phases to its XCD's accumulator slots 3..7: wave start -> tables staged, -> march start
+// (tile, pixel ray), -> march end, -> pixel written, -> wave end (cost bookkeeping).
+#ifndef BH_DIAG_PHASES
+#define BH_DIAG_PHASES 0
+#endif
+#if BH_DIAG_PHASES
+struct Phases { uint32_t t[6]; };
+#define BH_PHASE(i) (ph.t[i] = (uint32_t)__builtin_amdgcn_s_memtime())
+#define BH_PHASES_ARG , Phases& ph
+#else
+#define BH_PHASE(i) ((void)0)
+#define BH_PHASES_ARG
+#endif
+
 // One dispatch slot, marched by one wave.
 template <uint32_t FMT, uint32_t SF>
-__device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, const float* lut, uint32_t lane) {
+__device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, const float* lut,
+                                           uint32_t lane BH_PHASES_ARG) {
     const uint32_t nf = A.n_frames;
     uint32_t fi = 0, j = slot;
     if (nf > 1u) {
@@ -1239,6 +1304,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     st.n_rk = 0;
     st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
+    BH_PHASE(2);
     if (valid) {
         // the camera outside the unit sphere (1.01 leaves room for any rounding of |ro0|^2 against the
         // step's own r^2 > 1 + 2^-23 at iteration 0) and |s| <= 2^30 on every lane: the step without the
@@ -1251,6 +1317,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
             march_ray<SF>(a, f, st, fate, steps, lane);
         }
     }
+    BH_PHASE(3);
     if (valid) {
         // the frame's output pointers are loaded here, from an opaque copy of the frame index: loaded
         // up front they would hold 10 SGPRs through the march loop, over the 80 that keep 8
@@ -1266,6 +1333,7 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
 #endif
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), col, st.n_rk, fate, steps);
     }
+    BH_PHASE(4);
     if (a.tile_cost) {
         // the next frame's cost and its bucket histogram (a no-return atomic: the wave does not wait);
         // the last bucket is the remainder and is not counted
@@ -1307,8 +1375,13 @@ __device__ __forceinline__ void clock_end(unsigned long long* acc, const ClockSt
 template <uint32_t FMT, uint32_t SF>
 __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs A) {
     __shared__ float lut[lds_tables<FMT>()];
+#if BH_DIAG_PHASES
+    Phases ph;
+#endif
+    BH_PHASE(0);
     load_tables<FMT, 64u * BH_WG_WAVES>(A, lut);
     __syncthreads();
+    BH_PHASE(1);
     const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
     const uint32_t n_slots = A.n_tiles * A.n_frames;
 #if BH_SPW > 1
@@ -1329,8 +1402,20 @@ __global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs 
         const bool probe = A.clk && ((slot + (slot >> 8)) & A.clk_mask) == 0u;
         ClockStart c0{0u, 0u};
         if (probe) c0 = clock_start();
+#if BH_DIAG_PHASES
+        march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u, ph);
+        if (probe) clock_end(A.clk, c0);
+        BH_PHASE(5);
+        if (probe && (threadIdx.x & 63u) == 0u) {
+            const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+            for (int i = 0; i < 5; ++i)
+                __hip_atomic_fetch_add(A.clk + 16u * x + 3u + i, (unsigned long long)(ph.t[i + 1] - ph.t[i]), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+#else
         march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
         if (probe) clock_end(A.clk, c0);
+#endif
     }
 }
 

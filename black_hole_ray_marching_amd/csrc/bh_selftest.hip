@@ -40,6 +40,8 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 //       special values (+-0, axes, diagonals, tiny); ex[0..3] of a mismatch = y, x, got, want
 // op 9: the unit-vector pairs of op 8 (10 of every 16); counts how many the core hands to the fallback
 // op 11: wave_max_u32 (DPP scan) against a serial max, `count` rounds per wave
+// op 12: rcp_from_rsq over EVERY q with bits in [base, base + count) whose Q = RN(RN(q*q) * sqrt_core(q))
+//        passes the division guard, against the IEEE reciprocal 1/Q (ex = q, Q, got, want)
 // op 7: div_core over EVERY pair of significands (n, d) in [1, 2)^2 with d's 23 fraction bits in
 //       [base, base + count / 2^23): all 2^23 numerators per denominator (the full 2^46 square is
 //       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
@@ -142,6 +144,16 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
                 if (__float_as_uint(got) != __float_as_uint(want) && !(got != got && want != want))
                     record(cnt, ex, __float_as_uint(y), __float_as_uint(x), __float_as_uint(got), __float_as_uint(want));
             }
+        } else if (op == 12) {
+            const uint32_t bits = (uint32_t)(base + i);
+            const float q = __uint_as_float(bits);
+            if (crm::sqrt_bad(q)) continue;
+            const crm::SqrtY sy = crm::sqrt_core_y(q);
+            const float Q = (q * q) * sy.s;
+            if (crm::div_d_bad(Q)) continue;
+            const float got = crm::rcp_from_rsq(Q, sy.y).r, want = 1.0f / Q;
+            if (__float_as_uint(got) != __float_as_uint(want))
+                record(cnt, ex, bits, __float_as_uint(Q), __float_as_uint(got), __float_as_uint(want));
         } else if (op == 2 || op == 3) {
             const uint64_t h1 = mix64(base * 0x100000001B3ull + i), h2 = mix64(h1 ^ 0xD1B54A32D192ED03ull);
             float d = fabsf(rnd_float(h1, -40, 59));
@@ -167,7 +179,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 11 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 12 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;

@@ -33,12 +33,16 @@ template <> __device__ __forceinline__ uint4 zero_px<16>() { return make_uint4(0
 template <> __device__ __forceinline__ uint2 zero_px<8>() { return make_uint2(0u, 0x3C00u << 16); }
 template <> __device__ __forceinline__ uint32_t zero_px<4>() { return 0xFF000000u; }
 
-template <uint32_t BPP, bool PLANAR, bool MASK = false>
+// P14 (with BPP 8, PLANAR, MASK): BH_LAYOUT_TILES_RGBM14, the 14-bit fp16 channels (86 words per tile:
+// r | g << 14 | (b & 0xF) << 28, the bytes (b >> 4) & 0xFF, b's bit-12 and bit-13 words, the mask word).
+template <uint32_t BPP, bool PLANAR, bool MASK = false, bool P14 = false>
 __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __restrict__ packed, void* __restrict__ out,
                                                            void* __restrict__ out_bo, UnpackGrid u) {
     using P = typename PixelT<BPP>::T;
     static_assert(PLANAR || !MASK, "the mask travels with the planar layout only");
-    constexpr uint32_t TW = PLANAR ? 12u * BPP + (MASK ? 2u : 0u) : 16u * BPP;  // 32-bit words per packed tile
+    static_assert(!P14 || (BPP == 8 && PLANAR && MASK), "RGBM14 is an RGBA16F mask layout");
+    // 32-bit words per packed tile
+    constexpr uint32_t TW = P14 ? 86u : PLANAR ? 12u * BPP + (MASK ? 2u : 0u) : 16u * BPP;
     static_assert(TW % 2u == 0u, "packed tiles are whole 8-byte words");
     constexpr uint32_t TD = TW / 2u;                                // 8-byte words per packed tile
     constexpr uint32_t PER = (UNPACK_SPAN * TD + 255u) / 256u;      // staged words per thread
@@ -87,7 +91,12 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
         if (py >= u.height) break;
         const uint32_t e = (x & 7u) + 8u * r;  // pixel inside the tile
         P v;
-        if constexpr (!PLANAR) {
+        if constexpr (P14) {
+            const uint32_t w = tile[e], hb = (uint32_t)reinterpret_cast<const uint8_t*>(tile + 64)[e];
+            const uint32_t b12 = (tile[80u + (e >> 5)] >> (e & 31u)) & 1u, b13 = (tile[82u + (e >> 5)] >> (e & 31u)) & 1u;
+            const uint32_t b = (w >> 28) | (hb << 4) | (b12 << 12) | (b13 << 13);
+            v = make_uint2((w & 0x3FFFu) | (((w >> 14) & 0x3FFFu) << 16), b | (0x3C00u << 16));
+        } else if constexpr (!PLANAR) {
             v = reinterpret_cast<const P*>(tile)[e];
         } else if constexpr (BPP == 16) {  // RGBA32F
             const float* c = reinterpret_cast<const float*>(tile);
@@ -103,7 +112,7 @@ __global__ void __launch_bounds__(256) tiles_unpack_kernel(const uint32_t* __res
         reinterpret_cast<P*>(out)[(size_t)py * u.width + px] = v;
         if constexpr (MASK) {
             if (out_bo) {
-                const uint32_t mw = tile[12u * BPP + (e >> 5)];  // the mask word's half holding bit e
+                const uint32_t mw = tile[(P14 ? 84u : 12u * BPP) + (e >> 5)];  // the mask word's half holding bit e
                 reinterpret_cast<P*>(out_bo)[(size_t)py * u.width + px] = ((mw >> (e & 31u)) & 1u) ? zero_px<BPP>() : v;
             }
         }
@@ -218,12 +227,19 @@ static void unpack_launch_shape(uint32_t width, uint32_t height, uint32_t shard_
 template <bool PLANAR, bool MASK>
 static int unpack_launch(const void* packed, void* out, void* out_bo, uint32_t width, uint32_t height,
                          uint32_t shard_count, uint64_t stride_tiles, uint32_t bpp, uint32_t rows_in_flight,
-                         hipStream_t s, const uint32_t* tile_loc = nullptr) {
+                         hipStream_t s, const uint32_t* tile_loc = nullptr, bool p14 = false) {
     bh::UnpackGrid u;
     dim3 grid, block(256);
     unpack_launch_shape(width, height, shard_count, stride_tiles, rows_in_flight, &u, &grid);
     u.tile_loc = tile_loc;
     const uint32_t* p = static_cast<const uint32_t*>(packed);
+    if constexpr (PLANAR && MASK) {
+        if (p14) {
+            if (bpp != 8u) return (int)hipErrorInvalidValue;
+            hipLaunchKernelGGL((bh::tiles_unpack_kernel<8, true, true, true>), grid, block, 0, s, p, out, out_bo, u);
+            return (int)hipGetLastError();
+        }
+    }
     switch (bpp) {
         case 16: hipLaunchKernelGGL((bh::tiles_unpack_kernel<16, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
         case 8: hipLaunchKernelGGL((bh::tiles_unpack_kernel<8, PLANAR, MASK>), grid, block, 0, s, p, out, out_bo, u); break;
@@ -257,6 +273,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_tiles_unpack_rgbm
                                                                                const uint32_t* tile_loc,
                                                                                uint32_t format, uint32_t rows_in_flight,
                                                                                hipStream_t s) {
-    return unpack_launch<true, true>(packed, out, out_bo, width, height, shard_count, stride_tiles, format_bpp(format),
-                                     rows_in_flight, s, tile_loc);
+    return unpack_launch<true, true>(packed, out, out_bo, width, height, shard_count, stride_tiles,
+                                     format_bpp(format & 0xFFu), rows_in_flight, s, tile_loc,
+                                     (format & BH_UNPACK_RGBM14) != 0u);
 }

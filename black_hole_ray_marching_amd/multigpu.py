@@ -178,6 +178,65 @@ def unpack_rgbm_numpy(packed: np.ndarray, width: int, height: int, S: int, strid
     return col, bo
 
 
+RGBM14_TILE_BYTES = 344  # BH_LAYOUT_TILES_RGBM14 (include/bh_render.h): RGBA16F in 14-bit channels
+
+
+def pack_rgbm14_numpy(col: np.ndarray, zero: np.ndarray, k: int, S: int, stride: int, weights=None) -> np.ndarray:
+    """Host mirror of the march kernel's BH_LAYOUT_TILES_RGBM14 store (store_rgbm14) for shard k: `col`
+    (H, W, 4) float16 whose RGB are in [0, 1] (fp16 bits < 0x4000), `zero` (H, W) bool as pack_rgbm_numpy.
+    Per tile: 64 words r | g << 14 | (b & 0xF) << 28, 64 bytes (b >> 4) & 0xFF, b's bit-12 and bit-13
+    ballot words, the mask word.  Returns (stride, 344) uint8; pixels outside the frame are 0."""
+    H, W, _ = col.shape
+    bits = col.view(np.uint16).astype(np.uint32)
+    if (bits[..., :3] >= 0x4000).any():
+        raise ValueError("RGBM14 carries fp16 channels in [0, 1] only")
+    out = np.zeros((stride, RGBM14_TILE_BYTES), np.uint8)
+    lane = np.arange(64)
+    for t, (tx, ty) in enumerate(shard_tiles(W, H, k, S, weights)):
+        px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
+        ok = (px < W) & (py < H)
+        r, g, b = (np.zeros(64, np.uint32) for _ in range(3))
+        r[ok], g[ok], b[ok] = bits[py[ok], px[ok], 0], bits[py[ok], px[ok], 1], bits[py[ok], px[ok], 2]
+        zt = np.zeros(64, bool)
+        zt[ok] = zero[py[ok], px[ok]]
+        words = (r | (g << 14) | ((b & 0xF) << 28)).astype(np.uint32)
+        hi = ((b >> 4) & 0xFF).astype(np.uint8)
+        ballot = [sum(1 << int(i) for i in lane[m]) for m in (((b >> 12) & 1) == 1, ((b >> 13) & 1) == 1, zt)]
+        out[t, :256] = words.view(np.uint8)
+        out[t, 256:320] = hi
+        out[t, 320:] = np.array(ballot, np.uint64).view(np.uint8)
+    return out
+
+
+def unpack_rgbm14_numpy(packed: np.ndarray, width: int, height: int, S: int, stride: int, weights=None):
+    """Host mirror of bh_tiles_unpack_rgbm with BH_UNPACK_RGBM14: gathered (S * stride, 344) uint8 ->
+    (col, blackout) float16 (height, width, 4), alpha 1.0 restored, blackout = col with the masked RGB 0."""
+    col = np.zeros((height, width, 4), np.float16)
+    bo = np.zeros((height, width, 4), np.float16)
+    lane = np.arange(64)
+    one = np.float16(1.0)
+    for k in range(S):
+        for t, (tx, ty) in enumerate(shard_tiles(width, height, k, S, weights)):
+            tile = packed[k * stride + t]
+            w = tile[:256].view(np.uint32).astype(np.uint64)
+            hi = tile[256:320].astype(np.uint64)
+            m12, m13, mz = (tile[320 + 8 * j:328 + 8 * j].view(np.uint64)[0] for j in range(3))
+            sh = lane.astype(np.uint64)
+            b = (w >> np.uint64(28)) | (hi << np.uint64(4)) | (((m12 >> sh) & np.uint64(1)) << np.uint64(12)) \
+                | (((m13 >> sh) & np.uint64(1)) << np.uint64(13))
+            rgb = np.stack([w & np.uint64(0x3FFF), (w >> np.uint64(14)) & np.uint64(0x3FFF), b], -1)
+            rgb = rgb.astype(np.uint16).view(np.float16)
+            zero = ((mz >> sh) & np.uint64(1)).astype(bool)
+            px, py = tx * TILE + (lane & 7), ty * TILE + (lane >> 3)
+            ok = (px < width) & (py < height)
+            col[py[ok], px[ok], :3] = rgb[ok]
+            col[py[ok], px[ok], 3] = one
+            keep = ok & ~zero
+            bo[py[keep], px[keep], :3] = rgb[keep]
+            bo[py[ok], px[ok], 3] = one
+    return col, bo
+
+
 def gather_packed(packed, rank: int, world: int, gathered=None, group=None):
     """Gather every rank's packed tile buffer (same shape on all ranks) to rank 0.
 

@@ -19,7 +19,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import _abi
-from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
+from ._abi import (BH_LAYOUT_ROWMAJOR, BH_LAYOUT_TILES, BH_LAYOUT_TILES_RGB, BH_LAYOUT_TILES_RGBM, BH_LAYOUT_TILES_RGBM14, BH_UNPACK_RGBM14, BH_MATH_EXACT, BH_MATH_FAST, BH_OUT_RGBA16F,
                    BH_OUT_RGBA32F, BH_OUT_BGRA8_SRGB, BH_SCENE_DEFAULT, BYTES_PER_PIXEL, BhError, check, load)
 
 MAX_ITERATIONS = 1000  # src/black_hole_maybe.wgsl:85
@@ -313,7 +313,7 @@ class Scene:
             else:
                 nt = shard_tile_count(d.width, d.height, shard_index, shard_count)
             px = nt * 64
-            col_bytes = nt * tile_bytes(layout, fmt) if bpp and layout <= BH_LAYOUT_TILES_RGBM else px * bpp
+            col_bytes = nt * tile_bytes(layout, fmt) if bpp and layout <= BH_LAYOUT_TILES_RGBM14 else px * bpp
         _check_size(output, col_bytes, "output")
         _check_size(blackout_output, col_bytes, "blackout_output")
         _check_size(dbg_n_rk, px * 2, "dbg_n_rk")
@@ -458,13 +458,22 @@ def tiles_unpack_rgb(packed, out, width: int, height: int, shard_count: int, sha
                                          fmt, _stream_handle(stream)), "bh_tiles_unpack_rgb")
 
 
+def _rgbm_format(fmt: int):
+    """(bytes per pixel of the unpacked targets, packed layout) of an RGBM unpack format (0 bytes if invalid)."""
+    lay = BH_LAYOUT_TILES_RGBM14 if fmt & BH_UNPACK_RGBM14 else BH_LAYOUT_TILES_RGBM
+    base = fmt & 0xFF
+    ok = fmt & ~(0xFF | BH_UNPACK_RGBM14) == 0 and (lay == BH_LAYOUT_TILES_RGBM or base == BH_OUT_RGBA16F)
+    return (_abi.BYTES_PER_PIXEL.get(base, 0) if ok else 0), lay
+
+
 def tiles_unpack_rgbm(packed, out_col, out_blackout, width: int, height: int, shard_count: int,
                       shard_stride_tiles: int, fmt: int, stream=None, rows_in_flight: int = 0) -> None:
     """bh_tiles_unpack_rgbm: gathered BH_LAYOUT_TILES_RGBM shards -> both Scene::render targets, row-major
-    (`out_blackout` None == Option::None)."""
-    bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+    (`out_blackout` None == Option::None).  fmt = BH_OUT_RGBA16F | BH_UNPACK_RGBM14: BH_LAYOUT_TILES_RGBM14
+    shards."""
+    bpp, lay = _rgbm_format(fmt)
     _check_unpack(packed, [(out_col, "out_col"), (out_blackout, "out_blackout")], width, height, shard_count,
-                  shard_stride_tiles, tile_bytes(BH_LAYOUT_TILES_RGBM, fmt) if bpp else 0, bpp, "tiles_unpack_rgbm")
+                  shard_stride_tiles, tile_bytes(lay, fmt & 0xFF) if bpp else 0, bpp, "tiles_unpack_rgbm")
     check(load().bh_tiles_unpack_rgbm(_ptr(packed), _ptr(out_col), _ptr(out_blackout), width, height, shard_count,
                                       shard_stride_tiles, fmt, rows_in_flight, _stream_handle(stream)),
           "bh_tiles_unpack_rgbm")
@@ -517,10 +526,11 @@ def partition_map(width: int, height: int, weights):
 
 def tiles_unpack_rgbm_partition(packed, out_col, out_blackout, partition: "Partition", shard_stride_tiles: int,
                                 fmt: int, stream=None, rows_in_flight: int = 0) -> None:
-    """bh_tiles_unpack_rgbm_partition: gathered BH_LAYOUT_TILES_RGBM shards of `partition` -> both targets."""
-    bpp = _abi.BYTES_PER_PIXEL.get(fmt, 0)
+    """bh_tiles_unpack_rgbm_partition: gathered BH_LAYOUT_TILES_RGBM shards of `partition` -> both targets
+    (fmt with BH_UNPACK_RGBM14: BH_LAYOUT_TILES_RGBM14 shards)."""
+    bpp, lay = _rgbm_format(fmt)
     S = partition.shard_count
-    _check_size(packed, ((S - 1) * shard_stride_tiles + partition.counts[-1]) * (tile_bytes(BH_LAYOUT_TILES_RGBM, fmt)
+    _check_size(packed, ((S - 1) * shard_stride_tiles + partition.counts[-1]) * (tile_bytes(lay, fmt & 0xFF)
                                                                                 if bpp else 0), "packed",
                 "tiles_unpack_rgbm_partition")
     for t, name in ((out_col, "out_col"), (out_blackout, "out_blackout")):
@@ -531,7 +541,8 @@ def tiles_unpack_rgbm_partition(packed, out_col, out_blackout, partition: "Parti
 
 
 __all__ = ["Camera", "Partition", "partition_map", "tiles_unpack_rgbm_partition", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
-           "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM",
+           "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM", "BH_LAYOUT_TILES_RGBM14",
+           "BH_UNPACK_RGBM14",
            "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_LAYOUT_TILES_RGB", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

@@ -139,7 +139,7 @@ typedef enum {
                                src/black_hole_maybe.wgsl:369): each tile is three planes of 64
                                channel values in the format's memory order less alpha (R, G, B for
                                RGBA16F/RGBA32F; B, G, R for BGRA8), 3/4 of the bytes to gather */
-    BH_LAYOUT_TILES_RGBM = 3 /* BH_LAYOUT_TILES_RGB plus, after each tile's three planes, one 64-bit
+    BH_LAYOUT_TILES_RGBM = 3, /* BH_LAYOUT_TILES_RGB plus, after each tile's three planes, one 64-bit
                                little-endian word whose bit i is set when pixel i of the tile has
                                blackout_col == 0, i.e. dot(col, col) < 1 in fp32 (src/black_hole_maybe.wgsl:365-368):
                                the multi-GPU transport.  blackout_col is a per-pixel function of the
@@ -147,7 +147,18 @@ typedef enum {
                                travels with them (0.125 B/pixel) and the gathered col alone restores both
                                targets bit for bit (bh_tiles_unpack_rgbm).  Tile bytes: 776 (RGBA32F),
                                392 (RGBA16F), 200 (BGRA8).  Schedules TILE and PAIR only. */
+    BH_LAYOUT_TILES_RGBM14 = 4 /* BH_LAYOUT_TILES_RGBM for RGBA16F in 344 B per tile (5.375 B/pixel instead
+                               of 6.125): every colour channel is an fp16 in [0, 1] -- sky samples are
+                               bilinear mixes of decoded texels in [0, 1] (and g, b their c * sqrt(c)),
+                               surfaces 1, blackout 0 -- so its top two bits are 0 and 14 bits carry it.
+                               Per tile: 64 words r | g << 14 | (b & 0xF) << 28, 64 bytes (b >> 4) & 0xFF,
+                               two 64-bit words holding bit 12 / bit 13 of b for pixel i at bit i, then the
+                               blackout mask word.  RGBA16F, schedules TILE and PAIR only; unpack with
+                               bh_tiles_unpack_rgbm(_partition) and format BH_OUT_RGBA16F | BH_UNPACK_RGBM14. */
 } bh_layout;
+/* format flag of bh_tiles_unpack_rgbm / bh_tiles_unpack_rgbm_partition: the shards are
+ * BH_LAYOUT_TILES_RGBM14 (with BH_OUT_RGBA16F) */
+#define BH_UNPACK_RGBM14 0x100u
 
 /* Work schedule of the march kernel (same results, different speed). */
 typedef enum {
@@ -358,7 +369,8 @@ int bh_srgb_encode_table(float* out257);
  * the number of those pairs the core hands to the fallback; op 10: the bloom chain's code-table form of
  * the sRGB encoder against op 4's over bit patterns [base, base+count); op 11: the march kernel's
  * wave-wide max of the tile costs (DPP scan) against a serial max, `count` random rounds per wave
- * seeded by base).  *out_mismatches = number of differing results;
+ * seeded by base; op 12: the march step's reciprocal of rd_derivative's denominator seeded from the
+ * square-root core's v_rsq, over q bit patterns [base, base+count), against the IEEE 1/Q).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

@@ -221,6 +221,37 @@ def test_tile_bytes_of_every_layout():
         bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, 9)
 
 
+def test_rgbm14_tile_bytes_and_mirror():
+    """BH_LAYOUT_TILES_RGBM14: 344 B per RGBA16F tile (86 words, the mask word 8-byte aligned), other
+    formats refused; the host mirrors of its store and unpack restore both targets of any RGBA16F frame
+    whose channels are in [0, 1] exactly as the RGBM mirrors do."""
+    assert bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM14, bh.BH_OUT_RGBA16F) == 344 == multigpu.RGBM14_TILE_BYTES
+    for fmt in (bh.BH_OUT_RGBA32F, bh.BH_OUT_BGRA8_SRGB):
+        with pytest.raises(bh.BhError):
+            bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM14, fmt)
+    rng = np.random.default_rng(5)
+    H, W = 37, 53
+    c = rng.random((H, W, 4)).astype(np.float32)
+    c[rng.random((H, W)) < 0.1] = 0.0
+    c[rng.random((H, W)) < 0.05, :3] = 1.0
+    c[0, 0, :3] = [6.1e-5, 5.96e-8, 0.99951]  # smallest normal, smallest subnormal, largest below 1
+    c[..., 3] = 1.0
+    c16 = c.astype(np.float16)
+    zero = ((c[..., 0] * c[..., 0] + c[..., 1] * c[..., 1]) + c[..., 2] * c[..., 2]) < 1.0
+    for S, weights in ((1, None), (3, None), (3, [2, 5, 3])):
+        stride = multigpu.packed_stride(W, H, S, weights)
+        p14 = np.concatenate([multigpu.pack_rgbm14_numpy(c16, zero, k, S, stride, weights) for k in range(S)])
+        p16 = np.concatenate([multigpu.pack_rgbm_numpy(c16, zero, k, S, stride, weights) for k in range(S)])
+        c1, b1 = multigpu.unpack_rgbm14_numpy(p14, W, H, S, stride, weights)
+        c2, b2 = multigpu.unpack_rgbm_numpy(p16, W, H, S, stride, np.float16, 1.0, weights)
+        assert np.array_equal(c1.view(np.uint16), c2.view(np.uint16))
+        assert np.array_equal(b1.view(np.uint16), b2.view(np.uint16))
+    with pytest.raises(ValueError):  # a channel above 1 does not fit 14 bits
+        bad = c16.copy()
+        bad[1, 1, 0] = 2.0
+        multigpu.pack_rgbm14_numpy(bad, zero, 0, 1, multigpu.packed_stride(W, H, 1))
+
+
 @pytest.mark.parametrize("S", [1, 2, 3, 8])
 @pytest.mark.parametrize("dtype,alpha", [(np.float16, 1.0), (np.float32, 1.0), (np.uint8, 255)])
 def test_rgbm_pack_unpack_mirror_restores_both_targets(S, dtype, alpha):

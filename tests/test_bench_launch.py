@@ -25,13 +25,14 @@ def _bench(*args, env=None, timeout=240):
     return r.returncode, lines, r.stderr
 
 
+@pytest.mark.parametrize("transport", ["rgbm14", "rgbm"])
 @pytest.mark.parametrize("n", [2, 3])
-def test_self_launch_runs_n_ranks_and_verifies_the_gather(n):
-    rc, lines, err = _bench("--gpus", str(n), "--plumbing", "--steps", "3")
+def test_self_launch_runs_n_ranks_and_verifies_the_gather(n, transport):
+    rc, lines, err = _bench("--gpus", str(n), "--plumbing", "--steps", "3", "--transport", transport)
     assert rc == 0, err[-2000:]
     assert len(lines) == 1, lines            # rank 0 alone prints the line
     d = lines[0]
-    assert d["n_gpus"] == n and d["world_size"] == n and d["backend"] == "gloo"
+    assert d["n_gpus"] == n and d["world_size"] == n and d["backend"] == "gloo" and d["transport"] == transport
     assert d["frames_checked"] == 3 and d["gather_verified_bit_exact"] is True
 
 

@@ -141,6 +141,85 @@ def test_rgbm_shards_unpack_both_targets(torch_cuda, sky_full, S, fmt, schedule)
     scene.close()
 
 
+def _shards_rgbm14(torch, scene, W, H, S, schedule, partition=None):
+    """Every shard rendered in BH_LAYOUT_TILES_RGBM14 (RGBA16F col only), concatenated as the gather
+    produces them."""
+    tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM14, bh.BH_OUT_RGBA16F)
+    counts = partition.counts if partition else [bh.shard_tile_count(W, H, k, S) for k in range(S)]
+    stride = max(counts)
+    packed = torch.zeros((S * stride, tb), dtype=torch.uint8, device="cuda")
+    for k in range(S):
+        kw = dict(partition=partition) if partition else {}
+        scene.render(packed[k * stride:k * stride + counts[k]], None, fmt=bh.BH_OUT_RGBA16F,
+                     layout=bh.BH_LAYOUT_TILES_RGBM14, shard_index=k, shard_count=S, width=W, height=H,
+                     schedule=schedule, **kw)
+    return packed, stride
+
+
+@pytest.mark.parametrize("schedule", [bh.BH_SCHED_TILE, bh.BH_SCHED_PAIR])
+@pytest.mark.parametrize("S", [1, 2, 3, 8])
+@pytest.mark.parametrize("cam", ["A", "D"])
+def test_rgbm14_shards_unpack_both_targets(torch_cuda, sky_full, S, schedule, cam):
+    """The 14-bit transport (BH_LAYOUT_TILES_RGBM14, 5.375 B/pixel): every RGBA16F channel of the march is
+    an fp16 in [0, 1], so rank 0's unpack with BH_UNPACK_RGBM14 restores col and blackout_col equal bit
+    for bit to a single-GPU two-target render (frames with sky, disc, markers, shadow and partial
+    tiles)."""
+    torch = torch_cuda
+    W, H = 204, 100  # partial edge tiles
+    scene = bh.Scene(W, H, sky=sky_full, max_iters=512, math=bh.BH_MATH_EXACT)
+    scene.camera_uniform = camera_uniform(cam, W, H)
+    ref_c = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
+    ref_b = torch.zeros_like(ref_c)
+    scene.render(ref_c, ref_b, fmt=bh.BH_OUT_RGBA16F)
+    packed, stride = _shards_rgbm14(torch, scene, W, H, S, schedule)
+    for rows in (0, 3):
+        out_c = torch.full((H, W, 4), 7, dtype=torch.float16, device="cuda")
+        out_b = torch.full_like(out_c, 7)
+        bh.tiles_unpack_rgbm(packed, out_c, out_b, W, H, S, stride, bh.BH_OUT_RGBA16F | bh.BH_UNPACK_RGBM14,
+                             rows_in_flight=rows)
+        torch.cuda.synchronize()
+        assert torch.equal(out_c.view(torch.uint8), ref_c.view(torch.uint8)), f"col, rows={rows}"
+        assert torch.equal(out_b.view(torch.uint8), ref_b.view(torch.uint8)), f"blackout, rows={rows}"
+    # the host mirror of the unpack reads the same bytes
+    from black_hole_ray_marching_amd import multigpu
+    c, b = multigpu.unpack_rgbm14_numpy(packed.cpu().numpy(), W, H, S, stride)
+    assert np.array_equal(c.view(np.uint16), ref_c.cpu().numpy().view(np.uint16))
+    assert np.array_equal(b.view(np.uint16), ref_b.cpu().numpy().view(np.uint16))
+    scene.close()
+
+
+@pytest.mark.parametrize("weights", [[3, 4], [16, 20, 20, 20, 20, 20, 20, 20], [0, 5, 7]])
+def test_rgbm14_partition_shards_unpack_both_targets(torch_cuda, sky_full, weights):
+    """RGBM14 shards of weighted partitions (rank 0 lighter, a rank with weight 0) unpack with
+    bh_tiles_unpack_rgbm_partition to both targets of a single-GPU render, bit for bit."""
+    torch = torch_cuda
+    W, H = 256, 128
+    scene = bh.Scene(W, H, sky=sky_full, max_iters=512, math=bh.BH_MATH_EXACT)
+    ref_c = torch.zeros((H, W, 4), dtype=torch.float16, device="cuda")
+    ref_b = torch.zeros_like(ref_c)
+    scene.render(ref_c, ref_b, fmt=bh.BH_OUT_RGBA16F)
+    part = bh.Partition(W, H, weights)
+    packed, stride = _shards_rgbm14(torch, scene, W, H, len(weights), bh.BH_SCHED_TILE, part)
+    out_c = torch.zeros_like(ref_c)
+    out_b = torch.zeros_like(ref_c)
+    bh.tiles_unpack_rgbm_partition(packed, out_c, out_b, part, stride, bh.BH_OUT_RGBA16F | bh.BH_UNPACK_RGBM14)
+    torch.cuda.synchronize()
+    assert torch.equal(out_c.view(torch.uint8), ref_c.view(torch.uint8))
+    assert torch.equal(out_b.view(torch.uint8), ref_b.view(torch.uint8))
+    part.close()
+    scene.close()
+
+
+def test_rgbm14_needs_rgba16f(torch_cuda, sky_small):
+    torch = torch_cuda
+    scene = bh.Scene(16, 16, sky=sky_small)
+    buf = torch.zeros((64, 392), dtype=torch.uint8, device="cuda")
+    for fmt in (bh.BH_OUT_RGBA32F, bh.BH_OUT_BGRA8_SRGB):
+        with pytest.raises(bh.BhError):
+            scene.render(buf, None, fmt=fmt, layout=bh.BH_LAYOUT_TILES_RGBM14, shard_index=0, shard_count=2)
+    scene.close()
+
+
 def test_rgbm_partial_tiles_and_mask_word(torch_cuda, sky_small):
     """Partial edge tiles (100 x 52): the mask bits of pixels outside the frame are clear, and each
     tile's mask word equals the blackout decision of the fp32 render (dot(col, col) < 1)."""

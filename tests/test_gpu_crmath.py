@@ -54,6 +54,16 @@ def test_div_core_significand_blocks(lib, d0):
     assert m == 0, ex
 
 
+def test_rcp_from_rsq_exhaustive(lib):
+    """The march step's reciprocal of rd_derivative's denominator Q = (q*q)*sqrt(q), seeded from the square
+    root core's own v_rsq(q) (y^5, one refinement) instead of a v_rcp of Q: equal to the IEEE 1/Q for every
+    q whose Q passes the division guard [2^-40, 2^60] -- every such q lies in [2^-17, 2^25) -- so every
+    quotient of the step is the one the v_rcp form computed."""
+    lo, hi = 0x37000000, 0x4C000000  # bits of 2^-17 and 2^25
+    m, ex = run(lib, 12, lo, hi - lo)
+    assert m == 0, ex
+
+
 def test_div_core_near_exact_quotients(lib):
     m, ex = run(lib, 3, 777, 1 << 30)
     assert m == 0, ex
