@@ -519,49 +519,47 @@ __device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, co
     q.a = (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
     return q;
 }
-template <int FP, bool A1>
-__device__ __forceinline__ F4 lerp_sep(const float4* T, int32_t o, const SepEntry& c, const SepEntry& r) {
-    const float4 t00 = T[o], t10 = T[o + 1];
-    const float4 t01 = T[o + FP], t11 = T[o + FP + 1];
-    const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;    // sample()'s operations in its order
-    F4 q;
-    q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
-    q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
-    q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
-    // an opaque block's texels all have alpha 1.0, and then every tap's alpha is exactly 1.0:
-    // RN(ia + fa) == 1 for fa in [0, 1) and ia = RN(1 - fa) (|ia + fa - 1| <= 2^-25), likewise along y
-    q.a = A1 ? 1.0f : (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
-    return q;
-}
 
-// FP: the staged footprint's side; FS: the tile's row stride in float4, a multiple of 16 (see FS_YQ: in a
-// same-size pass lane l reads column ~l & 15 of row ~l >> 4)
-template <int FP, uint32_t EPI, int FS = (FP + 15) / 16 * 16>
-__global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, const SepEntry* __restrict__ sep, Tex out, CTex own0,
-                                           CTex own1, const uint2* __restrict__ same, Tex aux) {
+// FP: the staged footprint's side.  RAW: the tile holds the BGRA8 words (4 B per texel instead of 16, for
+// the wide footprint of the final pass: 44 x 48 words = 8.4 KiB instead of 33 KiB), decoded when a tap
+// reads them.  FS: the tile's row stride, a multiple of 16 float4 for the decoded tile (ds_read_b128 lane
+// groups take two rows: see FS_YQ; in a same-size pass lane l reads column ~l & 15 of row ~l >> 4) and 16
+// mod 32 words for the raw one (ds_read_b32: lanes 0-15 row r, 16-31 row r + 1 land on the other banks).
+template <int FP, bool RAW>
+constexpr int sep_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
+template <int FP, uint32_t EPI, bool RAW = false, int FS = sep_stride<FP, RAW>()>
+__global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, const SepEntry* __restrict__ sep,
+                                           Tex out, CTex own0, CTex own1, const uint2* __restrict__ same, Tex aux) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP * FS];
+    __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS];
     __shared__ SepEntry colp[8][16], rowp[8][16];
     const uint32_t bx = xcd_block().x * 16u, by = xcd_block().y * 16u;
     const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t tx = threadIdx.x & 15u, ty = threadIdx.x >> 4;
     const uint32_t x = bx + tx, y = by + ty;
     const bool in = x < ow && y < oh;
-    // the block's footprint: floors are monotone in the column (row), so the taps' floors at the first
-    // and last column bound it (scalar loads: block-uniform addresses)
+    // the block's footprint from the sampler's own arithmetic (no memory round trip before the staging
+    // loads): every rounding step is monotone in the texcoord, so the extreme taps (du(0) and du(4), dv(6)
+    // and dv(2)) of the first and last column (row) bound every tap's floor -- exactly the plan's extremes
+    const crm::Rcp Rw = crm::rcp_refined((float)ow), Rh = crm::rcp_refined((float)oh);
+    const Taps k(rx, ry);
     const uint32_t xl = min(bx + 15u, ow - 1u), yl = min(by + 15u, oh - 1u);
-    int32_t lo_x = INT_MAX, hi_x = INT_MIN, lo_y = INT_MAX, hi_y = INT_MIN;
+    const int32_t lo_x = (int32_t)floorf(sample_coord(texcoord(bx, Rw) + k.du_min(), a.w));
+    const int32_t hi_x = (int32_t)floorf(sample_coord(texcoord(xl, Rw) + k.du_max(), a.w));
+    const int32_t lo_y = (int32_t)floorf(sample_coord(texcoord(by, Rh) + k.dv_min(), a.h));
+    const int32_t hi_y = (int32_t)floorf(sample_coord(texcoord(yl, Rh) + k.dv_max(), a.h));
+    const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // floor .. floor + 1
+    // the host sizes FP for the launch (bh_bloom_sep_plan's extent), so the min never cuts
+    constexpr int R = (FP * FP + 255) / 256;
+    uint32_t raw[R];
+    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        lo_x = min(lo_x, sep[i * ow + bx].f);
-        hi_x = max(hi_x, sep[i * ow + xl].f);
-        lo_y = min(lo_y, sep[8u * ow + i * oh + by].f);
-        hi_y = max(hi_y, sep[8u * ow + i * oh + yl].f);
+    for (int r = 0; r < R; ++r) {
+        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
+        raw[r] = 0xFF000000u;
+        if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
     }
-    const int32_t nx = hi_x - lo_x + 2, ny = hi_y - lo_y + 2;  // floor .. floor + 1
-    // the host sizes FP for the launch (bh_bloom_sep_plan's extent); a larger block footprint never
-    // occurs, and would read the clamped tile edge rather than outside it
-    // this block's plan entries, as tile offsets: thread t < 128 column entry (t >> 4, t & 15), else row
+    // this block's plan entries as tile offsets: thread t < 128 column entry (t >> 4, t & 15), else row
     {
         const uint32_t i = (threadIdx.x >> 4) & 7u, j = threadIdx.x & 15u;
         if (threadIdx.x < 128u) {
@@ -574,7 +572,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, const SepEntry* __
             rowp[i][j] = e;
         }
     }
-    // own texels of the epilogue, loaded before the footprint and the tables, used last
+    // own texels of the epilogue, loaded before the tables, used last
     const uint32_t pix = (in ? y : 0u) * ow + (in ? x : 0u);
     uint32_t o0 = 0xFF000000u, o1 = 0xFF000000u;
     bool exact = false;
@@ -583,24 +581,18 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, const SepEntry* __
         if constexpr (EPI == EPI_FINAL) o1 = own1.px[pix];
         exact = in && same[in ? x : 0u].y == 0u && same[ow + (in ? y : 0u)].y == 0u;
     }
-    constexpr int R = (FP * FP + 255) / 256;
-    uint32_t raw[R];
-    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
-    const int32_t cx = min(nx, FP), cy = min(ny, FP);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
-        raw[r] = 0xFF000000u;
-        if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
-    }
     load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
     uint32_t m = min(o0, o1);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
         if (ly < cy) {
-            const F4 d = dec(L, raw[r]);
-            tile[ly * FS + lx] = make_float4(d.r, d.g, d.b, d.a);
+            if constexpr (RAW) {
+                tile[ly * FS + lx] = raw[r];
+            } else {
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FS + lx] = make_float4(d.r, d.g, d.b, d.a);
+            }
         }
         m = min(m, raw[r]);
     }
@@ -609,15 +601,41 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, const SepEntry* __
     if (!in) return;
     auto run = [&](auto A1c) {
         constexpr bool A1 = decltype(A1c)::value;
+        auto texel = [&](int32_t o) {
+            if constexpr (RAW) {
+                const F4 d = dec<A1>(L, tile[o]);
+                return make_float4(d.r, d.g, d.b, d.a);
+            } else {
+                return tile[o];
+            }
+        };
         F4 s{0.0f, 0.0f, 0.0f, 0.0f};
+        SepEntry c = colp[0][tx], r = rowp[0][ty];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            // one tap at a time (the sched barrier and the empty asm on the sums keep the compiler from
-            // hoisting later taps' reads or sinking this tap's work)
-            const SepEntry c = colp[i][tx], r = rowp[i][ty];
-            acc(s, lerp_sep<FS, A1>(tile, c.f + r.f, c, r), i);
+            // the next tap's plan entries are read while this tap computes; one tap at a time otherwise
+            // (the sched barrier and the empty asm on the sums keep the compiler from hoisting later taps'
+            // texel reads or sinking this tap's work: all 8 together take ~160 VGPRs)
+            SepEntry cn = c, rn = r;
+            if (i < 7) {
+                cn = colp[i + 1][tx];
+                rn = rowp[i + 1][ty];
+            }
+            const int32_t o = c.f + r.f;
+            const float4 t00 = texel(o), t10 = texel(o + 1), t01 = texel(o + FS), t11 = texel(o + FS + 1);
+            const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;  // sample()'s operations in its order
+            F4 q;
+            q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+            q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+            q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+            // an opaque block's texels all have alpha 1.0, and then every tap's alpha is exactly 1.0:
+            // RN(ia + fa) == 1 for fa in [0, 1) and ia = RN(1 - fa) (|ia + fa - 1| <= 2^-25), likewise along y
+            q.a = A1 ? 1.0f : (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+            acc(s, q, i);
             asm volatile("" ::"v"(s.r), "v"(s.g), "v"(s.b), "v"(s.a));
             __builtin_amdgcn_sched_barrier(0);
+            c = cn;
+            r = rn;
         }
         const F4 u = div12(s);
         if constexpr (EPI == EPI_PLAIN) {
@@ -730,6 +748,7 @@ __global__ void __launch_bounds__(256) fixup_kernel(Tables tb, CTex A, CTex B, C
         x = (uint32_t)(j % W);
         if (plan[x].y != 0u) return;  // an inexact column: its pixels are the first part's
     }
+    if (x >= W || y >= H) return;  // defensive: a list entry outside the frame
     const uint2 cx = plan[x], cy = plan[W + y];
     if constexpr (EPI == EPI_Y) {
         out.px[y * W + x] = enc(L, remix(sample_same(L, A, cx, cy), sample_same(L, B, cx, cy)));
@@ -831,12 +850,13 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
 // four pixels (14 LDS reads per pixel instead of 21 at 4096x2048), each pixel reduced exactly as
 // up8(PlanSrc) does.  HX / HY: the tap's half flags.
 constexpr int FP_YQ = 40;  // 32 + the taps' reach (38 at 4096x2048)
-// The tile's row stride in float4: a multiple of 16 (256 B, all 64 banks), so that the quad loops'
-// ds_read_b128 -- lane l reads column l & 15 of row l >> 4, and the instruction's lane groups {0-3, 12-15,
-// 20-27}, {4-11, 16-19, 28-31}, ... take two rows each -- touch 16 distinct 4-bank slots per group (a
-// 40-float4 stride puts row 1's columns 4-11 on the slots of row 0's 12-15 and 0-3: 2-way conflicts).
+// The tile's row stride in float4: odd.  The quad loops' ds_read_b128 lane groups ({0-3, 12-15, 20-27},
+// {4-11, 16-19, 28-31}, ...) take two quad rows each, and lane l reads texel column 2 (l & 15) + c: the
+// even 4-bank slots of one quad row, and with an even stride (40) the same slots in the next row -- 2-way
+// conflicts (rocprofv3: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.34).  An odd stride puts the next row
+// on the odd slots.
 #ifndef BH_BLOOM_FS_YQ
-#define BH_BLOOM_FS_YQ 48
+#define BH_BLOOM_FS_YQ 41
 #endif
 constexpr int FS_YQ = BH_BLOOM_FS_YQ;
 template <int HX, int HY>
@@ -1182,7 +1202,10 @@ __device__ __forceinline__ void quad_taps_std(const float4* base, F4 (&s)[2][2],
 // outermost blocks (and footprints over FP) take the general sampler per pixel.  STD: 0 = the runtime
 // plan P, else the standard plan A = STD (P still gives the interior).
 constexpr int FP_UPQ = 28;  // footprint of 16 texels + the taps' reach (24 at 4096x2048)
-// row stride in float4, a multiple of 16 for the quad reads' lane groups (see FS_YQ)
+// row stride in float4, a multiple of 16: here lane l reads texel column (l & 15) + c (a 2:1 pass reads
+// one texel per output quad), 16 consecutive slots per quad row, and the lane groups take two quad rows
+// (see FS_YQ): with 28 the second row overlapped the first's slots (bank conflicts 0.42 of LDS-active
+// cycles), with 32 it lands on the same slots of the next 64 banks (0.01)
 #ifndef BH_BLOOM_FS_UPQ
 #define BH_BLOOM_FS_UPQ 32
 #endif
@@ -1511,6 +1534,7 @@ static int sep_tile(int ext) { return ext <= 0 ? 0 : ext <= 24 ? 24 : ext <= 44 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
                                                                         const uint8_t* buckets, const uint32_t* codes,
                                                                         const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                        uint32_t rx, uint32_t ry,
                                                                         const uint32_t* sep, int ext, uint32_t epi,
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
@@ -1521,12 +1545,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     const uint2* S = reinterpret_cast<const uint2*>(same);
     const Tex O{out, ow, oh}, X{aux ? aux : out, ow, oh};
     const dim3 g = grid_for(ow, oh);
-#define BH_SEP(FP, E) hipLaunchKernelGGL((up_sep_kernel<FP, E>), g, dim3(256), 0, s, tb, A, P, O, O0, O1, S, X)
+#define BH_SEP(FP, E, RAW) \
+    hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
     const int fp = sep_tile(ext);
     if (fp == 24) {
-        if (epi == EPI_Y) BH_SEP(24, EPI_Y); else if (epi == EPI_FINAL) BH_SEP(24, EPI_FINAL); else BH_SEP(24, EPI_PLAIN);
+        if (epi == EPI_Y) BH_SEP(24, EPI_Y, false); else if (epi == EPI_FINAL) BH_SEP(24, EPI_FINAL, false);
+        else BH_SEP(24, EPI_PLAIN, false);
     } else if (fp == 44) {
-        if (epi == EPI_Y) BH_SEP(44, EPI_Y); else if (epi == EPI_FINAL) BH_SEP(44, EPI_FINAL); else BH_SEP(44, EPI_PLAIN);
+        if (epi == EPI_Y) BH_SEP(44, EPI_Y, true); else if (epi == EPI_FINAL) BH_SEP(44, EPI_FINAL, true);
+        else BH_SEP(44, EPI_PLAIN, true);
     } else {
         return (int)hipErrorInvalidValue;
     }
@@ -1542,6 +1569,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
                                                                           uint32_t h, hipStream_t s) {
+    if (n_cols > w || n_rows > h || !list) return (int)hipErrorInvalidValue;  // the list of this frame's plan
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
     if (n == 0) return 0;
     const Tables tb{lut, enc, buckets, codes};
@@ -1645,8 +1673,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
         }
     }
     if (shader == SH_UP && !P.valid && sep && sep_tile(sep_ext) != 0 && !g_no_sep) {
-        return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, sep, sep_ext, EPI_PLAIN, nullptr, nullptr, nullptr,
-                                   out, nullptr, ow, oh, s);
+        return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, rx, ry, sep, sep_ext, EPI_PLAIN, nullptr, nullptr,
+                                   nullptr, out, nullptr, ow, oh, s);
     }
     switch (shader) {
         case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;

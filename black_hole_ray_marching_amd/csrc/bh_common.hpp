@@ -244,6 +244,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t 
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
                                                                         const uint8_t* buckets, const uint32_t* codes,
                                                                         const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                        uint32_t rx, uint32_t ry,
                                                                         const uint32_t* sep, int ext, uint32_t epi,
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,

@@ -669,14 +669,15 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 // rx == 0: the same-size plan of the remixes (bh_bloom_same_plan, 8 B per column and row) followed by the
 // list of its inexact columns, then rows (the fused epilogues' fix-up pixels).  A capturing call never
 // builds one (bh_bloom refuses a set not prepared outside capture).
-const bh_ctx::SepPlan* sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw,
-                                uint32_t th, uint32_t rx, uint32_t ry, int* err) {
+// Returned by value (dev == nullptr on failure): the cache is a vector that later plans may reallocate.
+bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th,
+                         uint32_t rx, uint32_t ry, int* err) {
     const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
     for (const auto& p : b->sep_plans)
-        if (p.key == key) return &p;
+        if (p.key == key) return p;
     if (capturing) {
         *err = (int)hipErrorStreamCaptureUnsupported;
-        return nullptr;
+        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
     }
     bh_ctx::SepPlan P{key, nullptr, 0, 0u, 0u};
     std::vector<uint32_t> h;
@@ -698,17 +699,17 @@ const bh_ctx::SepPlan* sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_
     }
     if (P.ext < 0) {
         *err = (int)hipErrorInvalidValue;
-        return nullptr;
+        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
     }
     hipError_t e = hipMalloc(&P.dev, h.size() * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(P.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         if (P.dev) (void)hipFree(P.dev);
-        *err = hip_fail(e, "bloom separable plan");
-        return nullptr;
+        *err = (int)e;
+        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
     }
     b->sep_plans.push_back(P);
-    return &b->sep_plans.back();
+    return P;
 }
 
 struct BloomRun {
@@ -720,12 +721,12 @@ struct BloomRun {
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
         if (err != 0) return;
-        const bh_ctx::SepPlan* sp = sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1])
-                                        ? sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err)
-                                        : nullptr;
+        bh_ctx::SepPlan sp{};
+        if (sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1]))
+            sp = sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err);
         if (err == 0)
             err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
-                                       sp ? sp->dev : nullptr, sp ? sp->ext : 0, s);
+                                       sp.dev, sp.ext, s);
     }
 };
 
@@ -837,22 +838,22 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         // up passes with a separable plan carry the remixes as epilogues for the pixels whose column and
         // row sample exactly (bh_bloom.hip up_sep_kernel, EPI_Y / EPI_FINAL) and a fix-up pass covers the
         // inexact columns and rows; other plans run the plain pass and the plan remix kernels.
-        const bh_ctx::SepPlan* same = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
-        const uint32_t* plan = same ? same->dev : nullptr;
+        const bh_ctx::SepPlan same = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
+        const uint32_t* plan = same.dev;
         const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
         // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
         // fix-up of the inexact pixels -- or the plain pass and the remix kernel
         auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
                             uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
             if (R.err != 0) return;
-            const bh_ctx::SepPlan* sp = bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1])
-                                            ? sep_plan(B, capturing, W, H, sw, sh, res[0], res[1], &R.err)
-                                            : nullptr;
+            bh_ctx::SepPlan sp{};
+            if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
+                sp = sep_plan(B, capturing, W, H, sw, sh, res[0], res[1], &R.err);
             if (R.err != 0) return;
-            if (sp && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, sp->dev, sp->ext, epi, own0,
-                                          own1, plan, dst, aux, W, H, s) == 0) {
+            if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
+                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, s) == 0) {
                 R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
-                                              plan, list, same->nc, same->nr, dst, W, H, s);
+                                              plan, list, same.nc, same.nr, dst, W, H, s);
                 return;
             }
             R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);

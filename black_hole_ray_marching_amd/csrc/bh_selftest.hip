@@ -42,6 +42,10 @@ __device__ __forceinline__ void record(unsigned long long* cnt, uint32_t* ex, ui
 // op 11: wave_max_u32 (DPP scan) against a serial max, `count` rounds per wave
 // op 12: rcp_from_rsq over EVERY q with bits in [base, base + count) whose Q = RN(RN(q*q) * sqrt_core(q))
 //        passes the division guard, against the IEEE reciprocal 1/Q (ex = q, Q, got, want)
+// op 13: for every q with bits in [base, base + count) whose rcp_from_rsq reciprocal r differs from RN(1/Q)
+//        (op 12's mismatches: 1/Q within ~2^-41 of a rounding midpoint, r its faithful neighbour), div_core
+//        with that r over EVERY numerator significand n in [1, 2) against the IEEE quotient n / Q; the
+//        wave takes each such q in turn, its 64 lanes splitting the 2^23 numerators (ex = n, Q, got, want)
 // op 7: div_core over EVERY pair of significands (n, d) in [1, 2)^2 with d's 23 fraction bits in
 //       [base, base + count / 2^23): all 2^23 numerators per denominator (the full 2^46 square is
 //       tools/ubench/cr_forms.hip; the tests cover blocks that include the extreme fractions)
@@ -63,6 +67,41 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
             uint32_t want = 0;
             for (int l = 0; l < 64; ++l) want = max(want, (uint32_t)__builtin_amdgcn_readlane((int)v, l));
             if (lane == 0u && got != want) record(cnt, ex, (uint32_t)w, (uint32_t)r, got, want);
+        }
+        return;
+    }
+    if (op == 13) {
+        // wave-uniform trip count (every lane runs the same iterations; lanes past `count` test nothing)
+        const uint32_t lane = threadIdx.x & 63u;
+        const uint64_t w0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+        for (uint64_t b = w0; b < count; b += stride) {
+            const uint64_t i = b + lane;
+            bool bad = false;
+            float Q = 0.0f, r = 0.0f;
+            if (i < count) {
+                const float q = __uint_as_float((uint32_t)(base + i));
+                if (!crm::sqrt_bad(q)) {
+                    const crm::SqrtY sy = crm::sqrt_core_y(q);
+                    Q = (q * q) * sy.s;
+                    if (!crm::div_d_bad(Q)) {
+                        r = crm::rcp_from_rsq(Q, sy.y).r;
+                        bad = __float_as_uint(r) != __float_as_uint(1.0f / Q);
+                    }
+                }
+            }
+            uint64_t m = __builtin_amdgcn_ballot_w64(bad);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const float Qw = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(Q), l));
+                const float rw = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r), l));
+                for (uint32_t k = lane; k < (1u << 23); k += 64u) {
+                    const float n = __uint_as_float(0x3F800000u | k);
+                    const float got = crm::div_core(n, crm::Rcp{Qw, rw}), want = n / Qw;
+                    if (__float_as_uint(got) != __float_as_uint(want))
+                        record(cnt, ex, __float_as_uint(n), __float_as_uint(Qw), __float_as_uint(got), __float_as_uint(want));
+                }
+            }
         }
         return;
     }
@@ -179,7 +218,7 @@ __global__ void __launch_bounds__(256) selftest_kernel(int op, uint64_t base, ui
 
 extern "C" int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                                   uint32_t* out_examples, int device) {
-    if (op < 0 || op > 12 || !out_mismatches) return BH_ERR_INVALID_ARG;
+    if (op < 0 || op > 13 || !out_mismatches) return BH_ERR_INVALID_ARG;
     int prev = 0;
     (void)hipGetDevice(&prev);
     if (hipSetDevice(device) != hipSuccess) return BH_ERR_NO_DEVICE;

@@ -370,7 +370,9 @@ int bh_srgb_encode_table(float* out257);
  * the sRGB encoder against op 4's over bit patterns [base, base+count); op 11: the march kernel's
  * wave-wide max of the tile costs (DPP scan) against a serial max, `count` random rounds per wave
  * seeded by base; op 12: the march step's reciprocal of rd_derivative's denominator seeded from the
- * square-root core's v_rsq, over q bit patterns [base, base+count), against the IEEE 1/Q).  *out_mismatches = number of differing results;
+ * square-root core's v_rsq, over q bit patterns [base, base+count), against the IEEE 1/Q; op 13: for the
+ * q of that range whose seeded reciprocal differs from 1/Q, the division core with it over every numerator
+ * significand against the IEEE quotient).  *out_mismatches = number of differing results;
  * out_examples (8 u32, optional) = up to two (a, b, got, want) bit patterns.  Synchronous. */
 int bh_selftest_crmath(int op, uint64_t base, uint64_t count, uint64_t* out_mismatches,
                        uint32_t* out_examples, int device);

@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 4: the general fused bloom chain with fused epilogues -- parity, timings, kernel trace, PMC; A/B of
-# the quad kernels' padded tile strides (fs0: unpadded, fs1: padded = the build)
+# round 4: the general fused bloom chain with fused epilogues -- parity first, then timings, kernel trace,
+# PMC; A/B of the quad kernels' padded tile strides (fs0: unpadded, fs1: padded = the build)
 set -u
 O=gpurun_out/r04c; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bloom.py > $O/pytest_bloom.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_bloom.py > $O/pytest_bloom.log 2>&1 || exit 1
 for s in "1920 1080" "1280 720" "4096 2048"; do
   set -- $s
   timeout -k 10 120 python tools/bench_bloom.py --width $1 --height $2 --steps 50 >> $O/bloom.log 2>&1 || exit 1

@@ -24,6 +24,7 @@ def main():
     p.add_argument("--rows", default="64", help="comma list of tile rows in flight (0 = all)")
     p.add_argument("--root-ratio", default="1", help="comma list: numbers or 'auto'")
     p.add_argument("--it", type=int, default=12)
+    p.add_argument("--transport", choices=["rgbm", "rgbm14"], default="rgbm14")
     a = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
@@ -33,7 +34,9 @@ def main():
     fmt = bh.BH_OUT_RGBA16F
     D = a.D
     sky = bh.synthetic_sky(4096, 2048)
-    tb = bh.tile_bytes(bh.BH_LAYOUT_TILES_RGBM, fmt)
+    layout = bh.BH_LAYOUT_TILES_RGBM14 if a.transport == "rgbm14" else bh.BH_LAYOUT_TILES_RGBM
+    ufmt = fmt | bh.BH_UNPACK_RGBM14 if a.transport == "rgbm14" else fmt
+    tb = bh.tile_bytes(layout, fmt)
     for n in (int(v) for v in a.n.split(",")):
         for rr in a.root_ratio.split(","):
             ratio = multigpu.auto_root_ratio(n) if rr == "auto" else float(rr)
@@ -41,7 +44,7 @@ def main():
             part = bh.Partition(W, H, weights) if len(set(weights)) > 1 else None
             counts = part.counts if part else [bh.shard_tile_count(W, H, k, n) for k in range(n)]
             stride = max(counts)
-            kw = dict(layout=bh.BH_LAYOUT_TILES_RGBM, shard_count=n, **({"partition": part} if part else {}))
+            kw = dict(layout=layout, shard_count=n, **({"partition": part} if part else {}))
             for rows in (int(r) for r in a.rows.split(",")):
                 scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
                 bufs = [torch.empty((D * stride, tb), dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -62,9 +65,9 @@ def main():
                     for f in range(D):
                         if part:
                             bh.tiles_unpack_rgbm_partition(gathered[f * stride:], cols[f], bos[f], part, D * stride,
-                                                           fmt, stream=ss, rows_in_flight=rows)
+                                                           ufmt, stream=ss, rows_in_flight=rows)
                         else:
-                            bh.tiles_unpack_rgbm(gathered[f * stride:], cols[f], bos[f], W, H, n, D * stride, fmt,
+                            bh.tiles_unpack_rgbm(gathered[f * stride:], cols[f], bos[f], W, H, n, D * stride, ufmt,
                                                  stream=ss, rows_in_flight=rows)
 
                 def run(k, shard, do_render, do_unpack):
@@ -87,6 +90,7 @@ def main():
                 r0 = run(a.it, 0, True, True)
                 r1 = run(a.it, 1, True, False)
                 out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
+                       "transport": a.transport, "tile_bytes": tb,
                        "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": counts[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),

@@ -1,0 +1,50 @@
+"""Predicted multi-GPU line of the driver's protocol (`bench.py --gpus N --steps K --warmup W`) from one-GPU
+probes plus the xGMI link model.  Reads tools/probe_rank0.py's JSON lines (rank 0's render +
+unpack, another rank's render, the unpack alone; ms per frame) and prints, per (N, frames per launch D,
+transport, rank-0 ratio), the steady-state frame time and the line's ms per frame including the drain.
+
+Model (one step = one batch of D frames, batch i's gather overlaps batch i+1's render):
+  render    = max(rank 0's render + unpack (side stream), another rank's render)        [probe]
+  ingress   = (1 - s0) * frame_bytes / (links * link_GBps)   rank 0 receives N - 1 shards over N - 1 links
+  steady    = max(render, ingress)
+  drain     = (ingress + unpack) / K per frame: the last batch's gather and unpack follow its render
+  predicted = steady + drain;  speedup = one_gpu_ms / predicted
+s0 = rank 0's tile share (its tiles cross no link); frame_bytes = tiles * tile_bytes.  link_GBps: one xGMI
+link's rate in one direction (MI355X: 7 links of 153.6 GB/s bidirectional, 76.8 per direction; RCCL's
+achieved share of it is the model's unknown, `--link-eff`).
+
+    python tools/scale_model.py probe.jsonl --one-gpu-ms 0.556 [--k 20] [--link-gbps 76.8] [--link-eff 1.0]"""
+import argparse
+import json
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("probe")
+    p.add_argument("--one-gpu-ms", type=float, required=True)
+    p.add_argument("--k", type=int, default=20)
+    p.add_argument("--link-gbps", type=float, default=76.8)
+    p.add_argument("--link-eff", type=float, default=1.0)
+    a = p.parse_args()
+    rows = [json.loads(x) for x in open(a.probe) if x.startswith("{")]
+    print(f"one GPU {a.one_gpu_ms} ms/frame, K = {a.k}, link {a.link_gbps} GB/s x {a.link_eff} per direction")
+    print("| N | D | transport | weights | render (ms) | ingress (ms) | binds | predicted ms/frame | Gpix/s | vs 1 GPU |")
+    print("|---|---|---|---|---|---|---|---|---|---|")
+    for r in rows:
+        n = r["n"]
+        W, H = (int(v) for v in r["frame"].split("x"))
+        tiles = ((W + 7) // 8) * ((H + 7) // 8)
+        w = r.get("weights") or [1] * n
+        s0 = w[0] / sum(w)
+        frame_bytes = tiles * r["tile_bytes"]
+        ingress = (1.0 - s0) * frame_bytes / ((n - 1) * a.link_gbps * a.link_eff * 1e9) * 1e3
+        render = max(r["rank0_render_plus_unpack_ms"], r["rank1_render_ms"])
+        steady = max(render, ingress)
+        pred = steady + (ingress + r["unpack_only_ms"]) / a.k
+        print(f"| {n} | {r['frames_per_launch']} | {r.get('transport', 'rgbm')} | {w if r.get('weights') else 'even'} | "
+              f"{render:.4f} | {ingress:.4f} | {'render' if render >= ingress else 'xGMI'} | {pred:.4f} | "
+              f"{W * H / pred / 1e6:.1f} | {a.one_gpu_ms / pred:.2f}x |")
+
+
+if __name__ == "__main__":
+    main()
