@@ -80,9 +80,9 @@ __device__ __forceinline__ Rcp rcp_refined(float d) {
 // multiplies, 6 issue cycles, where v_rcp takes 8 and blocks the SIMD's vector issue for all of them:
 // tools/ubench/trans_mix.hip), within ~2^-20 of 1/Q; one refinement r = z + z(1 - Qz) lands within
 // ~2^-40 of 1/Q before its rounding: RN(1/Q) except where 1/Q lies within that of a rounding midpoint (840
-// of the 3.5e8 q in [2^-17, 2^25), selftest op 12), where it is the faithful neighbour.  div_core's one
-// correction does not need RN(1/Q) there: for each of those Q it returns the IEEE quotient for every
-// numerator significand (selftest op 13, exhaustive), so every quotient of the step is unchanged.
+// of the 3.5e8 q in [2^-17, 2^25), selftest op 12), where it is the faithful neighbour -- and with that
+// neighbour div_core's one correction misses the IEEE quotient for 60 (n, Q) pairs, at Q significands
+// next to 2 (selftest op 13).  So the march keeps rcp_refined (BH_RCP_SEED 0); measured, not used.
 __device__ __forceinline__ Rcp rcp_from_rsq(float Q, float y) {
     const float y2 = y * y, y4 = y2 * y2, z = y4 * y;
     const float e = __builtin_fmaf(-Q, z, 1.0f);

@@ -54,18 +54,15 @@ def test_div_core_significand_blocks(lib, d0):
     assert m == 0, ex
 
 
-def test_rcp_from_rsq_quotients_exhaustive(lib):
-    """The march step's reciprocal of rd_derivative's denominator Q = (q*q)*sqrt(q), seeded from the square
-    root core's own v_rsq(q) (y^5, one refinement) instead of a v_rcp of Q.  Over every q whose Q passes the
-    division guard [2^-40, 2^60] (every such q lies in [2^-17, 2^25)): the reciprocal is RN(1/Q) except for
-    a few hundred q whose 1/Q lies within ~2^-41 of a rounding midpoint (op 12 counts them), where it is
-    the faithful neighbour; for each of those, the one-correction division with it equals the IEEE
-    quotient for EVERY numerator significand (op 13) -- so every quotient of the step is the IEEE one."""
-    lo, hi = 0x37000000, 0x4C000000  # bits of 2^-17 and 2^25
+def test_rcp_from_rsq_is_not_exact(lib):
+    """A measured negative result kept as a guard against reusing it: the reciprocal of rd_derivative's Q
+    seeded from the square-root core's v_rsq (y^5, one refinement; BH_RCP_SEED, off) is RN(1/Q) except for a
+    few hundred near-midpoint Q (op 12), and with those the one-correction division misses the IEEE quotient
+    for some numerators (op 13) -- which is why the march keeps the v_rcp form (bh_crmath.hpp)."""
+    lo, hi = 0x37000000, 0x4C000000  # bits of 2^-17 and 2^25: every q whose Q passes the division guard
     m12, _ = run(lib, 12, lo, hi - lo)
-    assert m12 < 4096, m12  # the reciprocal itself: RN(1/Q) but for a few near-midpoint Q
-    m, ex = run(lib, 13, lo, hi - lo)
-    assert m == 0, ex
+    m13, ex = run(lib, 13, lo, hi - lo)
+    assert 0 < m12 < 4096 and m13 > 0, (m12, m13, ex)
 
 
 def test_div_core_near_exact_quotients(lib):
