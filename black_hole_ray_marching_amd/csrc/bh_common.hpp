@@ -35,6 +35,7 @@ struct MarchArgs {
     // Uniforms (src/black_hole_maybe.wgsl:58-69)
     float rs, dtm, max_dist, dp;
     uint32_t blackout_eh;
+    uint32_t skip_sdf;         // the root-free step may run (bh_march.hpp, sdf_skip: dtm > 0, 0 < rs <= 8)
     // frame
     uint32_t width, height, max_iters, scene_flags;
     uint32_t format, layout;

@@ -111,6 +111,11 @@ static bool stream_capturing(hipStream_t s) {
 namespace {
 
 thread_local std::string g_last_error;
+// a validation failure without its own message: name the entry point and the check's line
+static int bad_arg(const char* fn, int line) {
+    g_last_error = std::string(fn) + ": invalid argument (bh_host.cpp:" + std::to_string(line) + ")";
+    return BH_ERR_INVALID_ARG;
+}
 
 int hip_fail(hipError_t e, const char* what) {
     g_last_error = std::string(what) + ": " + hipGetErrorString(e);
@@ -310,13 +315,13 @@ const char* bh_last_error(void) { return g_last_error.c_str(); }
 // Scene::new defaults, src/scene.rs:89-137 (RS 1.0, max dt 0.5, bg 0.5, blackout PodBool::r#false()
 // whose inner is 1 (src/podbool.rs:24-26), max dist 250, distortion 1.0); 24 B padded to 32.
 int bh_srgb_encode_table(float* out257) {
-    if (!out257) return BH_ERR_INVALID_ARG;
+    if (!out257) return bad_arg(__func__, __LINE__);
     srgb_encode_table(out257);
     return BH_OK;
 }
 
 int bh_uniforms_default(bh_uniforms* out) {
-    if (!out) return BH_ERR_INVALID_ARG;
+    if (!out) return bad_arg(__func__, __LINE__);
     std::memset(out, 0, sizeof(*out));
     out->rs = 1.0f;
     out->delta_time_mult = 0.5f;
@@ -329,7 +334,7 @@ int bh_uniforms_default(bh_uniforms* out) {
 
 // src/scene.rs:68-76
 int bh_camera_default(uint32_t width, uint32_t height, bh_camera* out) {
-    if (!out || width == 0 || height == 0) return BH_ERR_INVALID_ARG;
+    if (!out || width == 0 || height == 0) return bad_arg(__func__, __LINE__);
     const float PI = 3.14159265358979323846f;  // std::f32::consts::PI
     *out = bh_camera{{0.0f, 0.0f, -20.0f}, {0.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 0.0f},
                      (float)width / (float)height, PI * 0.5f, 0.1f, 100.0f};
@@ -360,7 +365,7 @@ float axis_norm(uint8_t neg, uint8_t pos) { return (neg == pos) ? 0.0f : (pos ? 
 extern "C" {
 
 int bh_controller_update(const bh_controller* k, bh_camera* cam, float dt, int do_pan, int* moved) {
-    if (!k || !cam) return BH_ERR_INVALID_ARG;
+    if (!k || !cam) return bad_arg(__func__, __LINE__);
     V3 pos{cam->pos[0], cam->pos[1], cam->pos[2]};
     V3 dir{cam->dir[0], cam->dir[1], cam->dir[2]};
     V3 up{cam->up[0], cam->up[1], cam->up[2]};
@@ -401,7 +406,7 @@ int bh_controller_update(const bh_controller* k, bh_camera* cam, float dt, int d
 
 int bh_camera_look_at(const float pos[3], const float target[3], uint32_t width, uint32_t height,
                       bh_camera* out) {
-    if (!pos || !target) return BH_ERR_INVALID_ARG;
+    if (!pos || !target) return bad_arg(__func__, __LINE__);
     int st = bh_camera_default(width, height, out);
     if (st != BH_OK) return st;
     V3 p{pos[0], pos[1], pos[2]}, t{target[0], target[1], target[2]};
@@ -421,7 +426,7 @@ int bh_camera_look_at(const float pos[3], const float target[3], uint32_t width,
 // (columns s, u, -f).  glam's general f32 Mat4::inverse may differ from the transpose in the last
 // ulp; the corners are kernel INPUTS, so this host step is outside kernel parity.
 int bh_camera_uniform_update(const bh_camera* cam, bh_camera_uniform* out) {
-    if (!cam || !out) return BH_ERR_INVALID_ARG;
+    if (!cam || !out) return bad_arg(__func__, __LINE__);
     std::memset(out, 0, sizeof(*out));
     static const float st[3][2] = {{3.0f, 1.0f}, {-1.0f, 1.0f}, {-1.0f, -3.0f}};
     for (int i = 0; i < 3; ++i) { out->screen_tri[i][0] = st[i][0]; out->screen_tri[i][1] = st[i][1]; }
@@ -483,7 +488,7 @@ static void sky_rows(uint8_t* out, uint32_t w, uint32_t h, uint64_t seed, uint32
 
 // Rows are independent, so the result does not depend on the thread count.
 int bh_synthetic_sky(uint8_t* out, uint32_t w, uint32_t h, uint64_t seed) {
-    if (!out || w == 0 || h == 0) return BH_ERR_INVALID_ARG;
+    if (!out || w == 0 || h == 0) return bad_arg(__func__, __LINE__);
     unsigned nt = std::thread::hardware_concurrency();
     nt = nt == 0 ? 1 : (nt > 16 ? 16 : nt);
     if (nt > h) nt = h;
@@ -497,7 +502,7 @@ int bh_synthetic_sky(uint8_t* out, uint32_t w, uint32_t h, uint64_t seed) {
 }
 
 int bh_create(const uint8_t* sky, uint32_t sky_w, uint32_t sky_h, int device, bh_ctx** out) {
-    if (!sky || !out || sky_w == 0 || sky_h == 0 || sky_w > 32768u || sky_h > 32768u) return BH_ERR_INVALID_ARG;
+    if (!sky || !out || sky_w == 0 || sky_h == 0 || sky_w > 32768u || sky_h > 32768u) return bad_arg(__func__, __LINE__);
     *out = nullptr;
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
@@ -739,7 +744,7 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     // W, H <= 65536 as bh_render: the bloom kernels index texels with 32 bits (y * w + x < 2^32)
     if (!c || !col || !blackout || !out || W == 0 || H == 0 || W > 65536u || H > 65536u || levels < 1 || levels > 12 ||
         schedule > BH_BLOOM_LITERAL)
-        return BH_ERR_INVALID_ARG;
+        return bad_arg(__func__, __LINE__);
     hipError_t e;
     DeviceScope dev(c->device);
     if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
@@ -917,14 +922,14 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
 }
 
 int bh_graph_release(bh_ctx* c) {
-    if (!c) return BH_ERR_INVALID_ARG;
+    if (!c) return bad_arg(__func__, __LINE__);
     for (auto& o : c->orders) o.captured = false;
     for (auto& b : c->blooms) b.captured = false;
     return BH_OK;
 }
 
 int64_t bh_shard_tile_count(uint32_t width, uint32_t height, uint32_t shard_index, uint32_t shard_count) {
-    if (width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count) return BH_ERR_INVALID_ARG;
+    if (width == 0 || height == 0 || shard_count == 0 || shard_index >= shard_count) return bad_arg(__func__, __LINE__);
     return (int64_t)bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, shard_index, shard_count);
 }
 
@@ -1087,21 +1092,27 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     return bh_render_frames(c, 1u, cam, U, d, stream);
 }
 
+// A/B switch (diagnostics): BH_NO_SDF_SKIP set => every step evaluates its SDF roots (bh_march.hpp, sdf_skip)
+static bool sdf_skip_disabled() {
+    static const bool off = std::getenv("BH_NO_SDF_SKIP") != nullptr;
+    return off;
+}
+
 int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams, const bh_uniforms* U,
                      const bh_render_desc* descs, void* stream) {
-    if (!c || !cams || !U || !descs || n_frames == 0 || n_frames > BH_MAX_FRAMES) return BH_ERR_INVALID_ARG;
+    if (!c || !cams || !U || !descs || n_frames == 0 || n_frames > BH_MAX_FRAMES) return bad_arg(__func__, __LINE__);
     const bh_render_desc* d = &descs[0];
     const bh_camera_uniform* cam = &cams[0];
-    if (!d->out_col) return BH_ERR_INVALID_ARG;
-    if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return BH_ERR_INVALID_ARG;
-    if (d->max_iters == 0 || d->max_iters > 65535u) return BH_ERR_INVALID_ARG;
-    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGBM14) return BH_ERR_INVALID_ARG;
-    if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER | BH_SCHED_FLAG_ISSUE_ORDER | BH_SCHED_FLAG_LATENCY))) return BH_ERR_INVALID_ARG;
-    if (d->scene_flags & ~BH_SCENE_DEFAULT) return BH_ERR_INVALID_ARG;
-    if (d->shard_count == 0 || d->shard_index >= d->shard_count) return BH_ERR_INVALID_ARG;
-    if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return BH_ERR_INVALID_ARG;
+    if (!d->out_col) return bad_arg(__func__, __LINE__);
+    if (d->width == 0 || d->height == 0 || d->width > 65536u || d->height > 65536u) return bad_arg(__func__, __LINE__);
+    if (d->max_iters == 0 || d->max_iters > 65535u) return bad_arg(__func__, __LINE__);
+    if (d->format > BH_OUT_BGRA8_SRGB || d->math > BH_MATH_FAST || d->layout > BH_LAYOUT_TILES_RGBM14) return bad_arg(__func__, __LINE__);
+    if ((d->schedule & 0xFFu) > BH_SCHED_PERSISTENT || (d->schedule & ~(0xFFu | BH_SCHED_FLAG_STATIC_ORDER | BH_SCHED_FLAG_ISSUE_ORDER | BH_SCHED_FLAG_LATENCY))) return bad_arg(__func__, __LINE__);
+    if (d->scene_flags & ~BH_SCENE_DEFAULT) return bad_arg(__func__, __LINE__);
+    if (d->shard_count == 0 || d->shard_index >= d->shard_count) return bad_arg(__func__, __LINE__);
+    if (d->layout == BH_LAYOUT_ROWMAJOR && d->shard_count != 1) return bad_arg(__func__, __LINE__);
     for (uint32_t i = 0; i < n_frames; ++i) {
-        if (!descs[i].out_col || !same_launch(d, &descs[i])) return BH_ERR_INVALID_ARG;
+        if (!descs[i].out_col || !same_launch(d, &descs[i])) return bad_arg(__func__, __LINE__);
         if (!screen_tri_default(&cams[i])) { g_last_error = "non-default screen triangle"; return BH_ERR_UNSUPPORTED; }
     }
     if ((d->layout == BH_LAYOUT_TILES_RGBM || d->layout == BH_LAYOUT_TILES_RGBM14) &&
@@ -1125,6 +1136,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     std::memset(&a, 0, sizeof(a));
     a.rs = U->rs; a.dtm = U->delta_time_mult; a.max_dist = U->max_dist; a.dp = U->distortion_power;
     a.blackout_eh = U->blackout_eh;
+    a.skip_sdf = (U->delta_time_mult > 0.0f && U->rs > 0.0f && U->rs <= 8.0f && !sdf_skip_disabled()) ? 1u : 0u;
     a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
     a.format = d->format; a.layout = d->layout;
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;
@@ -1145,7 +1157,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     } else {
         nt = bh::shard_tile_count(a.tiles_x, a.tiles_y, d->shard_index, d->shard_count);
     }
-    if (nt * n_frames > 0xFFFFFFF0ull) return BH_ERR_INVALID_ARG;
+    if (nt * n_frames > 0xFFFFFFF0ull) return bad_arg(__func__, __LINE__);
     a.n_tiles = (uint32_t)nt;
     // centre-out dispatch blocks of ~one tile row of this shard, centred on the black hole's row
     a.order_block = (uint32_t)((nt + a.tiles_y - 1u) / a.tiles_y);
@@ -1213,7 +1225,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
 }
 
 int bh_set_clock_probe(bh_ctx* c, uint64_t* acc, uint32_t stride) {
-    if (!c || (acc && (stride == 0u || (stride & (stride - 1u)) != 0u))) return BH_ERR_INVALID_ARG;
+    if (!c || (acc && (stride == 0u || (stride & (stride - 1u)) != 0u))) return bad_arg(__func__, __LINE__);
     c->clk = reinterpret_cast<unsigned long long*>(acc);
     c->clk_mask = acc ? stride - 1u : 0u;
     return BH_OK;
@@ -1221,11 +1233,11 @@ int bh_set_clock_probe(bh_ctx* c, uint64_t* acc, uint32_t stride) {
 
 int bh_tiles_unpack(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
                     uint64_t shard_stride_tiles, uint32_t bpp, void* stream) {
-    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
-    if (bpp != 4 && bpp != 8 && bpp != 16) return BH_ERR_INVALID_ARG;
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return bad_arg(__func__, __LINE__);
+    if (bpp != 4 && bpp != 8 && bpp != 16) return bad_arg(__func__, __LINE__);
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
-            return BH_ERR_INVALID_ARG;
+            return bad_arg(__func__, __LINE__);
     int e = bh_launch_tiles_unpack(packed, out, width, height, shard_count, shard_stride_tiles, bpp,
                                    reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
@@ -1239,11 +1251,11 @@ static bool unpack_format_ok(uint32_t format) {
 
 int bh_tiles_unpack_rgb_rows(const void* packed, void* out, uint32_t width, uint32_t height, uint32_t shard_count,
                              uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight, void* stream) {
-    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
-    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return bad_arg(__func__, __LINE__);
+    if (format > BH_OUT_BGRA8_SRGB) return bad_arg(__func__, __LINE__);
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
-            return BH_ERR_INVALID_ARG;
+            return bad_arg(__func__, __LINE__);
     int e = bh_launch_tiles_unpack_rgb(packed, out, width, height, shard_count, shard_stride_tiles, format,
                                        rows_in_flight, reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
@@ -1258,11 +1270,11 @@ int bh_tiles_unpack_rgb(const void* packed, void* out, uint32_t width, uint32_t 
 int bh_tiles_unpack_rgbm(const void* packed, void* out, void* out_bo, uint32_t width, uint32_t height,
                          uint32_t shard_count, uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
                          void* stream) {
-    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return BH_ERR_INVALID_ARG;
-    if (!unpack_format_ok(format)) return BH_ERR_INVALID_ARG;
+    if (!packed || !out || width == 0 || height == 0 || shard_count == 0) return bad_arg(__func__, __LINE__);
+    if (!unpack_format_ok(format)) return bad_arg(__func__, __LINE__);
     for (uint32_t k = 0; k < shard_count; ++k)
         if (bh::shard_tile_count((width + 7u) / 8u, (height + 7u) / 8u, k, shard_count) > shard_stride_tiles)
-            return BH_ERR_INVALID_ARG;
+            return bad_arg(__func__, __LINE__);
     int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, width, height, shard_count, shard_stride_tiles, nullptr,
                                         format, rows_in_flight, reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
@@ -1294,9 +1306,9 @@ std::vector<uint32_t> partition_owners(uint32_t S, const uint32_t* w) {
 int bh_partition_map(uint32_t width, uint32_t height, uint32_t S, const uint32_t* weights, uint32_t* owner_out,
                      uint32_t* index_out) {
     if (width == 0 || height == 0 || width > 65536u || height > 65536u || S == 0 || S > 256 || !weights)
-        return BH_ERR_INVALID_ARG;
+        return bad_arg(__func__, __LINE__);
     const std::vector<uint32_t> owner = partition_owners(S, weights);
-    if (owner.empty()) return BH_ERR_INVALID_ARG;
+    if (owner.empty()) return bad_arg(__func__, __LINE__);
     const uint32_t M = (uint32_t)owner.size(), tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
     std::vector<uint32_t> next(S, 0);
     for (uint32_t ty = 0; ty < ty_n; ++ty)
@@ -1312,11 +1324,11 @@ int bh_partition_map(uint32_t width, uint32_t height, uint32_t S, const uint32_t
 
 int bh_partition_create(uint32_t width, uint32_t height, uint32_t S, const uint32_t* weights, int device,
                         bh_partition** out) {
-    if (!out) return BH_ERR_INVALID_ARG;
+    if (!out) return bad_arg(__func__, __LINE__);
     *out = nullptr;
     const uint32_t tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
     const size_t n = (size_t)tx_n * ty_n;
-    if (n >= (1u << 24)) return BH_ERR_INVALID_ARG;  // packed indices carry 24 bits
+    if (n >= (1u << 24)) return bad_arg(__func__, __LINE__);  // packed indices carry 24 bits
     std::vector<uint32_t> owner(n), index(n);
     int st = bh_partition_map(width, height, S, weights, owner.data(), index.data());
     if (st != BH_OK) return st;
@@ -1364,16 +1376,16 @@ int bh_partition_destroy(bh_partition* P) {
 }
 
 int64_t bh_partition_tile_count(const bh_partition* P, uint32_t shard_index) {
-    if (!P || shard_index >= P->shard_count) return BH_ERR_INVALID_ARG;
+    if (!P || shard_index >= P->shard_count) return bad_arg(__func__, __LINE__);
     return P->count[shard_index];
 }
 
 int bh_tiles_unpack_rgbm_partition(const void* packed, void* out, void* out_bo, const bh_partition* P,
                                    uint64_t shard_stride_tiles, uint32_t format, uint32_t rows_in_flight,
                                    void* stream) {
-    if (!packed || !out || !P || !unpack_format_ok(format)) return BH_ERR_INVALID_ARG;
+    if (!packed || !out || !P || !unpack_format_ok(format)) return bad_arg(__func__, __LINE__);
     for (uint32_t k = 0; k < P->shard_count; ++k)
-        if (P->count[k] > shard_stride_tiles) return BH_ERR_INVALID_ARG;
+        if (P->count[k] > shard_stride_tiles) return bad_arg(__func__, __LINE__);
     int e = bh_launch_tiles_unpack_rgbm(packed, out, out_bo, P->width, P->height, P->shard_count, shard_stride_tiles,
                                         P->tile_loc, format, rows_in_flight, reinterpret_cast<hipStream_t>(stream));
     if (e != 0) return hip_fail((hipError_t)e, "tiles unpack launch");
@@ -1381,14 +1393,14 @@ int bh_tiles_unpack_rgbm_partition(const void* packed, void* out, void* out_bo, 
 }
 
 int64_t bh_tile_bytes(uint32_t layout, uint32_t format) {
-    if (format > BH_OUT_BGRA8_SRGB) return BH_ERR_INVALID_ARG;
+    if (format > BH_OUT_BGRA8_SRGB) return bad_arg(__func__, __LINE__);
     const int64_t bpp = format == BH_OUT_RGBA32F ? 16 : format == BH_OUT_RGBA16F ? 8 : 4;
     switch (layout) {
         case BH_LAYOUT_TILES: return 64 * bpp;
         case BH_LAYOUT_TILES_RGB: return 48 * bpp;
         case BH_LAYOUT_TILES_RGBM: return 48 * bpp + 8;
         case BH_LAYOUT_TILES_RGBM14: return format == BH_OUT_RGBA16F ? 344 : BH_ERR_UNSUPPORTED;
-        default: return BH_ERR_INVALID_ARG;
+        default: return bad_arg(__func__, __LINE__);
     }
 }
 

@@ -265,7 +265,8 @@ struct FOps {
     __device__ __forceinline__ v3 accel(v3 p, float s) { return accel_qs<K>(p, s, dot(p, p), 0.0f); }
     __device__ __forceinline__ void sq_args(float, float) {}
     __device__ __forceinline__ void sq_arg(float) {}
-    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags, float&, float&) {
+    __device__ __forceinline__ void sdf_args(v3, float&, float&, float&) {}
+    __device__ __forceinline__ float sdf_from(v3 p, float rs, uint32_t flags, float, float, float) {
         const float rho = __builtin_amdgcn_sqrtf(p.x * p.x + p.z * p.z);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y) - 0.02f);
         // min of the four sphere SDFs == sqrt(min of squared distances) - 0.5 (sqrt is monotone)
@@ -419,11 +420,9 @@ struct XOps {
     }
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
-    // sdf(p) with the arguments of its two roots (for sq_args)
-    __device__ __forceinline__ float sdf(v3 p, float rs, uint32_t flags, float& rho2, float& qm) {
+    // sdf_args: the arguments of its two roots (rho^2, the markers' qm) and y*y; sdf_from: the rest
+    __device__ __forceinline__ void sdf_args(v3 p, float& rho2, float& yy, float& qm) {
         rho2 = p.x * p.x + p.z * p.z;
-        const float rho = sqrt(rho2);
-        const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
         // The four sphere arguments are q1,2 = (xx + (+-10 - y)^2) + zz and q3,4 = ((+-10 - x)^2 + yy)
         // + zz.  Of each pair only the sphere on the point's side can be the minimum, and its
         // argument is computed from t = RN(10 - |y|) (resp. |x|): RN(-10 - y) = -RN(10 + y) and
@@ -431,11 +430,16 @@ struct XOps {
         // monotone in |t|, so the rounded q of the near sphere is <= the far one's and equals
         // (xx + t*t) + zz bit for bit.  min(q1..q4) == min(qy, qx): 11 ops instead of 20
         // (tests/test_oracle.py::test_marker_pair_reduction checks the identity).
-        const float xx = p.x * p.x, yy = p.y * p.y;
+        const float xx = p.x * p.x;
+        yy = p.y * p.y;
         const float dz = -10.0f - p.z, zz = dz * dz;
         const float ty = 10.0f - fabsf(p.y), tx = 10.0f - fabsf(p.x);
         const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
         qm = fminf(qy, qx);
+    }
+    __device__ __forceinline__ float sdf_from(v3 p, float rs, uint32_t flags, float rho2, float, float qm) {
+        const float rho = sqrt(rho2);
+        const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
         const float m = sqrt(qm) - 0.5f;
         // fminf(disc, inf) == disc and fminf(inf, m) == m bit for bit: same result as selecting
         return fminf((flags & BH_SCENE_DISC) ? disc : __builtin_inff(),
@@ -471,6 +475,50 @@ constexpr bool sf_cam_out(uint32_t sf) { return sf != SF_DYN && (sf & SF_CAM_OUT
 constexpr float R2_GT1 = 0x1.000002p0f;
 
 __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
+
+#ifndef BH_SDF_SKIP
+#define BH_SDF_SKIP 1
+#endif
+#ifdef BH_DIAG_SLOW
+__device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps;
+// one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
+#define BH_DIAG_SKIP_COUNT()                                                                              \
+    do {                                                                                                  \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))          \
+            atomicAdd(&g_diag_skip_wave_steps, 1u);                                                       \
+    } while (0)
+#else
+#define BH_DIAG_SKIP_COUNT() do {} while (0)
+#endif
+
+#if !BH_FAST
+// Does this lane's step have dt == dtm*r (:307-310) and no surface hit (:286-288), whatever its three SDF
+// roots are?  From the step's own rounded values (r = RN(sqrt r2), dtr = RN(dtm r), rho2, y*y, the markers'
+// qm and the photon sphere's qps, all formed exactly as the full step forms them), with no root:
+//   T = RN(1.125 dtr + 0.002);  a distance term d = RN(RN(sqrt v) - c) passes when v >= RN(RN(T + c)^2):
+//   disc (:121)     rho2 >= (T + RN(6 rs))^2  or  y*y >= (T + 0.02)^2   [disc >= RN(rho - 6rs) and
+//                   >= RN(|y| - 0.02): fmaxf is >= each non-NaN operand]
+//   markers         qm  >= (T + 0.5)^2        photon sphere (:294)  qps >= (T + 0.075)^2
+// Proof that a passing lane has dt == dtr and no surface (exact mode: RN sqrt, IEEE ops; dtm > 0 and
+// 0 < rs <= 8, the host's skip_sdf gate, so dtr >= 0 and T >= 0.002 (1 - 2^-24)): u = RN(T + c) >=
+// (T + c)(1 - 2^-24) and RN(u^2) >= u^2 (1 - 2^-24), so sqrt v >= (T + c)(1 - 2^-24)^1.5 (for y*y = RN(y^2)
+// one more factor) and RN(sqrt v) >= (T + c)(1 - 2^-22); d >= RN(T - (T + c) 2^-22) >= T (1 - 2^-17.6)
+// (c <= 48.0001, T >= 0.00199).  So dist = min of the enabled terms >= that bound >= 0.00199 > MIN_DIST
+// (no surface), and 0.9f d >= (0.9f * 1.125) dtr (1 - 2^-17.5) = 1.0125 dtr (1 - 2^-17.5) > dtr, so
+// RN(0.9f dist) >= dtr (dtr is a float) and fminf(RN(dist * 0.9), dtr) == dtr.  NaN fails every test;
+// an infinite threshold passes only an infinite argument, whose distance is +inf as the full step's.
+// In the exact build's core pass a wrong r (r2 outside the root core's domain) also raises the k1
+// division guard, so that step re-runs in IEEE ops, where the proof holds as written.
+// tests/test_skip.py checks the implication on adversarial samples of the step's float32 arithmetic.
+__device__ __forceinline__ bool sdf_skip(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
+                                         float qm, float qps) {
+    const float T = __builtin_fmaf(dtr, 1.125f, 0.002f);
+    const float u6 = T + 6.0f * a.rs, uy = T + 0.02f, um = T + 0.5f, up = T + 0.075f;
+    const bool disc_ok = !(flags & BH_SCENE_DISC) | (rho2 >= u6 * u6) | (yy >= uy * uy);
+    const bool mark_ok = !(flags & BH_SCENE_MARKERS) | (qm >= um * um);
+    return disc_ok & mark_ok & (qps >= up * up);
+}
+#endif
 
 // UNI: every active lane of the wave is at loop iteration `it` (n_rk == it: the ping-pong loop), so the
 // cap test is a wave-uniform (scalar) compare.
@@ -508,28 +556,67 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         if (__builtin_amdgcn_ballot_w64(bo_on & (r2 < 1.0f)) != 0ull) ingoing = dot(rd, ro) < 0.0f;
         blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
     }
-    float rho2, qm;
-    const float ds = X.sdf(ro, a.rs, scene_flags, rho2, qm);         // :285
-    // the root guards of the enabled terms (a disabled term's value is discarded; a kernel built for
-    // one flag set drops its arithmetic entirely)
-    if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
-    else if constexpr (SFS == BH_SCENE_DISC) X.sq_arg(rho2);
-    else if constexpr (SFS == BH_SCENE_MARKERS) X.sq_arg(qm);
-    const bool surface = ds < MIN_DIST;                                // :286-288
+    float rho2, yy, qm;
+    X.sdf_args(ro, rho2, yy, qm);                                      // the SDF roots' arguments
+    const float dtr = a.dtm * r;                                       // :307-310's second operand
+    float dt;
+    bool surface = false;
+#if !BH_FAST && BH_SDF_SKIP
+    // Root-free step (BRANCHY): dt = min(0.9 dist, dtm r) needs dist only where it could fall below
+    // dtm r / 0.9, and the surface test only below MIN_DIST.  sdf_skip decides "dt == dtm r, no surface"
+    // from the squared arguments; when it holds on every live lane (blackout lanes leave either way)
+    // the wave skips the three roots, their guards and the distance arithmetic.  Same bits: see sdf_skip.
+    // The photon-sphere argument (:294) is formed before the exits for the test.
     if constexpr (BRANCHY) {
-        if (blackout | surface) {
-            fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
-            return true;
+        const v3 dc = sub(f.cps, ro);
+        const float qps = dot(dc, dc);
+        const bool ok = sdf_skip(a, scene_flags, dtr, rho2, yy, qm, qps) | blackout;
+        if (a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!ok) == 0ull) {
+            BH_DIAG_SKIP_COUNT();
+            if (blackout) {
+                fate = (uint32_t)BH_FATE_BLACKOUT;
+                return true;
+            }
+            dt = dtr;
+        } else {
+            const float ds = X.sdf_from(ro, a.rs, scene_flags, rho2, yy, qm);  // :285
+            if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
+            else if constexpr (SFS == BH_SCENE_DISC) X.sq_arg(rho2);
+            else if constexpr (SFS == BH_SCENE_MARKERS) X.sq_arg(qm);
+            if (blackout | (ds < MIN_DIST)) {                            // :286-288
+                fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+                return true;
+            }
+            const float dps = X.sqrt(qps) - 0.075f;
+            X.sq_arg(qps);
+            const float dist = fminf(ds, dps);                           // :299
+            dt = fminf(dist * 0.9f, dtr);                                // :307-310
         }
+    } else
+#endif
+    {
+        const float ds = X.sdf_from(ro, a.rs, scene_flags, rho2, yy, qm);  // :285
+        // the root guards of the enabled terms (a disabled term's value is discarded; a kernel built for
+        // one flag set drops its arithmetic entirely)
+        if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);
+        else if constexpr (SFS == BH_SCENE_DISC) X.sq_arg(rho2);
+        else if constexpr (SFS == BH_SCENE_MARKERS) X.sq_arg(qm);
+        surface = ds < MIN_DIST;                                           // :286-288
+        if constexpr (BRANCHY) {
+            if (blackout | surface) {
+                fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+                return true;
+            }
+        }
+        // :294 after the exits (measured: 1.5 % faster than before them, A/B r01; neutral without
+        // machine scheduling)
+        const v3 dc = sub(f.cps, ro);
+        const float qps = dot(dc, dc);
+        const float dps = X.sqrt(qps) - 0.075f;
+        X.sq_arg(qps);
+        const float dist = fminf(ds, dps);                                 // :299
+        dt = fminf(dist * 0.9f, dtr);                                      // :307-310
     }
-    // :294 after the exits (measured: 1.5 % faster than before them, A/B r01; neutral without
-    // machine scheduling)
-    const v3 dc = sub(f.cps, ro);
-    const float qps = dot(dc, dc);
-    const float dps = X.sqrt(qps) - 0.075f;
-    X.sq_arg(qps);
-    const float dist = fminf(ds, dps);                                 // :299
-    const float dt = fminf(dist * 0.9f, a.dtm * r);                    // :307-310
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);
     const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r, y1));
@@ -580,7 +667,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
 }
 
 #ifdef BH_DIAG_SLOW
-__device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;
+__device__ uint32_t g_diag_slow_lane_steps, g_diag_slow_wave_steps;  // (g_diag_skip/all_wave_steps above)
 #endif
 
 #ifndef BH_TAIL_PACKED
@@ -742,6 +829,10 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
     return step_bf<true, FOps, SF, UNI>(a, f, in, out, X, fate, it);
 #else
     XOps<true> X;
+#ifdef BH_DIAG_SLOW
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+        atomicAdd(&g_diag_all_wave_steps, 1u);
+#endif
     bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it);
 #ifdef BH_DIAG_SLOW
     const uint64_t badm = __builtin_amdgcn_ballot_w64(X.bad);

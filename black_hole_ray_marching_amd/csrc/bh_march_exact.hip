@@ -65,4 +65,13 @@ extern "C" int bh_diag_slow_counts(uint32_t* lane_steps, uint32_t* wave_steps) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_slow_wave_steps), &z, 4);
     return 0;
 }
+// and the root-free step's counters: wave-steps that skipped the SDF roots, all wave-steps
+extern "C" int bh_diag_skip_counts(uint32_t* skip_wave_steps, uint32_t* all_wave_steps) {
+    uint32_t z = 0;
+    if (hipMemcpyFromSymbol(skip_wave_steps, HIP_SYMBOL(bh::BH_NS::g_diag_skip_wave_steps), 4) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(all_wave_steps, HIP_SYMBOL(bh::BH_NS::g_diag_all_wave_steps), 4) != hipSuccess) return -1;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_skip_wave_steps), &z, 4);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_all_wave_steps), &z, 4);
+    return 0;
+}
 #endif

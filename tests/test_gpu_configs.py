@@ -149,6 +149,8 @@ def _shards_rgbm14(torch, scene, W, H, S, schedule, partition=None):
     stride = max(counts)
     packed = torch.zeros((S * stride, tb), dtype=torch.uint8, device="cuda")
     for k in range(S):
+        if counts[k] == 0:  # a weight-0 rank renders nothing
+            continue
         kw = dict(partition=partition) if partition else {}
         scene.render(packed[k * stride:k * stride + counts[k]], None, fmt=bh.BH_OUT_RGBA16F,
                      layout=bh.BH_LAYOUT_TILES_RGBM14, shard_index=k, shard_count=S, width=W, height=H,

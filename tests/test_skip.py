@@ -1,0 +1,80 @@
+"""The root-free march step (bh_march.hpp, sdf_skip): a lane that passes the test must have dt == dtm*r and
+no surface hit in the full step -- checked here on the step's own float32 arithmetic (numpy: IEEE
+add/mul and correctly rounded sqrt, as the exact mode's cores), with samples packed against the test's
+thresholds and the dt boundary (src/black_hole_maybe.wgsl:285-310)."""
+import numpy as np
+import pytest
+
+f32 = np.float32
+DISC, MARKERS = 1, 2
+
+
+def fma32(a, b, c):
+    return (a.astype(np.float64) * np.float64(b) + np.float64(c)).astype(f32)
+
+
+def predicate(flags, dtr, rho2, yy, qm, qps, rs):
+    T = fma32(dtr, 1.125, f32(0.002))
+    u6 = T + f32(6.0) * rs
+    uy, um, up = T + f32(0.02), T + f32(0.5), T + f32(0.075)
+    disc_ok = (rho2 >= u6 * u6) | (yy >= uy * uy) | (not flags & DISC)
+    mark_ok = (qm >= um * um) | (not flags & MARKERS)
+    return disc_ok & mark_ok & (qps >= up * up)
+
+
+def full_step(flags, dtr, rho2, y, qm, qps, rs):
+    """dt and the surface test of the full step (the exact mode's op sequence)."""
+    rho = np.sqrt(rho2)
+    disc = np.fmax(np.fmax(rho - f32(6.0) * rs, -(rho - f32(3.0) * rs)), np.abs(y) - f32(0.02))
+    m = np.sqrt(qm) - f32(0.5)
+    inf = f32(np.inf)
+    ds = np.fmin(disc if flags & DISC else inf, m if flags & MARKERS else inf)
+    dps = np.sqrt(qps) - f32(0.075)
+    dist = np.fmin(ds, dps)
+    dt = np.fmin(dist * f32(0.9), dtr)
+    return dt, ds < f32(0.001)
+
+
+def samples(rng, n, rs, dtm):
+    r = np.exp(rng.uniform(np.log(1.0), np.log(300.0), n)).astype(f32)
+    dtr = (f32(dtm) * r).astype(f32)
+    T = fma32(dtr, 1.125, f32(0.002))
+    # each distance term sits near its threshold (s ~ 1) or well inside (s ~ 0.5 .. 3)
+    def near(c):
+        s = np.where(rng.random(n) < 0.7, rng.uniform(0.9995, 1.0005, n), rng.uniform(0.5, 3.0, n))
+        return ((T.astype(np.float64) * s + c) ** 2).astype(f32)
+    rho2 = np.where(rng.random(n) < 0.5, near(6.0 * rs), rng.uniform(0, 40, n).astype(f32) ** 2).astype(f32)
+    y = np.sqrt(near(0.02).astype(np.float64)).astype(f32) * np.where(rng.random(n) < 0.5, f32(1), f32(-1))
+    y = np.where(rng.random(n) < 0.3, rng.uniform(-1, 1, n).astype(f32), y).astype(f32)
+    qm, qps = near(0.5), near(0.075)
+    # single-ulp nudges either way around the thresholds
+    for a in (rho2, qm, qps):
+        k = rng.integers(-3, 4, n).astype(np.int32)
+        a.view(np.int32)[:] += k
+    return dtr, rho2, y, qm, qps
+
+
+@pytest.mark.parametrize("flags", [DISC | MARKERS, DISC, MARKERS])
+@pytest.mark.parametrize("rs,dtm", [(1.0, 0.5), (8.0, 0.5), (0.25, 0.01), (1.0, 3.0)])
+def test_skip_implies_dt_equals_dtm_r(flags, rs, dtm):
+    rng = np.random.default_rng(hash((flags, rs, dtm)) & 0xFFFFFFFF)
+    rs = f32(rs)
+    passed = 0
+    for _ in range(6):
+        dtr, rho2, y, qm, qps = samples(rng, 200_000, rs, dtm)
+        ok = predicate(flags, dtr, rho2, (y * y).astype(f32), qm, qps, rs)
+        dt, surface = full_step(flags, dtr, rho2, y, qm, qps, rs)
+        bad = ok & ((dt != dtr) | surface)
+        assert not bad.any(), (dtr[bad][:4], rho2[bad][:4], y[bad][:4], qm[bad][:4], qps[bad][:4])
+        passed += int(ok.sum())
+    assert passed > 100_000  # the samples do exercise the skip
+
+
+def test_skip_rejects_nan_and_passes_infinite_distances():
+    rs = f32(1.0)
+    dtr = np.array([0.5, np.nan, 0.5, 0.5], f32)
+    big = np.array([np.inf, 1e6, np.nan, 1e6], f32)
+    ok = predicate(DISC | MARKERS, dtr, big, big, big, big, rs)
+    assert ok.tolist() == [True, False, False, True]
+    dt, surface = full_step(DISC | MARKERS, dtr[[0]], big[[0]], np.sqrt(big[[0]]), big[[0]], big[[0]], rs)
+    assert dt[0] == dtr[0] and not surface[0]
