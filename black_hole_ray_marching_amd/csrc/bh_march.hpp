@@ -495,28 +495,34 @@ __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps;
 // Does this lane's step have dt == dtm*r (:307-310) and no surface hit (:286-288), whatever its three SDF
 // roots are?  From the step's own rounded values (r = RN(sqrt r2), dtr = RN(dtm r), rho2, y*y, the markers'
 // qm and the photon sphere's qps, all formed exactly as the full step forms them), with no root:
-//   T = RN(1.125 dtr + 0.002);  a distance term d = RN(RN(sqrt v) - c) passes when v >= RN(RN(T + c)^2):
+//   T = RN(1.125 dtr + 0.002);  a distance term d = RN(RN(sqrt v) - c) passes when v >= u*u, u = RN(T + c)
+//   (tested as fma(-u, u, v) >= 0: one rounding, which keeps the sign of the exact difference):
 //   disc (:121)     rho2 >= (T + RN(6 rs))^2  or  y*y >= (T + 0.02)^2   [disc >= RN(rho - 6rs) and
 //                   >= RN(|y| - 0.02): fmaxf is >= each non-NaN operand]
 //   markers         qm  >= (T + 0.5)^2        photon sphere (:294)  qps >= (T + 0.075)^2
 // Proof that a passing lane has dt == dtr and no surface (exact mode: RN sqrt, IEEE ops; dtm > 0 and
 // 0 < rs <= 8, the host's skip_sdf gate, so dtr >= 0 and T >= 0.002 (1 - 2^-24)): u = RN(T + c) >=
-// (T + c)(1 - 2^-24) and RN(u^2) >= u^2 (1 - 2^-24), so sqrt v >= (T + c)(1 - 2^-24)^1.5 (for y*y = RN(y^2)
-// one more factor) and RN(sqrt v) >= (T + c)(1 - 2^-22); d >= RN(T - (T + c) 2^-22) >= T (1 - 2^-17.6)
+// (T + c)(1 - 2^-24), so sqrt v >= (T + c)(1 - 2^-24) (for y*y = RN(y^2) one more factor) and
+// RN(sqrt v) >= (T + c)(1 - 2^-22); d >= RN(T - (T + c) 2^-22) >= T (1 - 2^-17.6)
 // (c <= 48.0001, T >= 0.00199).  So dist = min of the enabled terms >= that bound >= 0.00199 > MIN_DIST
 // (no surface), and 0.9f d >= (0.9f * 1.125) dtr (1 - 2^-17.5) = 1.0125 dtr (1 - 2^-17.5) > dtr, so
-// RN(0.9f dist) >= dtr (dtr is a float) and fminf(RN(dist * 0.9), dtr) == dtr.  NaN fails every test;
-// an infinite threshold passes only an infinite argument, whose distance is +inf as the full step's.
+// RN(0.9f dist) >= dtr (dtr is a float) and fminf(RN(dist * 0.9), dtr) == dtr.  The terms combine with
+// the step's own fmaxf / fminf, so a NaN term is dropped exactly where the step drops that distance (a NaN
+// argument makes the step's term NaN too); a NaN T (r or dtr NaN) makes every term NaN and the slack NaN,
+// which fails; T = +inf gives -inf (finite v) or NaN (v = +inf) terms, which fail or are dropped.
 // In the exact build's core pass a wrong r (r2 outside the root core's domain) also raises the k1
 // division guard, so that step re-runs in IEEE ops, where the proof holds as written.
 // tests/test_skip.py checks the implication on adversarial samples of the step's float32 arithmetic.
-__device__ __forceinline__ bool sdf_skip(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
-                                         float qm, float qps) {
+__device__ __forceinline__ float sdf_skip_slack(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
+                                                float qm, float qps) {
     const float T = __builtin_fmaf(dtr, 1.125f, 0.002f);
     const float u6 = T + 6.0f * a.rs, uy = T + 0.02f, um = T + 0.5f, up = T + 0.075f;
-    const bool disc_ok = !(flags & BH_SCENE_DISC) | (rho2 >= u6 * u6) | (yy >= uy * uy);
-    const bool mark_ok = !(flags & BH_SCENE_MARKERS) | (qm >= um * um);
-    return disc_ok & mark_ok & (qps >= up * up);
+    // v - u^2 rounded once (fma): its sign is the sign of the exact v - u*u
+    float disc = fmaxf(__builtin_fmaf(-u6, u6, rho2), __builtin_fmaf(-uy, uy, yy));
+    float mark = __builtin_fmaf(-um, um, qm);
+    if (!(flags & BH_SCENE_DISC)) disc = __builtin_inff();
+    if (!(flags & BH_SCENE_MARKERS)) mark = __builtin_inff();
+    return fminf(fminf(disc, mark), __builtin_fmaf(-up, up, qps));
 }
 #endif
 
@@ -570,8 +576,13 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     if constexpr (BRANCHY) {
         const v3 dc = sub(f.cps, ro);
         const float qps = dot(dc, dc);
-        const bool ok = sdf_skip(a, scene_flags, dtr, rho2, yy, qm, qps) | blackout;
-        if (a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!ok) == 0ull) {
+        // lanes that need the roots: slack < 0 or NaN (llvm.amdgcn.fcmp ULT: the lane mask straight from the
+        // compare, no i1 round trip through a VGPR), minus the lanes that leave by the blackout exit
+        const float slack = sdf_skip_slack(a, scene_flags, dtr, rho2, yy, qm, qps);
+        uint64_t need = __builtin_amdgcn_fcmpf(slack, 0.0f, 12 /* FCMP_ULT */);
+        if constexpr (CO) need &= bo_on ? ~__builtin_amdgcn_fcmpf(r2, R2_GT1, 13 /* FCMP_ULE */) : ~0ull;
+        else need &= ~__builtin_amdgcn_ballot_w64(blackout);
+        if (a.skip_sdf != 0u && need == 0ull) {
             BH_DIAG_SKIP_COUNT();
             if (blackout) {
                 fate = (uint32_t)BH_FATE_BLACKOUT;

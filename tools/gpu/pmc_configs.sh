@@ -19,6 +19,9 @@ CFG[c3B]="--camera B"
 CFG[c5]="--max-iters 1000 --camera C"
 CFG[c3A_D1]="--frames-per-launch 1"
 CFG[c5_D1]="--max-iters 1000 --camera C --frames-per-launch 1"
+# config 1's per-wave fixed cost: the same frame at cap 1 and 2 (VALU per wave = fixed + steps x per-step)
+CFG[c1cap1]="--width 256 --height 256 --max-iters 1 --surfaces off"
+CFG[c1cap2]="--width 256 --height 256 --max-iters 2 --surfaces off"
 LIST="${@:-c1 c2 c3A c3B c5 c3A_D1 c5_D1}"
 for C in $LIST; do
   OUT=$ROOT/gpurun_out/pmc_$TAG/$C

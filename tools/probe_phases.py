@@ -5,7 +5,9 @@ The clock-probed waves (one in `stride`) add the shader cycles of five phases to
 accumulator (bh_march.hpp, BH_DIAG_PHASES): tables staged, tile + pixel ray, march, shading + store,
 cost bookkeeping.  Prints the mean cycles per sampled wave and each phase's share of the lifetime, for
 the headline workload (4096x2048, cap 512, camera A, 32 frames per launch, RGBA16F, two targets).
-    BH_LIB=tools/variants/phases.so python tools/probe_phases.py [--launches 20]"""
+    BH_LIB=tools/variants/phases.so python tools/probe_phases.py [--launches 20]
+config 1 (256x256, cap 64, no surfaces, 256 frames per launch):
+    ... tools/probe_phases.py --width 256 --height 256 --cap 64 --frames 256 --no-surfaces --stride 4"""
 import argparse
 import json
 import sys
@@ -25,9 +27,11 @@ p.add_argument("--cap", type=int, default=512)
 p.add_argument("--frames", type=int, default=32)
 p.add_argument("--launches", type=int, default=20)
 p.add_argument("--stride", type=int, default=64)
+p.add_argument("--no-surfaces", action="store_true", help="scene_flags 0 (BASELINE config 1's scene)")
 args = p.parse_args()
 W, H, D = args.width, args.height, args.frames
-scene = bh.Scene(W, H, sky=bh.synthetic_sky(4096, 2048), max_iters=args.cap, math=bh.BH_MATH_EXACT)
+scene = bh.Scene(W, H, sky=bh.synthetic_sky(4096, 2048), max_iters=args.cap, math=bh.BH_MATH_EXACT,
+                 **(dict(scene_flags=0) if args.no_surfaces else {}))
 cols = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(D)]
 bos = [torch.empty((H, W, 4), dtype=torch.float16, device="cuda") for _ in range(D)]
 batch = scene.prepare_frames(cols, bos, fmt=bh.BH_OUT_RGBA16F)
