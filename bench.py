@@ -103,6 +103,8 @@ def parse(argv=None):
                         "own tiles cross no link): 'calibrate' (default: the fastest of a few candidates, measured "
                         "before the warm-up), 'auto' (multigpu.auto_root_ratio) or a number; 1 = the plain "
                         "(tx + 3ty) %% N interleave")
+    p.add_argument("--unpack-priority", choices=["high", "normal"], default="high",
+                   help="N>1: the priority of rank 0's unpack stream (high: overlaps the next batch's render)")
     p.add_argument("--transport", choices=["auto", "rgbm", "rgbm14"], default="auto",
                    help="N>1 shard layout: BH_LAYOUT_TILES_RGBM (6.125 B/pixel of RGBA16F) or BH_LAYOUT_TILES_RGBM14 "
                         "(5.375: the fp16 channels in [0, 1] take 14 bits); auto = rgbm14 for rgba16f")
@@ -415,7 +417,9 @@ def main() -> int:
         tb = bh.tile_bytes(layout, fmt)
         frame_cols = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
         frame_bos = [torch.empty((H, W, 4), dtype=ch_dtype, device=dev) for _ in range(D)] if rank == 0 else None
-        side = torch.cuda.Stream(dev)
+        # rank 0's unpack stream: high priority so that its workgroups take CU slots as the next batch's
+        # render waves retire instead of queueing behind the whole render
+        side = torch.cuda.Stream(dev, priority=-1 if args.unpack_priority == "high" else 0)
 
         class Rig:
             """The N>1 data path for one tile partition: each rank renders its share of the batch's D
@@ -460,7 +464,7 @@ def main() -> int:
             # rank 0's share, measured: the batch time of a few candidate partitions --
             # rank 0 renders less when its unpack binds, more when the xGMI ingress of the others' shards
             # binds (its own tiles cross no link) -- untimed, before the warm-up; every rank takes rank 0's pick
-            ratios = sorted({round(multigpu.auto_root_ratio(n), 3), 0.9, 1.0, 1.15, 1.3})
+            ratios = sorted({round(multigpu.auto_root_ratio(n), 3), 0.4, 0.55, 0.7, 0.85, 1.0, 1.15, 1.3})
             ms = []
             for r in ratios:
                 rig = Rig(multigpu.root_weights(n, r) if r != 1.0 else None)
@@ -771,7 +775,7 @@ def main() -> int:
             result["world_size"] = dist.get_world_size()
             result["backend"] = dist.get_backend()
             result["transport"] = {"layout": "rgbm14" if p14 else "rgbm", "tile_bytes": tb,
-                                   "bytes_per_pixel": round(tb / 64.0, 4)}
+                                   "bytes_per_pixel": round(tb / 64.0, 4), "unpack_priority": args.unpack_priority}
             result["per_rank_s"] = [round(x, 6) for x in per_rank]
             result["ranks"] = ranks
             result["partition_calibration"] = calibration

@@ -75,10 +75,12 @@ def root_weights(n: int, root_ratio: float, unit: int = 20) -> list[int]:
 
 
 def auto_root_ratio(n: int) -> float:
-    """Rank 0's share relative to the others' when it also unpacks both targets of every frame: its
-    unpack costs it ~2.5 % x N of a shard's render time (measured 4 / 7 / 15 % at
-    N = 2 / 4 / 8 on the 4096x2048 frame, 23 % for 8192x4096 at N = 8)."""
-    return max(0.0, 1.0 - 0.025 * n)
+    """Rank 0's share relative to the others' when it also unpacks both targets of every frame: the
+    unpack is a fixed ~0.035 ms per 4096x2048 frame (RGBM14, HBM-bound; tools/probe_rank0.py, DESIGN.md
+    §7) while a shard renders in ~0.56 / N ms, so rank 0 balances at r = 1 - U N / R ~ 1 - 0.065 N
+    (0.87 / 0.74 / 0.48 at N = 2 / 4 / 8).  bench.py's calibration measures the real optimum on the node,
+    where rank 0's xGMI ingress (smaller for a larger share) also counts."""
+    return max(0.0, 1.0 - 0.065 * n)
 
 
 def shard_tile_index(tx: int, ty: int, width: int, height: int, S: int) -> tuple[int, int]:

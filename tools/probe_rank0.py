@@ -25,6 +25,7 @@ def main():
     p.add_argument("--root-ratio", default="1", help="comma list: numbers or 'auto'")
     p.add_argument("--it", type=int, default=12)
     p.add_argument("--transport", choices=["rgbm", "rgbm14"], default="rgbm14")
+    p.add_argument("--side-priority", default="0", help="comma list: the unpack stream's priority (0 normal, -1 high)")
     a = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
@@ -45,7 +46,7 @@ def main():
             counts = part.counts if part else [bh.shard_tile_count(W, H, k, n) for k in range(n)]
             stride = max(counts)
             kw = dict(layout=layout, shard_count=n, **({"partition": part} if part else {}))
-            for rows in (int(r) for r in a.rows.split(",")):
+            for rows, sp in ((int(r), int(q)) for r in a.rows.split(",") for q in a.side_priority.split(",")):
                 scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
                 bufs = [torch.empty((D * stride, tb), dtype=torch.uint8, device=dev) for _ in range(2)]
                 for k in (0, 1):  # the gathered launch: rank 0's and rank 1's blocks rendered for real
@@ -55,7 +56,7 @@ def main():
                 cols = [torch.empty((H, W, 4), dtype=torch.float16, device=dev) for _ in range(D)]
                 bos = [torch.empty_like(c) for c in cols]
                 rs = torch.cuda.current_stream()
-                ss = torch.cuda.Stream()
+                ss = torch.cuda.Stream(priority=sp)
 
                 def render(k):
                     scene.render_frames([bufs[k][f * stride:f * stride + counts[k]] for f in range(D)], None, fmt=fmt,
@@ -90,7 +91,7 @@ def main():
                 r0 = run(a.it, 0, True, True)
                 r1 = run(a.it, 1, True, False)
                 out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
-                       "transport": a.transport, "tile_bytes": tb,
+                       "transport": a.transport, "tile_bytes": tb, "side_priority": sp,
                        "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": counts[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),

@@ -13,7 +13,10 @@ s0 = rank 0's tile share (its tiles cross no link); frame_bytes = tiles * tile_b
 link's rate in one direction (MI355X: 7 links of 153.6 GB/s bidirectional, 76.8 per direction; RCCL's
 achieved share of it is the model's unknown, `--link-eff`).
 
-    python tools/scale_model.py probe.jsonl --one-gpu-ms 0.556 [--k 20] [--link-gbps 76.8] [--link-eff 1.0]"""
+    python tools/scale_model.py probe.jsonl --one-gpu-ms 0.556 [--k 20] [--link-gbps 76.8] [--link-eff 1.0]
+--rebalance: per (N, D, transport) also the best rank-0 share on the grid unit 20 (weights [w0, 20, ...]):
+rank 0's and another rank's render scale with their tile counts (per-tile rates from the probe row),
+rank 0 adds the unpack, and the ingress shrinks with rank 0's share."""
 import argparse
 import json
 
@@ -25,6 +28,7 @@ def main():
     p.add_argument("--k", type=int, default=20)
     p.add_argument("--link-gbps", type=float, default=76.8)
     p.add_argument("--link-eff", type=float, default=1.0)
+    p.add_argument("--rebalance", action="store_true")
     a = p.parse_args()
     rows = [json.loads(x) for x in open(a.probe) if x.startswith("{")]
     print(f"one GPU {a.one_gpu_ms} ms/frame, K = {a.k}, link {a.link_gbps} GB/s x {a.link_eff} per direction")
@@ -44,6 +48,26 @@ def main():
         print(f"| {n} | {r['frames_per_launch']} | {r.get('transport', 'rgbm')} | {w if r.get('weights') else 'even'} | "
               f"{render:.4f} | {ingress:.4f} | {'render' if render >= ingress else 'xGMI'} | {pred:.4f} | "
               f"{W * H / pred / 1e6:.1f} | {a.one_gpu_ms / pred:.2f}x |")
+        if a.rebalance and r.get("tiles"):
+            t0, t1 = r["tiles"]
+            a0 = r["rank0_render_ms"] / t0
+            a1 = r["rank1_render_ms"] / t1
+            U = r["rank0_render_plus_unpack_ms"] - r["rank0_render_ms"]
+            best = None
+            for w0 in range(0, 41):
+                tot = w0 + 20 * (n - 1)
+                s0n = w0 / tot
+                r0 = a0 * tiles * s0n + U
+                r1 = a1 * tiles * 20 / tot
+                ing = (1.0 - s0n) * frame_bytes / ((n - 1) * a.link_gbps * a.link_eff * 1e9) * 1e3
+                st = max(r0, r1, ing)
+                pr = st + (ing + r["unpack_only_ms"]) / a.k
+                if best is None or pr < best[0]:
+                    best = (pr, w0, r0, r1, ing)
+            pr, w0, r0, r1, ing = best
+            bind = "rank 0" if r0 >= max(r1, ing) else ("render" if r1 >= ing else "xGMI")
+            print(f"| {n} | {r['frames_per_launch']} | {r.get('transport', 'rgbm')} | rebalanced [{w0}, 20, ...] | "
+                  f"{max(r0, r1):.4f} | {ing:.4f} | {bind} | {pr:.4f} | {W * H / pr / 1e6:.1f} | {a.one_gpu_ms / pr:.2f}x |")
 
 
 if __name__ == "__main__":
