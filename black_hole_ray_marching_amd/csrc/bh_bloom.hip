@@ -850,22 +850,27 @@ __global__ void BLOOM_BOUNDS bloom_y_kernel(Tables tb, CTex X, uint32_t point, T
 // four pixels (14 LDS reads per pixel instead of 21 at 4096x2048), each pixel reduced exactly as
 // up8(PlanSrc) does.  HX / HY: the tap's half flags.
 constexpr int FP_YQ = 40;  // 32 + the taps' reach (38 at 4096x2048)
-// The tile's row stride in float4: odd.  The quad loops' ds_read_b128 lane groups ({0-3, 12-15, 20-27},
-// {4-11, 16-19, 28-31}, ...) take two quad rows each, and lane l reads texel column 2 (l & 15) + c: the
-// even 4-bank slots of one quad row, and with an even stride (40) the same slots in the next row -- 2-way
-// conflicts (rocprofv3: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.34).  An odd stride puts the next row
-// on the odd slots.
+// The tile's layout: entry (ly, lx) at ly * FS_YQ + lx + ((ly + p) >> 1), p = lo_y & 1 -- every second row
+// pair shifted by one float4.  The quad loops' ds_read_b128 lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19,
+// 28-31}, ...: 16 lanes, one pass over the 64 banks) take two quad rows each, and a lane reads at quad
+// column 2 (l & 15) -- only the even 4-bank slots of its quad row.  Without the shift the next quad row (two
+// texel rows down) lands on the even slots too, whatever the row stride: 2-way conflicts (rocprofv3:
+// SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.34 at strides 40 and 41).  With it a quad row is 2 FS_YQ + 1
+// float4 further, odd: the next quad row reads the odd slots.  (p makes the quad's first texel row even in
+// the shifted index, so a tap's row offsets are launch constants: yq_rowoff(d) = d FS_YQ + floor(d / 2).)
 #ifndef BH_BLOOM_FS_YQ
-#define BH_BLOOM_FS_YQ 41
+#define BH_BLOOM_FS_YQ 40
 #endif
 constexpr int FS_YQ = BH_BLOOM_FS_YQ;
+__host__ __device__ constexpr int32_t yq_rowoff(int32_t d) { return d * FS_YQ + (d >= 0 ? d / 2 : -((1 - d) / 2)); }
 template <int HX, int HY>
-__device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2]) {
+__device__ __forceinline__ void yquad_tap(const float4* T, int32_t d1, int i, F4 (&s)[2][2]) {
+    // T: the tap's first texel; the rows below it are d1 (FS_YQ or FS_YQ + 1) and 2 FS_YQ + 1 further
     float4 t[2 + HY][2 + HX];
 #pragma unroll
     for (int r = 0; r < 2 + HY; ++r)
 #pragma unroll
-        for (int c = 0; c < 2 + HX; ++c) t[r][c] = T[r * FS_YQ + c];
+        for (int c = 0; c < 2 + HX; ++c) t[r][c] = T[(r == 0 ? 0 : r == 1 ? d1 : 2 * FS_YQ + 1) + c];
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -885,9 +890,10 @@ __device__ __forceinline__ void yquad_tap(const float4* T, int i, F4 (&s)[2][2])
 template <int STD>
 __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y) {
     __shared__ Lds L;
-    __shared__ float4 tile[FP_YQ * FS_YQ];
+    __shared__ float4 tile[FP_YQ * FS_YQ + FP_YQ / 2 + 1];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const int32_t x0 = (int32_t)bx + P.lo_x, y0 = (int32_t)by + P.lo_y;  // the footprint, clamp-to-edge
+    const int32_t p = P.lo_y & 1;  // the row-pair shift's phase (see FS_YQ)
     {
         const int32_t nx = P.hi_x - P.lo_x + 32, ny = P.hi_y - P.lo_y + 32;
         const int32_t wm = (int32_t)X.w - 1, hm = (int32_t)X.h - 1;
@@ -904,14 +910,15 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
             if (ly < ny) {
                 const F4 d = dec(L, raw[r]);
-                tile[ly * FS_YQ + lx] = make_float4(d.r, d.g, d.b, d.a);
+                tile[ly * FS_YQ + lx + ((ly + p) >> 1)] = make_float4(d.r, d.g, d.b, d.a);
             }
         }
     }
     __syncthreads();
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
     if (x >= Y.w || y >= Y.h) return;
-    const int32_t base = ((int32_t)y - y0) * FS_YQ + ((int32_t)x - x0);
+    const int32_t m = (int32_t)y - y0;  // m + p is even
+    const int32_t base = m * FS_YQ + ((m + p) >> 1) + ((int32_t)x - x0);
     F4 s[2][2];
     // Y = X + 0.5 q(blur1 / 12) per pixel of the quad; both pixels of each quad row in one 8-byte store:
     // inside the frame, and rows 8-byte aligned (even width; x is even); else one word per pixel
@@ -923,7 +930,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
 #pragma unroll
             for (int a = 0; a < 2; ++a) {
                 const F4 b1 = quant(L, div12(s[b][a]));
-                const float4 v = tile[base + b * FS_YQ + a];  // the pixel's own texel
+                const float4 v = tile[base + b * FS_YQ + a];  // the pixel's own texel (row m + b, b < 2: no shift)
                 c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
             }
             if (full) {
@@ -939,12 +946,14 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
         // the standard plan: constant offsets and halves, one tap at a time (see quad_taps_std)
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const float4* T = tile + (base + fdiv8(STD * tap_m(1, i)) * FS_YQ + fdiv8(STD * tap_m(0, i)));
+            const int32_t dy = fdiv8(STD * tap_m(1, i));
+            const float4* T = tile + (base + yq_rowoff(dy) + fdiv8(STD * tap_m(0, i)));
+            const int32_t d1 = yq_rowoff(dy + 1) - yq_rowoff(dy);
             switch ((fmod8(STD * tap_m(0, i)) == 4 ? 1 : 0) | (fmod8(STD * tap_m(1, i)) == 4 ? 2 : 0)) {
-                case 0: yquad_tap<0, 0>(T, i, s); break;
-                case 1: yquad_tap<1, 0>(T, i, s); break;
-                case 2: yquad_tap<0, 1>(T, i, s); break;
-                default: yquad_tap<1, 1>(T, i, s); break;
+                case 0: yquad_tap<0, 0>(T, d1, i, s); break;
+                case 1: yquad_tap<1, 0>(T, d1, i, s); break;
+                case 2: yquad_tap<0, 1>(T, d1, i, s); break;
+                default: yquad_tap<1, 1>(T, d1, i, s); break;
             }
             pin(s);
             __builtin_amdgcn_sched_barrier(0);
@@ -953,12 +962,13 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     } else {
 #pragma unroll 1
         for (int i = 0; i < 8; i++) {
-            const float4* T = tile + (base + P.oy[i] * FS_YQ + P.ox[i]);
+            const float4* T = tile + (base + yq_rowoff(P.oy[i]) + P.ox[i]);
+            const int32_t d1 = FS_YQ + (P.oy[i] & 1);  // yq_rowoff(oy + 1) - yq_rowoff(oy)
             switch (((P.hx >> i) & 1u) | ((P.hy >> i) & 1u) << 1) {  // launch-uniform
-                case 0: yquad_tap<0, 0>(T, i, s); break;
-                case 1: yquad_tap<1, 0>(T, i, s); break;
-                case 2: yquad_tap<0, 1>(T, i, s); break;
-                default: yquad_tap<1, 1>(T, i, s); break;
+                case 0: yquad_tap<0, 0>(T, d1, i, s); break;
+                case 1: yquad_tap<1, 0>(T, d1, i, s); break;
+                case 2: yquad_tap<0, 1>(T, d1, i, s); break;
+                default: yquad_tap<1, 1>(T, d1, i, s); break;
             }
         }
         finish();

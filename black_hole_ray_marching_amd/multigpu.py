@@ -76,11 +76,12 @@ def root_weights(n: int, root_ratio: float, unit: int = 20) -> list[int]:
 
 def auto_root_ratio(n: int) -> float:
     """Rank 0's share relative to the others' when it also unpacks both targets of every frame: the
-    unpack is a fixed ~0.035 ms per 4096x2048 frame (RGBM14, HBM-bound; tools/probe_rank0.py, DESIGN.md
-    §7) while a shard renders in ~0.56 / N ms, so rank 0 balances at r = 1 - U N / R ~ 1 - 0.065 N
-    (0.87 / 0.74 / 0.48 at N = 2 / 4 / 8).  bench.py's calibration measures the real optimum on the node,
-    where rank 0's xGMI ingress (smaller for a larger share) also counts."""
-    return max(0.0, 1.0 - 0.065 * n)
+    unpack is a fixed ~0.034 ms per 4096x2048 frame (RGBM14, HBM-bound, and it does not overlap the next
+    batch's render even from a high-priority stream) while a tile renders in ~4.5 ns (tools/probe_rank0.py,
+    profiles/r04/n_gt_1/): balance at (20 - w0) / (w0 + 20 (N - 1)) = U / R, i.e. r ~ 1 - 0.054 N (0.89 /
+    0.78 / 0.57 at N = 2 / 4 / 8).  bench.py's calibration measures the real optimum on the node, where
+    rank 0's xGMI ingress (smaller for a larger share) also counts."""
+    return max(0.0, 1.0 - 0.054 * n)
 
 
 def shard_tile_index(tx: int, ty: int, width: int, height: int, S: int) -> tuple[int, int]:

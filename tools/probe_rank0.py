@@ -49,10 +49,11 @@ def main():
             for rows, sp in ((int(r), int(q)) for r in a.rows.split(",") for q in a.side_priority.split(",")):
                 scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
                 bufs = [torch.empty((D * stride, tb), dtype=torch.uint8, device=dev) for _ in range(2)]
-                for k in (0, 1):  # the gathered launch: rank 0's and rank 1's blocks rendered for real
+                K1 = 1 if n > 1 else 0  # n = 1: the whole frame in the packed layout (rank 1 := rank 0)
+                for k in sorted({0, K1}):  # the gathered launch: rank 0's and rank 1's blocks rendered for real
                     scene.render_frames([bufs[k][f * stride:f * stride + counts[k]] for f in range(D)], None, fmt=fmt,
                                         shard_index=k, **kw)
-                gathered = torch.cat([bufs[0], bufs[1]] + [bufs[1]] * (n - 2), 0)
+                gathered = torch.cat([bufs[0], bufs[1]] + [bufs[1]] * (n - 2), 0) if n > 1 else bufs[0]
                 cols = [torch.empty((H, W, 4), dtype=torch.float16, device=dev) for _ in range(D)]
                 bos = [torch.empty_like(c) for c in cols]
                 rs = torch.cuda.current_stream()
@@ -87,12 +88,12 @@ def main():
 
                 for _ in range(3):
                     run(4, 0, True, True)
-                    run(2, 1, True, False)
+                    run(2, K1, True, False)
                 r0 = run(a.it, 0, True, True)
-                r1 = run(a.it, 1, True, False)
+                r1 = run(a.it, K1, True, False)
                 out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
                        "transport": a.transport, "tile_bytes": tb, "side_priority": sp,
-                       "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": counts[:2],
+                       "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": (counts + counts)[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),
                        "predicted_frame_ms": round(max(r0, r1), 4)}
