@@ -26,6 +26,7 @@ def main():
     p.add_argument("--it", type=int, default=12)
     p.add_argument("--transport", choices=["rgbm", "rgbm14"], default="rgbm14")
     p.add_argument("--side-priority", default="0", help="comma list: the unpack stream's priority (0 normal, -1 high)")
+    p.add_argument("--render-streams", type=int, default=1, help="launches alternate over this many streams")
     a = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
@@ -58,10 +59,17 @@ def main():
                 bos = [torch.empty_like(c) for c in cols]
                 rs = torch.cuda.current_stream()
                 ss = torch.cuda.Stream(priority=sp)
+                rss = [rs] + [torch.cuda.Stream() for _ in range(a.render_streams - 1)]
+                nl = [0]
 
                 def render(k):
+                    # with several render streams consecutive launches alternate, so that one launch's last
+                    # waves overlap the next launch's first (each stream has its own learned order)
+                    st = rss[nl[0] % len(rss)]
+                    nl[0] += 1
                     scene.render_frames([bufs[k][f * stride:f * stride + counts[k]] for f in range(D)], None, fmt=fmt,
-                                        shard_index=k, stream=rs, **kw)
+                                        shard_index=k, stream=st, **kw)
+                    return st
 
                 def unpack():
                     for f in range(D):
@@ -76,11 +84,10 @@ def main():
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
                     for _ in range(k):
-                        if do_render:
-                            render(shard)
+                        st = render(shard) if do_render else rs
                         if do_unpack:
                             ev = torch.cuda.Event()
-                            ev.record(rs)
+                            ev.record(st)
                             ss.wait_event(ev)  # the bench's side stream waits for the receive
                             unpack()           # renders never wait for it (double-buffered receive)
                     torch.cuda.synchronize()
@@ -92,7 +99,7 @@ def main():
                 r0 = run(a.it, 0, True, True)
                 r1 = run(a.it, K1, True, False)
                 out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
-                       "transport": a.transport, "tile_bytes": tb, "side_priority": sp,
+                       "transport": a.transport, "tile_bytes": tb, "side_priority": sp, "render_streams": a.render_streams,
                        "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": (counts + counts)[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),
