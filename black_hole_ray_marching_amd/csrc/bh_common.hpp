@@ -36,6 +36,7 @@ struct MarchArgs {
     float rs, dtm, max_dist, dp;
     uint32_t blackout_eh;
     uint32_t skip_sdf;         // the root-free step may run (bh_march.hpp, sdf_skip: dtm > 0, 0 < rs <= 8)
+    float far_r2;              // r^2 beyond which a step needs no SDF argument (bh_host.cpp sdf_far_r2; +inf: off)
     // frame
     uint32_t width, height, max_iters, scene_flags;
     uint32_t format, layout;

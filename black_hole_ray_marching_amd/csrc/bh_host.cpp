@@ -1092,6 +1092,27 @@ int bh_render(bh_ctx* c, const bh_camera_uniform* cam, const bh_uniforms* U, con
     return bh_render_frames(c, 1u, cam, U, d, stream);
 }
 
+// The far-field radius of the root-free step (bh_march.hpp): r^2 beyond which every SDF term of a step
+// provably exceeds the root-free test's threshold T = RN(1.125 RN(dtm r) + 0.002) <= 1.1251 dtm R + 0.003
+// (R = |p| exact; the roundings of r, dtm r and T are within 2^-21 of R).  For a point at distance R:
+//   disc (:121)  >= R / sqrt2 - max(6 rs, 0.02)   (rho^2 + y^2 = R^2: rho or |y| is >= R / sqrt2, and the
+//                                                 sdf is >= rho - 6 rs and >= |y| - 0.02)
+//   markers      >= R - 10 sqrt2 - 0.5            (the four centres lie at 10 sqrt2 from the origin)
+//   photon (:294) >= R - 1.5 rs - 0.075           (its centre lies at 1.5 rs)
+// R0 = the largest R at which one of them meets 1.1251 dtm R + 0.003; beyond 1.01 R0 each exceeds the
+// threshold by >= 0.01 R0 (0.7071 - 1.1251 dtm) > 0.001 absolute, far above the step's own rounding of
+// those terms (relative 2^-21: a few 1e-5 at R ~ 40), so the computed distance exceeds T and the root-free
+// test's chain gives dt == dtm r and no surface.  r^2 is compared as computed (within 2^-22 of R^2: inside
+// the 1 % margin).  +inf (off) when dtm is too large for the disc bound to ever clear (dtm >= 0.62).
+static float sdf_far_r2(float rs, float dtm) {
+    const double k = 1.1251 * (double)dtm, a1 = std::sqrt(0.5) - k, a2 = 1.0 - k;
+    if (!(a1 > 0.01) || !(rs > 0.0f)) return INFINITY;
+    const double R0 = std::max({(std::max(6.0 * rs, 0.02) + 0.003) / a1, (10.0 * std::sqrt(2.0) + 0.5 + 0.003) / a2,
+                                (1.5 * rs + 0.075 + 0.003) / a2});
+    const double R = 1.01 * R0;
+    return std::nextafter((float)(R * R), INFINITY);
+}
+
 // A/B switch (diagnostics): BH_NO_SDF_SKIP set => every step evaluates its SDF roots (bh_march.hpp, sdf_skip)
 static bool sdf_skip_disabled() {
     static const bool off = std::getenv("BH_NO_SDF_SKIP") != nullptr;
@@ -1137,6 +1158,7 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     a.rs = U->rs; a.dtm = U->delta_time_mult; a.max_dist = U->max_dist; a.dp = U->distortion_power;
     a.blackout_eh = U->blackout_eh;
     a.skip_sdf = (U->delta_time_mult > 0.0f && U->rs > 0.0f && U->rs <= 8.0f && !sdf_skip_disabled()) ? 1u : 0u;
+    a.far_r2 = a.skip_sdf ? sdf_far_r2(U->rs, U->delta_time_mult) : INFINITY;
     a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
     a.format = d->format; a.layout = d->layout;
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;

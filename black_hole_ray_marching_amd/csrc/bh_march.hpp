@@ -480,15 +480,21 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 #define BH_SDF_SKIP 1
 #endif
 #ifdef BH_DIAG_SLOW
-__device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps;
+__device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wave_steps;
 // one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
 #define BH_DIAG_SKIP_COUNT()                                                                              \
     do {                                                                                                  \
         if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))          \
             atomicAdd(&g_diag_skip_wave_steps, 1u);                                                       \
     } while (0)
+#define BH_DIAG_FAR_COUNT()                                                                               \
+    do {                                                                                                  \
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))          \
+            atomicAdd(&g_diag_far_wave_steps, 1u);                                                        \
+    } while (0)
 #else
 #define BH_DIAG_SKIP_COUNT() do {} while (0)
+#define BH_DIAG_FAR_COUNT() do {} while (0)
 #endif
 
 #if !BH_FAST
@@ -563,10 +569,26 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         blackout = bo_on & (((r2 < 1.0f) & ingoing) | (not_out & (in.outside != 0u)));
     }
     float rho2, yy, qm;
-    X.sdf_args(ro, rho2, yy, qm);                                      // the SDF roots' arguments
     const float dtr = a.dtm * r;                                       // :307-310's second operand
     float dt;
     bool surface = false;
+#if !BH_FAST && BH_SDF_SKIP
+    // Far field: a lane with a.far_r2 <= r^2 <= FLT_MAX (the host's sdf_far_r2, +inf when off) is so far
+    // from the disc, the markers and the photon sphere that every distance term exceeds the root-free
+    // test's threshold by construction (proof at sdf_far_r2, bh_host.cpp): when every lane that stays is
+    // there, the wave forms no SDF argument at all.  (r^2 = +inf is excluded: there dtm r is +inf while a
+    // distance term may stay finite.)
+    if (BRANCHY && __builtin_amdgcn_ballot_w64(!(r2 >= a.far_r2 && r2 <= 0x1.fffffep127f) & !blackout) == 0ull) {
+        BH_DIAG_FAR_COUNT();
+        if (blackout) {
+            fate = (uint32_t)BH_FATE_BLACKOUT;
+            return true;
+        }
+        dt = dtr;
+    } else
+#endif
+    {
+    X.sdf_args(ro, rho2, yy, qm);                                      // the SDF roots' arguments
 #if !BH_FAST && BH_SDF_SKIP
     // Root-free step (BRANCHY): dt = min(0.9 dist, dtm r) needs dist only where it could fall below
     // dtm r / 0.9, and the surface test only below MIN_DIST.  sdf_skip decides "dt == dtm r, no surface"
@@ -626,6 +648,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         X.sq_arg(qps);
         const float dist = fminf(ds, dps);                                 // :299
         dt = fminf(dist * 0.9f, dtr);                                      // :307-310
+    }
     }
     // get_delta_photon_rk4 (:134-151)
     const v3 ro_k1 = smul(dt, rd);

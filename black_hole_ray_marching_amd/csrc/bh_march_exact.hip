@@ -65,7 +65,14 @@ extern "C" int bh_diag_slow_counts(uint32_t* lane_steps, uint32_t* wave_steps) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_slow_wave_steps), &z, 4);
     return 0;
 }
-// and the root-free step's counters: wave-steps that skipped the SDF roots, all wave-steps
+// and the root-free step's counters: wave-steps that skipped the SDF roots (far field included), all
+// wave-steps, far-field wave-steps
+extern "C" int bh_diag_far_count(uint32_t* far_wave_steps) {
+    uint32_t z = 0;
+    if (hipMemcpyFromSymbol(far_wave_steps, HIP_SYMBOL(bh::BH_NS::g_diag_far_wave_steps), 4) != hipSuccess) return -1;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(bh::BH_NS::g_diag_far_wave_steps), &z, 4);
+    return 0;
+}
 extern "C" int bh_diag_skip_counts(uint32_t* skip_wave_steps, uint32_t* all_wave_steps) {
     uint32_t z = 0;
     if (hipMemcpyFromSymbol(skip_wave_steps, HIP_SYMBOL(bh::BH_NS::g_diag_skip_wave_steps), 4) != hipSuccess) return -1;

@@ -86,3 +86,63 @@ def test_skip_rejects_nan_and_infinite_thresholds():
     assert ok.tolist() == [True, False, False, True, False, False]
     dt, surface = full_step(DISC | MARKERS, dtr[[0]], big[[0]], np.sqrt(big[[0]]), big[[0]], big[[0]], rs)
     assert dt[0] == dtr[0] and not surface[0]
+
+
+def far_r2(rs, dtm):
+    """mirror of bh_host.cpp sdf_far_r2"""
+    k = 1.1251 * dtm
+    a1, a2 = np.sqrt(0.5) - k, 1.0 - k
+    if not a1 > 0.01:
+        return np.inf
+    R0 = max((max(6.0 * rs, 0.02) + 0.003) / a1, (10.0 * np.sqrt(2.0) + 0.5 + 0.003) / a2, (1.5 * rs + 0.075 + 0.003) / a2)
+    return np.nextafter(f32((1.01 * R0) ** 2), f32(np.inf))
+
+
+def step_from_point(p, rs, dtm, cam):
+    """dt and the surface test of the full step at positions p (n, 3) float32 -- the exact mode's op
+    sequence from the position itself (bh_march.hpp sdf_args / sdf_from, :285-310)."""
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+    r2 = (x * x + y * y) + z * z
+    r = np.sqrt(r2)
+    dtr = f32(dtm) * r
+    rho = np.sqrt(x * x + z * z)
+    disc = np.fmax(np.fmax(rho - f32(6.0) * rs, -(rho - f32(3.0) * rs)), np.abs(y) - f32(0.02))
+    zz = (f32(-10.0) - z) ** 2
+    ty, tx = f32(10.0) - np.abs(y), f32(10.0) - np.abs(x)
+    qm = np.fmin((x * x + ty * ty) + zz, (tx * tx + y * y) + zz)
+    m = np.sqrt(qm) - f32(0.5)
+    cps = (-cam / np.sqrt((cam * cam).sum()) * f32(1.5) * rs).astype(f32)
+    dc = cps - p
+    dps = np.sqrt((dc[:, 0] * dc[:, 0] + dc[:, 1] * dc[:, 1]) + dc[:, 2] * dc[:, 2]) - f32(0.075)
+    ds = np.fmin(disc, m)
+    dt = np.fmin(np.fmin(ds, dps) * f32(0.9), dtr)
+    return r2, dtr, dt, ds < f32(0.001)
+
+
+@pytest.mark.parametrize("rs,dtm", [(1.0, 0.5), (0.25, 0.5), (8.0, 0.5), (1.0, 0.1), (1.0, 0.6), (0.003, 0.3)])
+def test_far_field_implies_dt_equals_dtm_r(rs, dtm):
+    """bh_march.hpp's far-field level: every lane with far_r2 <= r^2 <= FLT_MAX has dt == RN(dtm r) and no
+    surface hit, checked on points just beyond the radius (all directions, the markers' and the disc plane's
+    included) and far out."""
+    rng = np.random.default_rng(int(rs * 1000 + dtm * 10))
+    F = far_r2(rs, dtm)
+    assert np.isfinite(F)
+    rs = f32(rs)
+    R = np.sqrt(np.float64(F))
+    n = 400_000
+    d = rng.normal(size=(n, 3))
+    d[: n // 4, 1] *= 1e-3               # near the disc plane
+    d[n // 4: n // 2] = [0.0, 1.0, -1.0] + 0.02 * rng.normal(size=(n // 4, 3))  # towards a marker
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    mag = np.where(rng.random(n) < 0.8, R * (1 + rng.uniform(0, 1e-3, n)), R * np.exp(rng.uniform(0, 8, n)))
+    p = (d * mag[:, None]).astype(f32)
+    cam = np.array([0.0, 0.0, -20.0], f32) if rs != f32(8.0) else np.array([3.0, 1.0, -40.0], f32)
+    r2, dtr, dt, surface = step_from_point(p, rs, dtm, cam)
+    far = (r2 >= F) & (r2 <= f32(np.finfo(np.float32).max))
+    assert far.sum() > n // 2
+    bad = far & ((dt != dtr) | surface)
+    assert not bad.any(), p[bad][:4]
+
+
+def test_far_field_off_for_large_dtm():
+    assert far_r2(1.0, 0.7) == np.inf

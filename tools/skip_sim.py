@@ -103,6 +103,8 @@ for it in range(a.cap):
                 "tight y, m, p": t_y & t_m & t_p, "tight in|out, m, p": (t_in | t_out) & t_m & t_p,
                 "tight out, m, p": t_out & t_m & t_p, "tight out|y, m, p": (t_out | t_y) & t_m & t_p,
                 "tight out, m; loose p": t_out & t_m & (qps - f32(0.01126) >= B)}
+    for Rf in (40.0, 45.0, 50.0):
+        variants[f"far r >= {Rf}"] = r2 >= f32(Rf * Rf)
     for kv, vv in variants.items():
         lvv = ((vv | blackout) | ~live).reshape(-1, 64).all(1)
         var_hits[kv] = var_hits.get(kv, 0) + int((lvv & act).sum())
