@@ -103,6 +103,8 @@ def summarise(cdir):
         out["valu_lane_utilization"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 4)
     if c.get("SQ_WAVES"):
         out["valu_per_wave"] = round(c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"], 1)
+        out["trans_per_wave"] = round(c.get("SQ_INSTS_VALU_TRANS_F32", 0) / c["SQ_WAVES"], 2)
+        out["salu_per_wave"] = round(c.get("SQ_INSTS_SALU", 0) / c["SQ_WAVES"], 1)
     if bench:
         k = bench["kernel"]
         out["bench_hip_event_avg_ms"] = k["avg_ms"]
