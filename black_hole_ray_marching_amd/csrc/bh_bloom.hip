@@ -520,6 +520,9 @@ __device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, co
     return q;
 }
 
+#ifndef BH_BLOOM_SEP_PIPE
+#define BH_BLOOM_SEP_PIPE 1
+#endif
 // FP: the staged footprint's side.  RAW: the tile holds the BGRA8 words (4 B per texel instead of 16, for
 // the wide footprint of the final pass: 44 x 48 words = 8.4 KiB instead of 33 KiB), decoded when a tap
 // reads them.  FS: the tile's row stride, a multiple of 16 float4 for the decoded tile (ds_read_b128 lane
@@ -611,6 +614,17 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
         };
         F4 s{0.0f, 0.0f, 0.0f, 0.0f};
         SepEntry c = colp[0][tx], r = rowp[0][ty];
+#if BH_BLOOM_SEP_PIPE
+        // software-pipelined: tap i + 1's four tile reads are issued before tap i computes (the LDS
+        // latency of one tap hides behind the other's lerps); RAW tiles pipeline the words, decoded at use
+        using W = std::conditional_t<RAW, uint32_t, float4>;
+        auto word = [&](int32_t o) -> W { return tile[o]; };
+        W w00, w10, w01, w11;
+        {
+            const int32_t o = c.f + r.f;
+            w00 = word(o); w10 = word(o + 1); w01 = word(o + FS); w11 = word(o + FS + 1);
+        }
+#endif
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             // the next tap's plan entries are read while this tap computes; one tap at a time otherwise
@@ -621,8 +635,25 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 cn = colp[i + 1][tx];
                 rn = rowp[i + 1][ty];
             }
+#if BH_BLOOM_SEP_PIPE
+            const W v00 = w00, v10 = w10, v01 = w01, v11 = w11;
+            if (i < 7) {
+                const int32_t on = cn.f + rn.f;
+                w00 = word(on); w10 = word(on + 1); w01 = word(on + FS); w11 = word(on + FS + 1);
+            }
+            auto unpack = [&](const W& v) {
+                if constexpr (RAW) {
+                    const F4 d = dec<A1>(L, v);
+                    return make_float4(d.r, d.g, d.b, d.a);
+                } else {
+                    return v;
+                }
+            };
+            const float4 t00 = unpack(v00), t10 = unpack(v10), t01 = unpack(v01), t11 = unpack(v11);
+#else
             const int32_t o = c.f + r.f;
             const float4 t00 = texel(o), t10 = texel(o + 1), t01 = texel(o + FS), t11 = texel(o + FS + 1);
+#endif
             const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;  // sample()'s operations in its order
             F4 q;
             q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
