@@ -428,8 +428,10 @@ def main() -> int:
             overlaps batch i+1's render; rank 0 unpacks every frame's col and blackout_col on a side stream."""
 
             def __init__(self, weights):
+                # always a partition, equal weights included: its tile list (one load per wave) is cheaper
+                # than the plain interleave's per-wave shard walk (4.48 vs 4.72 ns per tile at N = 8, D = 16)
                 self.weights = weights
-                self.part = bh.Partition(W, H, weights, device=local) if weights else None
+                self.part = bh.Partition(W, H, weights or [20] * n, device=local)
                 self.stride = max(self.part.counts) if self.part else multigpu.packed_stride(W, H, n)
                 self.my_tiles = self.part.counts[rank] if self.part else bh.shard_tile_count(W, H, rank, n)
                 self.shard = dict(layout=layout, shard_index=rank, shard_count=n)
@@ -845,13 +847,14 @@ def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     carries), and for frames of fewer than 16384 tiles enough frames for ~2^19 tiles per launch (up to
     BH_MAX_FRAMES = 256, staged through the device frame table): 256x256 cap 64 at D = 32/64/128/256
     0.00643/0.00620/0.00608/0.00604, 1920x1080 at D = 32/64/128 0.1500/0.1498/0.1492, the headline at
-    D = 32/64 0.6078/0.6074 (profiles/r02c/frames_table/).  N > 1: 16 -- the last batch's gather and
-    unpack cannot overlap a next render, so the pipeline drains one batch at the end of the timed region
-    (at N = 8 about D x 0.12 ms against ~0.085 ms of render per frame): with a step = one batch that is
-    ~1/(K+1) of K steps whatever D is, while the shard's render gains ~6 % from 8 to 16 frames per launch
-    and the receive buffers grow with D."""
+    D = 32/64 0.6078/0.6074 (profiles/r02c/frames_table/).  N > 1: 64 -- the last batch's gather and
+    unpack cannot overlap a next render, so the pipeline drains one batch at the end of the timed region:
+    with a step = one batch that is ~1/(K+1) of K steps whatever D is, while a shard's tiles get cheaper
+    with longer launches (N = 8, weighted partition: 4.48 / 4.40 / 4.36 ns per tile at D = 16 / 32 / 64,
+    the one-GPU frame 4.08; profiles/r04/n_gt_1/rank0_D.jsonl); the receive buffers grow with D (rank 0
+    at N = 8: ~6 GB of 288)."""
     if n > 1:
-        return 16
+        return 64
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
     D = 32
     while D < bh_max_frames() and tiles * D < (1 << 19):

@@ -571,7 +571,9 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
             colp[i][j] = e;
         } else {
             SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
-            e.f = (e.f - lo_y) * FS;
+            const int32_t ly = e.f - lo_y;
+            e.f = ly * FS + (ly >> 1);
+            e.pad = ly;
             rowp[i][j] = e;
         }
     }
@@ -684,6 +686,192 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 }
             }
         }
+    };
+    if (a1) run(std::true_type{});
+    else run(std::false_type{});
+}
+
+// ---- the separable up pass with one 2x2 pixel quad per lane (32x32 pixels per block) -------------------
+// Adjacent pixels' taps mostly share texels: in a same-size pass a tap's floor steps by one texel per
+// pixel, in a 2:1 pass by 0 or 1 with the pixel's parity.  Per tap, when every lane of the wave has the
+// same steps (dx between its two columns' floors, dy between its two rows'), with dx, dy in {0, 1}, the
+// quad's texels are one (2 + dx) x (2 + dy) window: 4..9 tile reads for four pixels instead of 16 (the
+// LDS bandwidth bound the one-pixel kernel measured, §7b).  Each pixel still runs sample()'s lerps on its
+// own four texels with its own column and row weights, in the same order: the same bits.  A wave whose
+// steps differ (an exceptional column or row, the frame edge) reads each pixel's four texels.
+// Tile layout: entry (ly, lx) at ly * FS + lx + (ly >> 1) -- every row pair shifted by one entry, so rows
+// two apart (a same-size pass's consecutive quad rows) are 2 FS + 1 entries apart and the next quad row
+// reads the other bank parity (the yq tile's row-pair shift, see FS_YQ).  A row entry of the plan holds
+// that row offset and (pad) the row ly itself: the row below is FS + (ly & 1) further.
+template <int FP, bool RAW>
+constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
+template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>()>
+__global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
+                                                      const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
+                                                      const uint2* __restrict__ same, Tex aux) {
+    __shared__ Lds L;
+    __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS + FP / 2];
+    __shared__ SepEntry colp[8][32], rowp[8][32];
+    const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
+    const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
+    const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
+    const uint32_t x0 = bx + 2u * qx, y0 = by + 2u * qy;  // the quad's first pixel
+    // the block's footprint from the sampler's own arithmetic (see up_sep_kernel)
+    const crm::Rcp Rw = crm::rcp_refined((float)ow), Rh = crm::rcp_refined((float)oh);
+    const Taps k(rx, ry);
+    const uint32_t xl = min(bx + 31u, ow - 1u), yl = min(by + 31u, oh - 1u);
+    const int32_t lo_x = (int32_t)floorf(sample_coord(texcoord(bx, Rw) + k.du_min(), a.w));
+    const int32_t hi_x = (int32_t)floorf(sample_coord(texcoord(xl, Rw) + k.du_max(), a.w));
+    const int32_t lo_y = (int32_t)floorf(sample_coord(texcoord(by, Rh) + k.dv_min(), a.h));
+    const int32_t hi_y = (int32_t)floorf(sample_coord(texcoord(yl, Rh) + k.dv_max(), a.h));
+    const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // the host sizes FP: no cut
+    constexpr int R = (FP * FP + 255) / 256;
+    uint32_t raw[R];
+    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
+        raw[r] = 0xFF000000u;
+        if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
+    }
+    // plan entries as tile offsets: entry e < 256 column (e >> 5, e & 31), else row
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t i = (threadIdx.x >> 5) & 7u, j = threadIdx.x & 31u;
+        if (h == 0) {
+            SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
+            e.f -= lo_x;
+            colp[i][j] = e;
+        } else {
+            SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
+            e.f = (e.f - lo_y) * FS;
+            rowp[i][j] = e;
+        }
+    }
+    // own texels of the epilogue (four pixels), loaded before the tables, used last
+    uint32_t o0[2][2], o1[2][2];
+    bool in[2][2], exact[2][2];
+    uint32_t m = 0xFF000000u;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t x = x0 + c, y = y0 + b;
+            in[b][c] = x < ow && y < oh;
+            const uint32_t pix = (in[b][c] ? y : 0u) * ow + (in[b][c] ? x : 0u);
+            o0[b][c] = o1[b][c] = 0xFF000000u;
+            exact[b][c] = false;
+            if constexpr (EPI != EPI_PLAIN) {
+                o0[b][c] = own0.px[pix];
+                if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
+                exact[b][c] = in[b][c] && same[in[b][c] ? x : 0u].y == 0u && same[ow + (in[b][c] ? y : 0u)].y == 0u;
+            }
+            m = min(m, min(o0[b][c], o1[b][c]));
+        }
+    load_tables(tb, L);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
+        if (ly < cy) {
+            if constexpr (RAW) {
+                tile[ly * FS + lx + (ly >> 1)] = raw[r];
+            } else {
+                const F4 d = dec(L, raw[r]);
+                tile[ly * FS + lx + (ly >> 1)] = make_float4(d.r, d.g, d.b, d.a);
+            }
+        }
+        m = min(m, raw[r]);
+    }
+    const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+    if (!in[0][0]) return;  // the quad's first pixel outside: the whole quad is
+    auto run = [&](auto A1c) {
+        constexpr bool A1 = decltype(A1c)::value;
+        auto texel = [&](int32_t o) {
+            if constexpr (RAW) {
+                const F4 d = dec<A1>(L, tile[o]);
+                return make_float4(d.r, d.g, d.b, d.a);
+            } else {
+                const float4 v = tile[o];
+                return make_float4(v.x, v.y, v.z, A1 ? 1.0f : v.w);
+            }
+        };
+        auto lerp = [&](const float4& t00, const float4& t10, const float4& t01, const float4& t11, const SepEntry& c,
+                        const SepEntry& r) {
+            const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;  // sample()'s operations in its order
+            F4 q;
+            q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
+            q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
+            q.b = (t00.z * ia + t10.z * fa) * ib + (t01.z * ia + t11.z * fa) * fb;
+            q.a = A1 ? 1.0f : (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
+            return q;
+        };
+        F4 s[2][2];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const SepEntry cL = colp[i][2u * qx], cR = colp[i][2u * qx + 1u];
+            const SepEntry rT = rowp[i][2u * qy], rB = rowp[i][2u * qy + 1u];
+            const int32_t dx = cR.f - cL.f, dy = rB.pad - rT.pad;  // the two columns' / rows' floor steps
+            const int32_t dx0 = __builtin_amdgcn_readfirstlane(dx), dy0 = __builtin_amdgcn_readfirstlane(dy);
+            const bool uni = __builtin_amdgcn_ballot_w64((dx != dx0) | (dy != dy0)) == 0ull && (dx0 == 0 || dx0 == 1) &&
+                             (dy0 == 0 || dy0 == 1);
+            const int32_t o = cL.f + rT.f;
+            const int32_t d1 = FS + (rT.pad & 1), d2 = 2 * FS + 1;  // the window's rows 1 and 2
+            auto window = [&](auto DXc, auto DYc) {
+                constexpr int DX = decltype(DXc)::value, DY = decltype(DYc)::value;
+                float4 t[2 + DY][2 + DX];
+#pragma unroll
+                for (int r = 0; r < 2 + DY; ++r)
+#pragma unroll
+                    for (int c = 0; c < 2 + DX; ++c) t[r][c] = texel(o + (r == 0 ? 0 : r == 1 ? d1 : d2) + c);
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int ca = c ? DX : 0, rb = b ? DY : 0;
+                        acc(s[b][c], lerp(t[rb][ca], t[rb][ca + 1], t[rb + 1][ca], t[rb + 1][ca + 1], c ? cR : cL, b ? rB : rT), i);
+                    }
+            };
+            if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+            else if (uni && dx0 == 0 && dy0 == 1) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
+            else if (uni && dx0 == 1 && dy0 == 0) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
+            else if (uni && dx0 == 0 && dy0 == 0) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+            else {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const SepEntry& ce = c ? cR : cL;
+                        const SepEntry& re = b ? rB : rT;
+                        const int32_t op = ce.f + re.f, dn = FS + (re.pad & 1);
+                        acc(s[b][c], lerp(texel(op), texel(op + 1), texel(op + dn), texel(op + dn + 1), ce, re), i);
+                    }
+            }
+            asm volatile("" ::"v"(s[0][0].r), "v"(s[0][1].r), "v"(s[1][0].r), "v"(s[1][1].r));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                if (!in[b][c]) continue;
+                const uint32_t pix = (y0 + b) * ow + x0 + c;
+                const F4 u = div12(s[b][c]);
+                if constexpr (EPI == EPI_PLAIN) {
+                    out.px[pix] = enc(L, u);
+                } else {
+                    const uint32_t ue = enc(L, u);
+                    aux.px[pix] = ue;
+                    if (exact[b][c]) {
+                        const F4 uq = dec<A1>(L, ue);
+                        if constexpr (EPI == EPI_Y) {
+                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), uq));
+                        } else {
+                            const F4 z = quant<A1>(L, remix(dec<A1>(L, o1[b][c]), uq));
+                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), z));
+                        }
+                    }
+                }
+            }
     };
     if (a1) run(std::true_type{});
     else run(std::false_type{});
@@ -1530,8 +1718,9 @@ int std_tap_plan(const TapPlan& P) {
 // The separable plan of an 8-tap pass (see SepEntry / up_sep_kernel): 8 * (ow + oh) entries of 4 words
 // into `outp` (per tap and column, then per tap and row), from the kernel's own f32 arithmetic: texcoord
 // (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset, sample_coord and
-// floor.  Returns the largest 16x16 block footprint along either axis (the staged tile's side), or -1
-// (texture sides above 65535).
+// floor.  Returns the largest 16x16 block footprint along either axis (the staged tile's side of
+// up_sep_kernel) in the low 16 bits and the largest 32x32 block footprint (up_sepq_kernel) in the high
+// ones, or -1 (texture sides above 65535).
 extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                      uint32_t th, uint32_t rx, uint32_t ry,
                                                                      uint32_t* outp) {
@@ -1553,25 +1742,37 @@ extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t 
         for (uint32_t x = 0; x < ow; ++x) axis(ow, tw, du, x, outp + 4u * ((size_t)i * ow + x));
         for (uint32_t y = 0; y < oh; ++y) axis(oh, th, dv, y, outp + 4u * (8u * (size_t)ow + (size_t)i * oh + y));
     }
-    int ext = 0;
-    for (int ax = 0; ax < 2; ++ax) {
-        const uint32_t n = ax ? oh : ow;
-        const size_t base = ax ? 8u * (size_t)ow : 0u;
-        for (uint32_t b = 0; b < n; b += 16u) {
-            const uint32_t l = std::min(b + 15u, n - 1u);
-            int32_t lo = INT_MAX, hi = INT_MIN;
-            for (int i = 0; i < 8; ++i) {
-                lo = std::min(lo, fl(base + (size_t)i * n + b));
-                hi = std::max(hi, fl(base + (size_t)i * n + l));
+    int ext[2] = {0, 0};  // 16- and 32-pixel blocks
+    for (int q = 0; q < 2; ++q) {
+        const uint32_t B = q ? 32u : 16u;
+        for (int ax = 0; ax < 2; ++ax) {
+            const uint32_t n = ax ? oh : ow;
+            const size_t base = ax ? 8u * (size_t)ow : 0u;
+            for (uint32_t b = 0; b < n; b += B) {
+                const uint32_t l = std::min(b + B - 1u, n - 1u);
+                int32_t lo = INT_MAX, hi = INT_MIN;
+                for (int i = 0; i < 8; ++i) {
+                    lo = std::min(lo, fl(base + (size_t)i * n + b));
+                    hi = std::max(hi, fl(base + (size_t)i * n + l));
+                }
+                ext[q] = std::max(ext[q], hi - lo + 2);
             }
-            ext = std::max(ext, hi - lo + 2);
         }
     }
-    return ext;
+    return std::min(ext[0], 0x7FFF) | std::min(ext[1], 0x7FFF) << 16;  // up_sep_kernel's | up_sepq_kernel's
 }
 
 // The staged tile side of up_sep_kernel for a plan's footprint extent, or 0 (too large: the general pass)
-static int sep_tile(int ext) { return ext <= 0 ? 0 : ext <= 24 ? 24 : ext <= 44 ? 44 : 0; }
+static int sep_tile(int ext) {
+    ext &= 0xFFFF;
+    return ext <= 0 ? 0 : ext <= 24 ? 24 : ext <= 44 ? 44 : 0;
+}
+// the quad kernel's staged side for the 32x32 block extent, or 0 (the one-pixel kernel); BH_BLOOM_NO_SEPQ: A/B
+static const bool g_no_sepq = std::getenv("BH_BLOOM_NO_SEPQ") != nullptr;
+static int sepq_tile(int ext) {
+    ext = (ext >> 16) & 0xFFFF;
+    return g_no_sepq || ext <= 0 ? 0 : ext <= 28 ? 28 : ext <= 40 ? 40 : ext <= 60 ? 60 : 0;
+}
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
                                                                         const uint8_t* buckets, const uint32_t* codes,
                                                                         const uint32_t* a, uint32_t aw, uint32_t ah,
@@ -1588,6 +1789,25 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     const dim3 g = grid_for(ow, oh);
 #define BH_SEP(FP, E, RAW) \
     hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
+#define BH_SEPQ(FP, E, RAW, FS) \
+    hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
+    const int fq = sepq_tile(ext);
+    const dim3 gq((ow + 31u) / 32u, (oh + 31u) / 32u);
+    if (fq == 28) {
+        if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, false, 32); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, false, 32);
+        else BH_SEPQ(28, EPI_PLAIN, false, 32);
+        return (int)hipGetLastError();
+    }
+    if (fq == 40) {
+        if (epi == EPI_Y) BH_SEPQ(40, EPI_Y, false, 40); else if (epi == EPI_FINAL) BH_SEPQ(40, EPI_FINAL, false, 40);
+        else BH_SEPQ(40, EPI_PLAIN, false, 40);
+        return (int)hipGetLastError();
+    }
+    if (fq == 60) {
+        if (epi == EPI_Y) BH_SEPQ(60, EPI_Y, true, 80); else if (epi == EPI_FINAL) BH_SEPQ(60, EPI_FINAL, true, 80);
+        else BH_SEPQ(60, EPI_PLAIN, true, 80);
+        return (int)hipGetLastError();
+    }
     const int fp = sep_tile(ext);
     if (fp == 24) {
         if (epi == EPI_Y) BH_SEP(24, EPI_Y, false); else if (epi == EPI_FINAL) BH_SEP(24, EPI_FINAL, false);

@@ -115,7 +115,7 @@ def test_steps_are_batches_and_the_settle_is_optional():
     assert a.settle_ms == 0.0 and a.warmup == 5 and a.steps == 20
     assert bench.parse(["--settle-ms", "100"]).settle_ms == 100.0
     assert bench.auto_frames_per_launch(1, 4096, 2048, 512) == 32
-    assert bench.auto_frames_per_launch(8, 4096, 2048, 512) == 16
+    assert bench.auto_frames_per_launch(8, 4096, 2048, 512) == 64
 
 
 def test_clock_accumulators_to_mhz():
