@@ -571,9 +571,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
             colp[i][j] = e;
         } else {
             SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
-            const int32_t ly = e.f - lo_y;
-            e.f = ly * FS + (ly >> 1);
-            e.pad = ly;
+            e.f = (e.f - lo_y) * FS;
             rowp[i][j] = e;
         }
     }
@@ -744,7 +742,9 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
             colp[i][j] = e;
         } else {
             SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
-            e.f = (e.f - lo_y) * FS;
+            const int32_t ly = e.f - lo_y;
+            e.f = ly * FS + (ly >> 1);
+            e.pad = ly;
             rowp[i][j] = e;
         }
     }
