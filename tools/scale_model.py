@@ -36,6 +36,8 @@ def main():
     print("|---|---|---|---|---|---|---|---|---|---|")
     for r in rows:
         n = r["n"]
+        if n < 2:  # a one-GPU reference row (probe --n 1): nothing crosses a link
+            continue
         W, H = (int(v) for v in r["frame"].split("x"))
         tiles = ((W + 7) // 8) * ((H + 7) // 8)
         w = r.get("weights") or [1] * n
