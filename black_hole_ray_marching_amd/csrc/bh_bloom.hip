@@ -709,7 +709,9 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
                                                       const uint2* __restrict__ same, Tex aux) {
     __shared__ Lds L;
     __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS + FP / 2];
-    __shared__ SepEntry colp[8][32], rowp[8][32];
+    // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
+    // the lanes instead of every second one (2-way bank conflicts)
+    __shared__ SepEntry colp[8][2][16], rowp[8][2][16];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
@@ -739,13 +741,13 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
         if (h == 0) {
             SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
             e.f -= lo_x;
-            colp[i][j] = e;
+            colp[i][j & 1u][j >> 1] = e;
         } else {
             SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
             const int32_t ly = e.f - lo_y;
             e.f = ly * FS + (ly >> 1);
             e.pad = ly;
-            rowp[i][j] = e;
+            rowp[i][j & 1u][j >> 1] = e;
         }
     }
     // own texels of the epilogue (four pixels), loaded before the tables, used last
@@ -808,8 +810,8 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
         F4 s[2][2];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const SepEntry cL = colp[i][2u * qx], cR = colp[i][2u * qx + 1u];
-            const SepEntry rT = rowp[i][2u * qy], rB = rowp[i][2u * qy + 1u];
+            const SepEntry cL = colp[i][0][qx], cR = colp[i][1][qx];
+            const SepEntry rT = rowp[i][0][qy], rB = rowp[i][1][qy];
             const int32_t dx = cR.f - cL.f, dy = rB.pad - rT.pad;  // the two columns' / rows' floor steps
             const int32_t dx0 = __builtin_amdgcn_readfirstlane(dx), dy0 = __builtin_amdgcn_readfirstlane(dy);
             const bool uni = __builtin_amdgcn_ballot_w64((dx != dx0) | (dy != dy0)) == 0ull && (dx0 == 0 || dx0 == 1) &&
