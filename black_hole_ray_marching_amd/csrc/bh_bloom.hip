@@ -701,6 +701,9 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 // two apart (a same-size pass's consecutive quad rows) are 2 FS + 1 entries apart and the next quad row
 // reads the other bank parity (the yq tile's row-pair shift, see FS_YQ).  A row entry of the plan holds
 // that row offset and (pad) the row ly itself: the row below is FS + (ly & 1) further.
+#ifndef BH_BLOOM_SEPQ_STREAM
+#define BH_BLOOM_SEPQ_STREAM 0
+#endif
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
 template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>()>
@@ -820,6 +823,34 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
             const int32_t d1 = FS + (rT.pad & 1), d2 = 2 * FS + 1;  // the window's rows 1 and 2
             auto window = [&](auto DXc, auto DYc) {
                 constexpr int DX = decltype(DXc)::value, DY = decltype(DYc)::value;
+#if BH_BLOOM_SEPQ_STREAM
+                // rows 0 and 1 for the top pixels, then row 2 replaces row 0 for the bottom ones: 2 (2 + DX)
+                // texels live at a time instead of 3 (2 + DX)
+                float4 t0[2 + DX], t1[2 + DX];
+#pragma unroll
+                for (int c = 0; c < 2 + DX; ++c) { t0[c] = texel(o + c); t1[c] = texel(o + d1 + c); }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ca = c ? DX : 0;
+                    acc(s[0][c], lerp(t0[ca], t0[ca + 1], t1[ca], t1[ca + 1], c ? cR : cL, rT), i);
+                }
+                if constexpr (DY == 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int c = 0; c < 2 + DX; ++c) t0[c] = texel(o + d2 + c);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int ca = c ? DX : 0;
+                        acc(s[1][c], lerp(t1[ca], t1[ca + 1], t0[ca], t0[ca + 1], c ? cR : cL, rB), i);
+                    }
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int ca = c ? DX : 0;
+                        acc(s[1][c], lerp(t0[ca], t0[ca + 1], t1[ca], t1[ca + 1], c ? cR : cL, rB), i);
+                    }
+                }
+#else
                 float4 t[2 + DY][2 + DX];
 #pragma unroll
                 for (int r = 0; r < 2 + DY; ++r)
@@ -832,6 +863,7 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
                         const int ca = c ? DX : 0, rb = b ? DY : 0;
                         acc(s[b][c], lerp(t[rb][ca], t[rb][ca + 1], t[rb + 1][ca], t[rb + 1][ca + 1], c ? cR : cL, b ? rB : rT), i);
                     }
+#endif
             };
             if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 0 && dy0 == 1) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
