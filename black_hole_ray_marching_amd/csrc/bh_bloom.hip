@@ -702,7 +702,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 // reads the other bank parity (the yq tile's row-pair shift, see FS_YQ).  A row entry of the plan holds
 // that row offset and (pad) the row ly itself: the row below is FS + (ly & 1) further.
 #ifndef BH_BLOOM_SEPQ_STREAM
-#define BH_BLOOM_SEPQ_STREAM 0
+#define BH_BLOOM_SEPQ_STREAM 1
 #endif
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
