@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 4, final validation: GPU suite, smoke, the driver's bench command and its rocprofv3 trace, bloom at
+# three sizes, 2- and 3-rank rehearsals of the N>1 path (64 frames per launch, tile-list partitions)
+set -u
+O=gpurun_out/r04s; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 200 --timeout-method thread tests > $O/pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/bench_prof -o run -- python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-extra > $O/bench_prof.json 2> $O/bench_prof.err || exit 1
+for s in "1920 1080" "1280 720" "4096 2048"; do
+  set -- $s
+  timeout -k 10 120 python tools/bench_bloom.py --width $1 --height $2 --steps 50 >> $O/bloom.log 2>&1 || exit 1
+done
+BH_BENCH_REHEARSAL=1 timeout -k 10 400 python bench.py --gpus 2 --verify-gather --steps 4 --warmup 2 --no-cpu > $O/reh2.json 2> $O/reh2.err || exit 1
+BH_BENCH_REHEARSAL=1 timeout -k 10 400 python bench.py --gpus 3 --verify-gather --steps 4 --warmup 2 --no-cpu > $O/reh3.json 2> $O/reh3.err || exit 1
