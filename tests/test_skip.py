@@ -14,8 +14,9 @@ def fma32(a, b, c):
 
 
 def fms(u, v):
-    """fma(-u, u, v): v - u*u rounded once (float64 holds u*u exactly)"""
-    return (v.astype(np.float64) - u.astype(np.float64) ** 2).astype(f32)
+    """fma(-u, u, v): v - u*u rounded once (float64 holds u*u exactly; inf - inf is NaN, as the fma's)"""
+    with np.errstate(invalid="ignore", over="ignore"):
+        return (v.astype(np.float64) - u.astype(np.float64) ** 2).astype(f32)
 
 
 def predicate(flags, dtr, rho2, yy, qm, qps, rs):
