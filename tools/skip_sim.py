@@ -62,6 +62,8 @@ def accel(p):
 wave_steps = skip_steps = exact_steps = 0
 cond_hits = np.zeros(4)
 var_hits = {}
+tr_counts = [0, 0]
+prev_dec = prev_act = None
 for it in range(a.cap):
     lw = live.reshape(-1, 64)
     act = lw.any(1)
@@ -105,6 +107,12 @@ for it in range(a.cap):
                 "tight out, m; loose p": t_out & t_m & (qps - f32(0.01126) >= B)}
     for Rf in (40.0, 45.0, 50.0):
         variants[f"far r >= {Rf}"] = r2 >= f32(Rf * Rf)
+    # transitions of the wave-level decision (tight out|y, m, p): after a slow step, how often fast?
+    dec = (((variants["tight out|y, m, p"] | blackout) | ~live).reshape(-1, 64).all(1))
+    if it > 0:
+        tr_counts[0] += int((act & prev_act & ~prev_dec).sum())
+        tr_counts[1] += int((act & prev_act & ~prev_dec & dec).sum())
+    prev_dec, prev_act = dec, act
     for kv, vv in variants.items():
         lvv = ((vv | blackout) | ~live).reshape(-1, 64).all(1)
         var_hits[kv] = var_hits.get(kv, 0) + int((lvv & act).sum())
@@ -138,3 +146,4 @@ print("live lane-steps %d: disc test fails %.3f, marker/photon test fails %.3f, 
       % (cond_hits[0], cond_hits[1] / cond_hits[0], cond_hits[2] / cond_hits[0], cond_hits[3] / cond_hits[0]))
 for kv, vv in var_hits.items():
     print(f"  {kv}: {vv / wave_steps:.3f}")
+print(f"after a slow wave-step: {tr_counts[0]} steps, of them fast {tr_counts[1] / max(tr_counts[0], 1):.3f}")
