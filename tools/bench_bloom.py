@@ -21,6 +21,7 @@ p.add_argument("--height", type=int, default=2048)
 p.add_argument("--levels", type=int, default=3)
 p.add_argument("--steps", type=int, default=100)
 p.add_argument("--warmup", type=int, default=10)
+p.add_argument("--schedule", choices=["both", "auto", "literal"], default="both")
 args = p.parse_args()
 W, H = args.width, args.height
 scene = bh.Scene(W, H, sky=bh.synthetic_sky(), max_iters=512, math=bh.BH_MATH_EXACT)
@@ -30,6 +31,8 @@ out = torch.empty_like(col)
 scene.render(col, bo, fmt=bh.BH_OUT_BGRA8_SRGB)
 stream = torch.cuda.current_stream()
 for name, sched in (("auto", bh.BH_BLOOM_AUTO), ("literal", bh.BH_BLOOM_LITERAL)):
+    if args.schedule not in ("both", name):
+        continue
     for _ in range(args.warmup):
         scene.bloom(col, bo, out, levels=args.levels, schedule=sched, stream=stream)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
