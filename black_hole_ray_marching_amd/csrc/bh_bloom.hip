@@ -701,9 +701,6 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 // two apart (a same-size pass's consecutive quad rows) are 2 FS + 1 entries apart and the next quad row
 // reads the other bank parity (the yq tile's row-pair shift, see FS_YQ).  A row entry of the plan holds
 // that row offset and (pad) the row ly itself: the row below is FS + (ly & 1) further.
-#ifndef BH_BLOOM_SEPQ_POINT
-#define BH_BLOOM_SEPQ_POINT 1
-#endif
 #ifndef BH_BLOOM_SEPQ_STREAM
 #define BH_BLOOM_SEPQ_STREAM 1
 #endif
@@ -868,22 +865,7 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
                     }
 #endif
             };
-            // point taps: a tap whose column and row weights are 0 on every pixel of the wave samples one
-            // texel, exactly -- (t00 * 1 + t10 * 0) * 1 + (t01 * 1 + t11 * 0) * 0 == t00 for the finite,
-            // non-negative decoded texels (the final pass's taps at +-6 / +-12 texels away from the few
-            // inexact columns and rows): one read per pixel instead of a window
-            const bool point = BH_BLOOM_SEPQ_POINT &&
-                               __builtin_amdgcn_ballot_w64(!((cL.fa == 0.0f) & (cR.fa == 0.0f) & (rT.fa == 0.0f) &
-                                                             (rB.fa == 0.0f))) == 0ull;
-            if (point) {
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const float4 t = texel((c ? cR : cL).f + (b ? rB : rT).f);
-                        acc(s[b][c], F4{t.x, t.y, t.z, A1 ? 1.0f : t.w}, i);
-                    }
-            } else if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+            if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 0 && dy0 == 1) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 1 && dy0 == 0) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
             else if (uni && dx0 == 0 && dy0 == 0) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
