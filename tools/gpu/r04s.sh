@@ -2,7 +2,7 @@
 # round 4, final validation: GPU suite, smoke, the driver's bench command and its rocprofv3 trace, bloom at
 # three sizes, 2- and 3-rank rehearsals of the N>1 path (64 frames per launch, tile-list partitions)
 set -u
-O=gpurun_out/r04s; mkdir -p $O
+O=gpurun_out/${OUT:-r04s}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 200 --timeout-method thread tests > $O/pytest_gpu.log 2>&1 || exit 1
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1
