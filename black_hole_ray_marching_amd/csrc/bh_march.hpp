@@ -1499,7 +1499,16 @@ __device__ __forceinline__ void clock_end(unsigned long long* acc, const ClockSt
 
 // One wave per dispatch slot (the grid covers every slot), BH_WG_WAVES waves per workgroup.
 template <uint32_t FMT, uint32_t SF>
-__global__ void __launch_bounds__(64 * BH_WG_WAVES) march_tile_kernel(MarchArgs A) {
+#ifndef BH_MARCH_WPE
+#define BH_MARCH_WPE 0
+#endif
+#if BH_MARCH_WPE
+#define BH_MARCH_WPE_ATTR __attribute__((amdgpu_waves_per_eu(BH_MARCH_WPE, BH_MARCH_WPE)))
+#else
+#define BH_MARCH_WPE_ATTR
+#endif
+// BH_MARCH_WPE (A/B only): ask the register allocator for that many waves per SIMD (§5 item 24)
+__global__ void __launch_bounds__(64 * BH_WG_WAVES) BH_MARCH_WPE_ATTR march_tile_kernel(MarchArgs A) {
     __shared__ float lut[lds_tables<FMT>()];
 #if BH_DIAG_PHASES
     Phases ph;
