@@ -98,6 +98,11 @@ CASES = [
     ("A", 64, 40, 512, 2, {}),                    # markers only
     ("E", 48, 32, 512, 3, {}),                    # shadow-edge zoom: capped "Zeno" rays
     ("E", 64, 40, 1000, 3, {"blackout_eh": 0}),   # ... without blackout (rays reach r ~ 0)
+    # the root-free step's gates (bh_host.cpp: skip for dtm > 0 and 0 < rs <= 8; far-field radius from rs
+    # and dtm, off for dtm >= 0.62): a far radius near 190, the rs limit, both off
+    ("A", 64, 40, 512, 3, {"delta_time_mult": 0.6}),
+    ("B", 64, 40, 512, 3, {"rs": 8.0}),
+    ("A", 48, 32, 512, 3, {"rs": 9.0, "delta_time_mult": 0.7}),
 ]
 
 
