@@ -1,0 +1,6 @@
+#!/bin/bash
+# round 4: the GPU suite on the final tree (new parity cases at the root-free step's gates)
+set -u
+O=gpurun_out/r04x; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 200 --timeout-method thread tests > $O/pytest_gpu.log 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
