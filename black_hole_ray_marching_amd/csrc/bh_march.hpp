@@ -479,6 +479,9 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 #ifndef BH_SDF_SKIP
 #define BH_SDF_SKIP 1
 #endif
+#ifndef BH_SKIP_STICKY
+#define BH_SKIP_STICKY 0
+#endif
 #ifdef BH_DIAG_SLOW
 __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wave_steps;
 // one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
@@ -536,7 +539,7 @@ __device__ __forceinline__ float sdf_skip_slack(const MarchArgs& a, uint32_t fla
 // cap test is a wave-uniform (scalar) compare.
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
-                                        uint32_t& fate, uint32_t it = 0u) {
+                                        uint32_t& fate, uint32_t it = 0u, uint32_t* sk = nullptr) {
     constexpr uint32_t SFS = sf_scene(SF);
     constexpr bool CO = sf_cam_out(SF);
     const uint32_t scene_flags = (SFS == SF_DYN) ? a.scene_flags : SFS;
@@ -580,6 +583,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // distance term may stay finite.)
     if (BRANCHY && __builtin_amdgcn_ballot_w64(!(r2 >= a.far_r2 && r2 <= 0x1.fffffep127f) & !blackout) == 0ull) {
         BH_DIAG_FAR_COUNT();
+        if (BH_SKIP_STICKY && sk) *sk = 0u;
         if (blackout) {
             fate = (uint32_t)BH_FATE_BLACKOUT;
             return true;
@@ -602,8 +606,16 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         // blackout select becomes a branch around the test.  Taking the lane mask straight from the compare,
         // llvm.amdgcn.fcmp, and masking the blackout lanes as integers is 4 VALU fewer and measured 0.9 %
         // slower: profiles/r04/ab_skip_forms/.)
-        const float slack = blackout ? __builtin_inff() : sdf_skip_slack(a, scene_flags, dtr, rho2, yy, qm, qps);
-        if (a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull) {
+        // BH_SKIP_STICKY (A/B): after a tested step that took the roots, the next step takes them without
+        // the test (after a slow step only ~24 % of the next are fast: tools/skip_sim.py), then tests again
+        const bool test = !BH_SKIP_STICKY || !sk || *sk == 0u;
+        bool fast = false;
+        if (test) {
+            const float slack = blackout ? __builtin_inff() : sdf_skip_slack(a, scene_flags, dtr, rho2, yy, qm, qps);
+            fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
+        }
+        if (BH_SKIP_STICKY && sk) *sk = (test && !fast) ? 1u : 0u;
+        if (fast) {
             BH_DIAG_SKIP_COUNT();
             if (blackout) {
                 fate = (uint32_t)BH_FATE_BLACKOUT;
@@ -856,9 +868,10 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
 // fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
 template <uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
-                                              uint32_t& fate, uint32_t it = 0u) {
+                                              uint32_t& fate, uint32_t it = 0u, uint32_t* sk = nullptr) {
 #if BH_FAST
     FOps X;
+    (void)sk;
     return step_bf<true, FOps, SF, UNI>(a, f, in, out, X, fate, it);
 #else
     XOps<true> X;
@@ -866,7 +879,7 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
     if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
         atomicAdd(&g_diag_all_wave_steps, 1u);
 #endif
-    bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it);
+    bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it, sk);
 #ifdef BH_DIAG_SLOW
     const uint64_t badm = __builtin_amdgcn_ballot_w64(X.bad);
     if (badm != 0ull && (threadIdx.x & 63u) == 0u) {
@@ -1341,6 +1354,7 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
     // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
     RayState sb = st;
     bool alive = true;
+    uint32_t sk = 0u;  // BH_SKIP_STICKY: the root-free test's state (step_bf)
     // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
     // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
     constexpr uint32_t TRIP_PAIRS = 3;
@@ -1349,13 +1363,13 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
 #pragma unroll
         for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
             if (alive) {
-                if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j)) {
+                if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j, &sk)) {
                     alive = false;
                     if (fate_before_rk(fate)) sb.n_rk = 0u;
                 }
             }
             if (alive) {
-                if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u)) {
+                if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u, &sk)) {
                     alive = false;
                     if (fate_before_rk(fate)) st.n_rk = 0u;
                 }
