@@ -982,6 +982,108 @@ __global__ void __launch_bounds__(256) remix2_plan_kernel(Tables tb, CTex col, C
 // listed ones).  EPI_Y: out = remix(S(A), S(B)) (A = X, B = U1); EPI_FINAL: out = remix(S(A), S(F)),
 // F = q(remix(S(B), S(C))) (A = col, B = Y, C = B-texture) -- remix_plan_kernel's / remix2_plan_kernel's
 // per-pixel arithmetic.
+#ifndef BH_BLOOM_FIXUP_GATHER
+#define BH_BLOOM_FIXUP_GATHER 1  // 0 (A/B): the per-sample form below
+#endif
+// A same-size sample's texel words, gathered before the block stages its tables: (x0, y0), (x1, y0),
+// (x0, y1), (x1, y1).  A word whose weight is 0 is not read (0 instead): it enters sample_same's lerp as
+// t * 0 == +0 for any finite decoded t >= 0, so finish_same gives sample_same's bits.
+struct SameWords { uint32_t t[4]; float fa, fb; };
+__device__ __forceinline__ SameWords gather_same(CTex t, uint2 cx, uint2 cy) {
+    const uint32_t x0 = cx.x & 0xFFFFu, x1 = cx.x >> 16, r0 = (cy.x & 0xFFFFu) * t.w, r1 = (cy.x >> 16) * t.w;
+    SameWords s;
+    s.fa = __uint_as_float(cx.y);
+    s.fb = __uint_as_float(cy.y);
+    const bool ex = s.fa != 0.0f, ey = s.fb != 0.0f;
+    s.t[0] = t.px[r0 + x0];
+    s.t[1] = ex ? t.px[r0 + x1] : 0u;
+    s.t[2] = ey ? t.px[r1 + x0] : 0u;
+    s.t[3] = ex && ey ? t.px[r1 + x1] : 0u;
+    return s;
+}
+__device__ __forceinline__ F4 finish_same(const Lds& L, const SameWords& s) {
+    if (s.fa == 0.0f && s.fb == 0.0f) return dec(L, s.t[0]);
+    const F4 a = dec(L, s.t[0]), b = dec(L, s.t[1]), c = dec(L, s.t[2]), d = dec(L, s.t[3]);
+    return lerp_plan(make_float4(a.r, a.g, a.b, a.a), make_float4(b.r, b.g, b.b, b.a), make_float4(c.r, c.g, c.b, c.a),
+                     make_float4(d.r, d.g, d.b, d.a), s.fa, s.fb);
+}
+// The gather form: the kernel's global reads in two dependent round trips (the list entry, then the
+// plan entries of the pixel's column and row and of their neighbours, then every texel word) with the
+// tables' staging overlapping them, instead of five (tables, list, plan, F's plan entries, texels).  A
+// same-size sample's texels are its pixel's own and one neighbour (t is within an ulp-sized offset of
+// the pixel's index), so F's plan entries are among the three preloaded per axis; `pick` reads the plan
+// for any other index.
+template <uint32_t EPI>
+__global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CTex B, CTex C,
+                                                           const uint2* __restrict__ plan,
+                                                           const uint32_t* __restrict__ list, uint32_t n_cols,
+                                                           uint32_t n_rows, Tex out) {
+    __shared__ Lds L;
+    const uint32_t W = out.w, H = out.h;
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x, nc = (uint64_t)n_cols * H;
+    uint32_t x = 0u, y = 0u;
+    bool live = true;
+    if (i < nc) {
+        x = list[i / H];
+        y = (uint32_t)(i % H);
+    } else {
+        const uint64_t j = i - nc;
+        live = j < (uint64_t)n_rows * W;
+        if (live) {
+            y = list[n_cols + j / W];
+            x = (uint32_t)(j % W);
+        }
+    }
+    live = live && x < W && y < H;  // defensive: a list entry outside the frame
+    if (!live) x = y = 0u;
+    const uint2 cx = plan[x], cy = plan[W + y];
+    if (i >= nc && cx.y != 0u) live = false;  // an inexact column: its pixels are the first part's
+    const SameWords a = gather_same(A, cx, cy);
+    if constexpr (EPI == EPI_Y) {
+        const SameWords b = gather_same(B, cx, cy);
+        load_tables(tb, L);
+        if (!live) return;
+        out.px[y * W + x] = enc(L, remix(finish_same(L, a), finish_same(L, b)));
+    } else {
+        const uint2 PX[3] = {plan[x ? x - 1u : 0u], cx, plan[min(x + 1u, W - 1u)]};
+        const uint2 PY[3] = {plan[W + (y ? y - 1u : 0u)], cy, plan[W + min(y + 1u, H - 1u)]};
+        auto pick = [&](uint32_t u, uint32_t c, const uint2(&P)[3], uint32_t base) -> uint2 {
+            if (u == c) return P[1];
+            if (u + 1u == c) return P[0];
+            if (u == c + 1u) return P[2];
+            return plan[base + u];
+        };
+        const float fa = __uint_as_float(cx.y), fb = __uint_as_float(cy.y);
+        const bool ex = fa != 0.0f, ey = fb != 0.0f;
+        const uint2 px0 = pick(cx.x & 0xFFFFu, x, PX, 0u), px1 = pick(cx.x >> 16, x, PX, 0u);
+        const uint2 py0 = pick(cy.x & 0xFFFFu, y, PY, W), py1 = pick(cy.x >> 16, y, PY, W);
+        // F at the (up to 4) texels of final_in1 the lerp weighs (remix2_plan_kernel)
+        SameWords fbw[4] = {}, fcw[4] = {};
+        fbw[0] = gather_same(B, px0, py0);
+        fcw[0] = gather_same(C, px0, py0);
+        if (ex) {
+            fbw[1] = gather_same(B, px1, py0);
+            fcw[1] = gather_same(C, px1, py0);
+        }
+        if (ey) {
+            fbw[2] = gather_same(B, px0, py1);
+            fcw[2] = gather_same(C, px0, py1);
+        }
+        if (ex && ey) {
+            fbw[3] = gather_same(B, px1, py1);
+            fcw[3] = gather_same(C, px1, py1);
+        }
+        load_tables(tb, L);
+        if (!live) return;
+        auto F = [&](int k) { return quant(L, remix(finish_same(L, fbw[k]), finish_same(L, fcw[k]))); };
+        const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
+        const F4 f0 = F(0), f1 = ex ? F(1) : z, f2 = ey ? F(2) : z, f3 = ex && ey ? F(3) : z;
+        const F4 f = lerp_plan(make_float4(f0.r, f0.g, f0.b, f0.a), make_float4(f1.r, f1.g, f1.b, f1.a),
+                               make_float4(f2.r, f2.g, f2.b, f2.a), make_float4(f3.r, f3.g, f3.b, f3.a), fa, fb);
+        out.px[y * W + x] = enc(L, remix(finish_same(L, a), f));
+    }
+}
+
 template <uint32_t EPI>
 __global__ void __launch_bounds__(256) fixup_kernel(Tables tb, CTex A, CTex B, CTex C, const uint2* __restrict__ plan,
                                                     const uint32_t* __restrict__ list, uint32_t n_cols, uint32_t n_rows,
@@ -1082,6 +1184,74 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
         }
         out.px[(uint32_t)y * out.w + x] = enc(L, r);
     }
+}
+
+// Two downsamples in one pass (the fused chains' blur: the intermediate level is read by nothing but the
+// next downsample).  down_word is pass_kernel<SH_DOWN>'s stored word at pixel (x, y) of an mw x mh pass
+// over `a` (Rw, Rh the reciprocals of mw, mh) -- its arithmetic and its short forms, a centre's own word
+// included -- and down2_kernel evaluates pass_kernel<SH_DOWN> over that texture, each texel it weighs
+// computed on the spot.  A 2:1 downsample weighs each intermediate texel for one output pixel, so
+// nothing is computed twice; the intermediate level is never stored.
+__device__ __forceinline__ uint32_t down_word(const Lds& L, CTex a, uint32_t x, uint32_t y, const crm::Rcp& Rw,
+                                              const crm::Rcp& Rh) {
+    const float u = texcoord(x, Rw), v = texcoord(y, Rh);
+    const float tx = sample_coord(u, a.w), ty = sample_coord(v, a.h);
+    const float fx = floorf(tx), fy = floorf(ty);
+    const float fa = tx - fx, fb = ty - fy;
+    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
+    const int32_t x0 = clampi((int32_t)fx, 0, wm), y0 = clampi((int32_t)fy, 0, hm);
+    const int32_t x1 = clampi((int32_t)fx + 1, 0, wm), y1 = clampi((int32_t)fy + 1, 0, hm);
+    if (fa == 0.0f && fb == 0.0f) return a.px[(uint32_t)y0 * a.w + (uint32_t)x0];
+    const GlobalSrc A{a, &L};
+    F4 r;
+    if (fa == 0.5f && fb == 0.5f) {
+        const F4 q00 = A.at(x0, y0), q10 = A.at(x1, y0), q01 = A.at(x0, y1), q11 = A.at(x1, y1);
+        r = {((q00.r + q10.r) + (q01.r + q11.r)) * 0.25f, ((q00.g + q10.g) + (q01.g + q11.g)) * 0.25f,
+             ((q00.b + q10.b) + (q01.b + q11.b)) * 0.25f, ((q00.a + q10.a) + (q01.a + q11.a)) * 0.25f};
+    } else {
+        r = sample(A, u, v);
+    }
+    return enc(L, r);
+}
+struct DownSrc {
+    static constexpr bool kA1 = false;
+    CTex t;  // the intermediate level: only its size (px unused)
+    CTex a;  // its source
+    const Lds* L;
+    crm::Rcp Rw, Rh;
+    __device__ __forceinline__ F4 at(int32_t x, int32_t y) const {
+        return dec(*L, down_word(*L, a, (uint32_t)x, (uint32_t)y, Rw, Rh));
+    }
+};
+__global__ void BLOOM_BOUNDS down2_kernel(Tables tb, CTex a, uint32_t mw, uint32_t mh, Tex out) {
+    __shared__ Lds L;
+    const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
+    const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
+    load_tables(tb, L);
+    if (x >= out.w || y >= out.h) return;
+    const DownSrc M{CTex{nullptr, mw, mh}, a, &L, crm::rcp_refined((float)mw), crm::rcp_refined((float)mh)};
+    const float u = texcoord(x, Rw), v = texcoord(y, Rh);
+    const float tx = sample_coord(u, mw), ty = sample_coord(v, mh);
+    const float fx = floorf(tx), fy = floorf(ty);
+    const float fa = tx - fx, fb = ty - fy;
+    const int32_t wm = (int32_t)mw - 1, hm = (int32_t)mh - 1;
+    const int32_t x0 = clampi((int32_t)fx, 0, wm), y0 = clampi((int32_t)fy, 0, hm);
+    const int32_t x1 = clampi((int32_t)fx + 1, 0, wm), y1 = clampi((int32_t)fy + 1, 0, hm);
+    uint32_t w;
+    if (fa == 0.0f && fb == 0.0f) {
+        w = down_word(L, a, (uint32_t)x0, (uint32_t)y0, M.Rw, M.Rh);
+    } else {
+        F4 r;
+        if (fa == 0.5f && fb == 0.5f) {
+            const F4 q00 = M.at(x0, y0), q10 = M.at(x1, y0), q01 = M.at(x0, y1), q11 = M.at(x1, y1);
+            r = {((q00.r + q10.r) + (q01.r + q11.r)) * 0.25f, ((q00.g + q10.g) + (q01.g + q11.g)) * 0.25f,
+                 ((q00.b + q10.b) + (q01.b + q11.b)) * 0.25f, ((q00.a + q10.a) + (q01.a + q11.a)) * 0.25f};
+        } else {
+            r = sample(M, u, v);
+        }
+        w = enc(L, r);
+    }
+    out.px[y * out.w + x] = w;
 }
 
 // Fused stage 1 (same-size sampling exact): Y = X + 0.5 * q(blur1(X)), blur1 = up8(X, res (W, H)).
@@ -1870,12 +2040,32 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
     const Tables tb{lut, enc, buckets, codes};
     const dim3 g((uint32_t)((n + 255u) / 256u));
     const uint2* S = reinterpret_cast<const uint2*>(same);
-    if (epi == EPI_Y)
+    static const bool per_sample = !BH_BLOOM_FIXUP_GATHER || std::getenv("BH_BLOOM_FIXUP_SAMPLE") != nullptr;  // A/B
+    if (!per_sample && epi == EPI_Y)
+        hipLaunchKernelGGL(fixup_gather_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
+                           CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h});
+    else if (!per_sample)
+        hipLaunchKernelGGL(fixup_gather_kernel<EPI_FINAL>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
+                           CTex{c, w, h}, S, list, n_cols, n_rows, Tex{out, w, h});
+    else if (epi == EPI_Y)
         hipLaunchKernelGGL(fixup_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{b, w, h}, S, list,
                            n_cols, n_rows, Tex{out, w, h});
     else
         hipLaunchKernelGGL(fixup_kernel<EPI_FINAL>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{c, w, h}, S,
                            list, n_cols, n_rows, Tex{out, w, h});
+    return (int)hipGetLastError();
+}
+
+// Two downsamples a -> (mw x mh) -> out in one pass (down2_kernel); false: not taken (BH_BLOOM_NO_DOWN2,
+// A/B), the caller runs the two passes
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const float* lut, const float* enc,
+                                                                          const uint8_t* buckets, const uint32_t* codes,
+                                                                          const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                          uint32_t mw, uint32_t mh, uint32_t* out,
+                                                                          uint32_t ow, uint32_t oh, hipStream_t s) {
+    if (mw == 0u || mh == 0u) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(down2_kernel, grid_for(ow, oh), dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{a, aw, ah},
+                       mw, mh, Tex{out, ow, oh});
     return (int)hipGetLastError();
 }
 

@@ -258,6 +258,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
                                                                           uint32_t h, hipStream_t s);
+// two downsamples a -> mw x mh -> out in one pass (the intermediate level not stored)
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const float* lut, const float* enc,
+                                                                          const uint8_t* buckets, const uint32_t* codes,
+                                                                          const uint32_t* a, uint32_t aw, uint32_t ah,
+                                                                          uint32_t mw, uint32_t mh, uint32_t* out,
+                                                                          uint32_t ow, uint32_t oh, hipStream_t s);
 // the same-size plan of a w x h frame (bh_bloom.hip): (w + h) uint2 entries; the plan remixes
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_plan(uint32_t w, uint32_t h, uint32_t* outp);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(const float* lut, const float* enc,

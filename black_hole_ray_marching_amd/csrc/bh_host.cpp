@@ -733,6 +733,25 @@ struct BloomRun {
             err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
                                        sp.dev, sp.ext, s);
     }
+    // the fused chains' blur downsamples src (res[0]) -> down[1] -> ... -> down[levels - 1]; returns the
+    // last level.  An intermediate level is read by nothing but the next downsample, so pairs run as one
+    // pass (bh_launch_bloom_down2, the intermediate not stored); BH_BLOOM_NO_DOWN2 runs them one by one (A/B)
+    const uint32_t* downs(const uint32_t* src, uint32_t levels, uint32_t** down, const BloomPlan& P) {
+        static const bool no_down2 = std::getenv("BH_BLOOM_NO_DOWN2") != nullptr;
+        const uint32_t* dn = src;
+        uint32_t l = 1;
+        for (; !no_down2 && l + 1 < levels && err == 0; l += 2) {
+            err = bh_launch_bloom_down2(c->lut, c->enc, c->enc_b, c->enc_e, dn, P.res[l - 1][0], P.res[l - 1][1],
+                                        P.res[l][0], P.res[l][1], down[l + 1], P.res[l + 1][0], P.res[l + 1][1], s);
+            dn = down[l + 1];
+        }
+        for (; l < levels; ++l) {
+            pass(bh_bloom_shader_down, dn, P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1], down[l], P.res[l][0],
+                 P.res[l][1]);
+            dn = down[l];
+        }
+        return dn;
+    }
 };
 
 }  // namespace
@@ -821,13 +840,7 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
             if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
             S = copy_in[1];
         }
-        const uint32_t* dn = S;  // down[0] == S
-        for (uint32_t l = 1; l < levels; ++l) {
-            R.pass(bh_bloom_shader_down, dn, P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1], down[l],
-                   P.res[l][0], P.res[l][1]);
-            dn = down[l];
-        }
-        const uint32_t* u_src = dn;  // up[levels-1] == down[levels-1]
+        const uint32_t* u_src = R.downs(S, levels, down, P);  // down[0] == S; up[levels-1] == down[levels-1]
         for (uint32_t l = 0; l + 1 < levels; ++l) {
             const uint32_t ti = levels - l - 2;
             R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
@@ -872,13 +885,7 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
             fused_up(1u, X, W, H, full, remix_in1[0], X, nullptr, copy_in[1]);
             S = copy_in[1];
         }
-        const uint32_t* dn = S;
-        for (uint32_t l = 1; l < levels; ++l) {
-            R.pass(bh_bloom_shader_down, dn, P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1], down[l],
-                   P.res[l][0], P.res[l][1]);
-            dn = down[l];
-        }
-        const uint32_t* u_src = dn;
+        const uint32_t* u_src = R.downs(S, levels, down, P);
         for (uint32_t l = 0; l + 1 < levels; ++l) {
             const uint32_t ti = levels - l - 2;
             R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
