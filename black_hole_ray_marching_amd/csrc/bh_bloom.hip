@@ -1995,8 +1995,14 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
 #define BH_SEPQ(FP, E, RAW, FS) \
     hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
-    const int fq = sepq_tile(ext);
+    // A/B: BH_BLOOM_SEPQ_MIN_BLOCKS=n runs a pass of fewer than n quad blocks (32x32 pixels) with the
+    // one-pixel kernel (four times the blocks) when its footprint fits
+    static const uint32_t min_blocks = [] {
+        const char* e = std::getenv("BH_BLOOM_SEPQ_MIN_BLOCKS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
     const dim3 gq((ow + 31u) / 32u, (oh + 31u) / 32u);
+    const int fq = gq.x * gq.y < min_blocks && sep_tile(ext) != 0 ? 0 : sepq_tile(ext);
     if (fq == 28) {
         if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, false, 32); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, false, 32);
         else BH_SEPQ(28, EPI_PLAIN, false, 32);
