@@ -1187,71 +1187,73 @@ __global__ void BLOOM_BOUNDS pass_kernel(Tables tb, CTex a, CTex b, uint32_t rx,
 }
 
 // Two downsamples in one pass (the fused chains' blur: the intermediate level is read by nothing but the
-// next downsample).  down_word is pass_kernel<SH_DOWN>'s stored word at pixel (x, y) of an mw x mh pass
-// over `a` (Rw, Rh the reciprocals of mw, mh) -- its arithmetic and its short forms, a centre's own word
-// included -- and down2_kernel evaluates pass_kernel<SH_DOWN> over that texture, each texel it weighs
-// computed on the spot.  A 2:1 downsample weighs each intermediate texel for one output pixel, so
-// nothing is computed twice; the intermediate level is never stored.
-__device__ __forceinline__ uint32_t down_word(const Lds& L, CTex a, uint32_t x, uint32_t y, const crm::Rcp& Rw,
-                                              const crm::Rcp& Rh) {
+// next downsample).  A texel of the intermediate level is pass_kernel<SH_DOWN>'s stored word at that
+// pixel -- its arithmetic and its short forms, a centre's own word included -- and down2_kernel evaluates
+// pass_kernel<SH_DOWN> over that texture, each texel it weighs computed on the spot.  A 2:1 downsample
+// weighs each intermediate texel for one output pixel, so nothing is computed twice; the intermediate
+// level is never stored.  Every texel index is arithmetic on the pixel's coordinates, so the 16 source
+// words are read at once, before the block stages its tables (one dependent round trip, not three).
+struct DownAt {  // the sampler's texels and weights of a pass pixel (sample()'s own arithmetic)
+    int32_t x0, x1, y0, y1;
+    float fa, fb;
+};
+__device__ __forceinline__ DownAt down_at(uint32_t x, uint32_t y, const crm::Rcp& Rw, const crm::Rcp& Rh, uint32_t sw,
+                                          uint32_t sh) {
     const float u = texcoord(x, Rw), v = texcoord(y, Rh);
-    const float tx = sample_coord(u, a.w), ty = sample_coord(v, a.h);
+    const float tx = sample_coord(u, sw), ty = sample_coord(v, sh);
     const float fx = floorf(tx), fy = floorf(ty);
-    const float fa = tx - fx, fb = ty - fy;
-    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
-    const int32_t x0 = clampi((int32_t)fx, 0, wm), y0 = clampi((int32_t)fy, 0, hm);
-    const int32_t x1 = clampi((int32_t)fx + 1, 0, wm), y1 = clampi((int32_t)fy + 1, 0, hm);
-    if (fa == 0.0f && fb == 0.0f) return a.px[(uint32_t)y0 * a.w + (uint32_t)x0];
-    const GlobalSrc A{a, &L};
+    const int32_t wm = (int32_t)sw - 1, hm = (int32_t)sh - 1;
+    return {clampi((int32_t)fx, 0, wm), clampi((int32_t)fx + 1, 0, wm), clampi((int32_t)fy, 0, hm),
+            clampi((int32_t)fy + 1, 0, hm), tx - fx, ty - fy};
+}
+// pass_kernel<SH_DOWN>'s value at a pixel from its four texels' words w (00, 10, 01, 11): the centre's own
+// word (as a decoded value: enc(dec(t)) == t), the 2:1 quad form or sample()'s lerps
+__device__ __forceinline__ F4 down_value(const Lds& L, const uint32_t (&w)[4], float fa, float fb) {
+    const F4 q00 = dec(L, w[0]);
+    if (fa == 0.0f && fb == 0.0f) return q00;
+    const F4 q10 = dec(L, w[1]), q01 = dec(L, w[2]), q11 = dec(L, w[3]);
     F4 r;
     if (fa == 0.5f && fb == 0.5f) {
-        const F4 q00 = A.at(x0, y0), q10 = A.at(x1, y0), q01 = A.at(x0, y1), q11 = A.at(x1, y1);
         r = {((q00.r + q10.r) + (q01.r + q11.r)) * 0.25f, ((q00.g + q10.g) + (q01.g + q11.g)) * 0.25f,
              ((q00.b + q10.b) + (q01.b + q11.b)) * 0.25f, ((q00.a + q10.a) + (q01.a + q11.a)) * 0.25f};
     } else {
-        r = sample(A, u, v);
+        const float ia = 1.0f - fa, ib = 1.0f - fb;
+        r.r = (q00.r * ia + q10.r * fa) * ib + (q01.r * ia + q11.r * fa) * fb;
+        r.g = (q00.g * ia + q10.g * fa) * ib + (q01.g * ia + q11.g * fa) * fb;
+        r.b = (q00.b * ia + q10.b * fa) * ib + (q01.b * ia + q11.b * fa) * fb;
+        r.a = (q00.a * ia + q10.a * fa) * ib + (q01.a * ia + q11.a * fa) * fb;
     }
-    return enc(L, r);
+    return r;
 }
-struct DownSrc {
-    static constexpr bool kA1 = false;
-    CTex t;  // the intermediate level: only its size (px unused)
-    CTex a;  // its source
-    const Lds* L;
-    crm::Rcp Rw, Rh;
-    __device__ __forceinline__ F4 at(int32_t x, int32_t y) const {
-        return dec(*L, down_word(*L, a, (uint32_t)x, (uint32_t)y, Rw, Rh));
-    }
-};
+// the stored word of a pass pixel: its centre's own word, else enc of the value
+__device__ __forceinline__ uint32_t down_store(const Lds& L, const uint32_t (&w)[4], float fa, float fb) {
+    return fa == 0.0f && fb == 0.0f ? w[0] : enc(L, down_value(L, w, fa, fb));
+}
 __global__ void BLOOM_BOUNDS down2_kernel(Tables tb, CTex a, uint32_t mw, uint32_t mh, Tex out) {
     __shared__ Lds L;
     const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
-    const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
-    load_tables(tb, L);
-    if (x >= out.w || y >= out.h) return;
-    const DownSrc M{CTex{nullptr, mw, mh}, a, &L, crm::rcp_refined((float)mw), crm::rcp_refined((float)mh)};
-    const float u = texcoord(x, Rw), v = texcoord(y, Rh);
-    const float tx = sample_coord(u, mw), ty = sample_coord(v, mh);
-    const float fx = floorf(tx), fy = floorf(ty);
-    const float fa = tx - fx, fb = ty - fy;
-    const int32_t wm = (int32_t)mw - 1, hm = (int32_t)mh - 1;
-    const int32_t x0 = clampi((int32_t)fx, 0, wm), y0 = clampi((int32_t)fy, 0, hm);
-    const int32_t x1 = clampi((int32_t)fx + 1, 0, wm), y1 = clampi((int32_t)fy + 1, 0, hm);
-    uint32_t w;
-    if (fa == 0.0f && fb == 0.0f) {
-        w = down_word(L, a, (uint32_t)x0, (uint32_t)y0, M.Rw, M.Rh);
-    } else {
-        F4 r;
-        if (fa == 0.5f && fb == 0.5f) {
-            const F4 q00 = M.at(x0, y0), q10 = M.at(x1, y0), q01 = M.at(x0, y1), q11 = M.at(x1, y1);
-            r = {((q00.r + q10.r) + (q01.r + q11.r)) * 0.25f, ((q00.g + q10.g) + (q01.g + q11.g)) * 0.25f,
-                 ((q00.b + q10.b) + (q01.b + q11.b)) * 0.25f, ((q00.a + q10.a) + (q01.a + q11.a)) * 0.25f};
-        } else {
-            r = sample(M, u, v);
-        }
-        w = enc(L, r);
+    const bool in = x < out.w && y < out.h;
+    const DownAt o = down_at(in ? x : 0u, in ? y : 0u, crm::rcp_refined((float)out.w), crm::rcp_refined((float)out.h),
+                             mw, mh);
+    const crm::Rcp Mw = crm::rcp_refined((float)mw), Mh = crm::rcp_refined((float)mh);
+    // the four intermediate texels (00, 10, 01, 11) and the four source words of each
+    DownAt m[4];
+    uint32_t w[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = down_at((uint32_t)(k & 1 ? o.x1 : o.x0), (uint32_t)(k & 2 ? o.y1 : o.y0), Mw, Mh, a.w, a.h);
+        const uint32_t r0 = (uint32_t)m[k].y0 * a.w, r1 = (uint32_t)m[k].y1 * a.w;
+        w[k][0] = a.px[r0 + (uint32_t)m[k].x0];
+        w[k][1] = a.px[r0 + (uint32_t)m[k].x1];
+        w[k][2] = a.px[r1 + (uint32_t)m[k].x0];
+        w[k][3] = a.px[r1 + (uint32_t)m[k].x1];
     }
-    out.px[y * out.w + x] = w;
+    load_tables(tb, L);
+    if (!in) return;
+    uint32_t mid[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mid[k] = down_store(L, w[k], m[k].fa, m[k].fb);
+    out.px[y * out.w + x] = down_store(L, mid, o.fa, o.fb);
 }
 
 // Fused stage 1 (same-size sampling exact): Y = X + 0.5 * q(blur1(X)), blur1 = up8(X, res (W, H)).
