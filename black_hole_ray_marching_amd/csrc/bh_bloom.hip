@@ -2005,6 +2005,22 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     }();
     const dim3 gq((ow + 31u) / 32u, (oh + 31u) / 32u);
     const int fq = gq.x * gq.y < min_blocks && sep_tile(ext) != 0 ? 0 : sepq_tile(ext);
+    // A/B: BH_BLOOM_SEPQ_RAW bit 0 / bit 1 stage the 28 / 40 tiles as raw words too (decoded per read;
+    // 4x less LDS per block, so more blocks per CU, for 4 table reads per texel read)
+    static const uint32_t raw_mask = [] {
+        const char* e = std::getenv("BH_BLOOM_SEPQ_RAW");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    }();
+    if (fq == 28 && (raw_mask & 1u)) {
+        if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, true, 48); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, true, 48);
+        else BH_SEPQ(28, EPI_PLAIN, true, 48);
+        return (int)hipGetLastError();
+    }
+    if (fq == 40 && (raw_mask & 2u)) {
+        if (epi == EPI_Y) BH_SEPQ(40, EPI_Y, true, 48); else if (epi == EPI_FINAL) BH_SEPQ(40, EPI_FINAL, true, 48);
+        else BH_SEPQ(40, EPI_PLAIN, true, 48);
+        return (int)hipGetLastError();
+    }
     if (fq == 28) {
         if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, false, 32); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, false, 32);
         else BH_SEPQ(28, EPI_PLAIN, false, 32);
