@@ -704,17 +704,42 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 #ifndef BH_BLOOM_SEPQ_STREAM
 #define BH_BLOOM_SEPQ_STREAM 1
 #endif
+// BH_BLOOM_SEPQ_E8: the block's plan entries in 8 bytes (floor offset and row as int16, fa; ia = 1 - fa
+// recomputed, the host plan's own operation) -- 4 KiB less LDS per block.  BH_BLOOM_SEPQ_WPE: a waves per
+// EU bound for the quad kernel (0: none).  Both A/B switches.
+#ifndef BH_BLOOM_SEPQ_E8
+#define BH_BLOOM_SEPQ_E8 0
+#endif
+#ifndef BH_BLOOM_SEPQ_WPE
+#define BH_BLOOM_SEPQ_WPE 0
+#endif
+#if BH_BLOOM_SEPQ_E8
+struct QEntry { int16_t f, pad; float fa; };
+__device__ __forceinline__ float q_ia(const QEntry& e) { return 1.0f - e.fa; }
+__device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry& e) {
+    return {(int16_t)f, (int16_t)pad, e.fa};
+}
+#else
+using QEntry = SepEntry;
+__device__ __forceinline__ float q_ia(const QEntry& e) { return e.ia; }
+__device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry& e) { return {f, e.fa, e.ia, pad}; }
+#endif
+#if BH_BLOOM_SEPQ_WPE
+#define SEPQ_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_SEPQ_WPE)))
+#else
+#define SEPQ_BOUNDS __launch_bounds__(256)
+#endif
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
 template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>()>
-__global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
+__global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
                                                       const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
                                                       const uint2* __restrict__ same, Tex aux) {
     __shared__ Lds L;
     __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS + FP / 2];
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
     // the lanes instead of every second one (2-way bank conflicts)
-    __shared__ SepEntry colp[8][2][16], rowp[8][2][16];
+    __shared__ QEntry colp[8][2][16], rowp[8][2][16];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
@@ -742,15 +767,12 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
     for (int h = 0; h < 2; ++h) {
         const uint32_t i = (threadIdx.x >> 5) & 7u, j = threadIdx.x & 31u;
         if (h == 0) {
-            SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
-            e.f -= lo_x;
-            colp[i][j & 1u][j >> 1] = e;
+            const SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
+            colp[i][j & 1u][j >> 1] = q_entry(e.f - lo_x, 0, e);
         } else {
-            SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
+            const SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
             const int32_t ly = e.f - lo_y;
-            e.f = ly * FS + (ly >> 1);
-            e.pad = ly;
-            rowp[i][j & 1u][j >> 1] = e;
+            rowp[i][j & 1u][j >> 1] = q_entry(ly * FS + (ly >> 1), ly, e);
         }
     }
     // own texels of the epilogue (four pixels), loaded before the tables, used last
@@ -800,9 +822,9 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
                 return make_float4(v.x, v.y, v.z, A1 ? 1.0f : v.w);
             }
         };
-        auto lerp = [&](const float4& t00, const float4& t10, const float4& t01, const float4& t11, const SepEntry& c,
-                        const SepEntry& r) {
-            const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;  // sample()'s operations in its order
+        auto lerp = [&](const float4& t00, const float4& t10, const float4& t01, const float4& t11, const QEntry& c,
+                        const QEntry& r) {
+            const float ia = q_ia(c), fa = c.fa, ib = q_ia(r), fb = r.fa;  // sample()'s operations in its order
             F4 q;
             q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
             q.g = (t00.y * ia + t10.y * fa) * ib + (t01.y * ia + t11.y * fa) * fb;
@@ -813,8 +835,8 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
         F4 s[2][2];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const SepEntry cL = colp[i][0][qx], cR = colp[i][1][qx];
-            const SepEntry rT = rowp[i][0][qy], rB = rowp[i][1][qy];
+            const QEntry cL = colp[i][0][qx], cR = colp[i][1][qx];
+            const QEntry rT = rowp[i][0][qy], rB = rowp[i][1][qy];
             const int32_t dx = cR.f - cL.f, dy = rB.pad - rT.pad;  // the two columns' / rows' floor steps
             const int32_t dx0 = __builtin_amdgcn_readfirstlane(dx), dy0 = __builtin_amdgcn_readfirstlane(dy);
             const bool uni = __builtin_amdgcn_ballot_w64((dx != dx0) | (dy != dy0)) == 0ull && (dx0 == 0 || dx0 == 1) &&
@@ -874,8 +896,8 @@ __global__ void __launch_bounds__(256) up_sepq_kernel(Tables tb, CTex a, uint32_
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const SepEntry& ce = c ? cR : cL;
-                        const SepEntry& re = b ? rB : rT;
+                        const QEntry& ce = c ? cR : cL;
+                        const QEntry& re = b ? rB : rT;
                         const int32_t op = ce.f + re.f, dn = FS + (re.pad & 1);
                         acc(s[b][c], lerp(texel(op), texel(op + 1), texel(op + dn), texel(op + dn + 1), ce, re), i);
                     }
