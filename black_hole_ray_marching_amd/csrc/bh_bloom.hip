@@ -724,6 +724,11 @@ using QEntry = SepEntry;
 __device__ __forceinline__ float q_ia(const QEntry& e) { return e.ia; }
 __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry& e) { return {f, e.fa, e.ia, pad}; }
 #endif
+// The raw 60-word tile's row stride (A/B; any stride keeps the quad rows' bank parity: the next quad row
+// is 2 FS + 1 words further, an odd number).  64 instead of 80: 15 KiB of tile instead of 19
+#ifndef BH_BLOOM_SEPQ_FS60
+#define BH_BLOOM_SEPQ_FS60 80
+#endif
 #if BH_BLOOM_SEPQ_WPE
 #define SEPQ_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_SEPQ_WPE)))
 #else
@@ -2054,8 +2059,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
         return (int)hipGetLastError();
     }
     if (fq == 60) {
-        if (epi == EPI_Y) BH_SEPQ(60, EPI_Y, true, 80); else if (epi == EPI_FINAL) BH_SEPQ(60, EPI_FINAL, true, 80);
-        else BH_SEPQ(60, EPI_PLAIN, true, 80);
+        constexpr int FS60 = BH_BLOOM_SEPQ_FS60;
+        if (epi == EPI_Y) BH_SEPQ(60, EPI_Y, true, FS60); else if (epi == EPI_FINAL) BH_SEPQ(60, EPI_FINAL, true, FS60);
+        else BH_SEPQ(60, EPI_PLAIN, true, FS60);
         return (int)hipGetLastError();
     }
     const int fp = sep_tile(ext);
