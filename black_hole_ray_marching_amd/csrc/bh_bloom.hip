@@ -708,7 +708,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 // recomputed, the host plan's own operation) -- 4 KiB less LDS per block.  BH_BLOOM_SEPQ_WPE: a waves per
 // EU bound for the quad kernel (0: none).  Both A/B switches.
 #ifndef BH_BLOOM_SEPQ_E8
-#define BH_BLOOM_SEPQ_E8 0
+#define BH_BLOOM_SEPQ_E8 1
 #endif
 #ifndef BH_BLOOM_SEPQ_WPE
 #define BH_BLOOM_SEPQ_WPE 0
