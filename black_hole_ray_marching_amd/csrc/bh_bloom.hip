@@ -711,7 +711,7 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 #define BH_BLOOM_SEPQ_E8 1
 #endif
 #ifndef BH_BLOOM_SEPQ_WPE
-#define BH_BLOOM_SEPQ_WPE 0
+#define BH_BLOOM_SEPQ_WPE 6
 #endif
 #if BH_BLOOM_SEPQ_E8
 struct QEntry { int16_t f, pad; float fa; };
@@ -727,7 +727,7 @@ __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry
 // The raw 60-word tile's row stride (A/B; any stride keeps the quad rows' bank parity: the next quad row
 // is 2 FS + 1 words further, an odd number).  64 instead of 80: 15 KiB of tile instead of 19
 #ifndef BH_BLOOM_SEPQ_FS60
-#define BH_BLOOM_SEPQ_FS60 80
+#define BH_BLOOM_SEPQ_FS60 64
 #endif
 #if BH_BLOOM_SEPQ_WPE
 #define SEPQ_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_SEPQ_WPE)))
