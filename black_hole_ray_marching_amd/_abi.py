@@ -13,6 +13,7 @@ BH_ERR_UNSUPPORTED = -2
 BH_ERR_HIP = -3
 BH_ERR_NO_DEVICE = -4
 BH_ERR_OUT_OF_MEMORY = -5
+BH_ERR_INTERNAL = -6
 
 BH_OUT_RGBA32F, BH_OUT_RGBA16F, BH_OUT_BGRA8_SRGB = 0, 1, 2
 BH_BLOOM_AUTO, BH_BLOOM_LITERAL = 0, 1
@@ -112,6 +113,7 @@ SIGNATURES = {
                                        C.POINTER(C.c_int)]),
     "bh_bloom": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_void_p, C.c_void_p]),
+    "bh_bloom_check": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
     "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "bh_graph_release": (C.c_int, [C.c_void_p]),

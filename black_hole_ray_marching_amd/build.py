@@ -11,6 +11,7 @@ import os
 import shutil
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -72,14 +73,18 @@ def _stale(target: Path, deps: list[Path]) -> bool:
 def build_product(force: bool = False) -> Path:
     OBJ.mkdir(exist_ok=True)
     headers = list(CSRC.glob("*.hpp")) + [ROOT / "include" / "bh_render.h"]
-    objs = []
+    objs, jobs = [], []
     for src, flags in TU_FLAGS.items():
         s = CSRC / src
         o = OBJ / (s.stem + ".o")
         deps = [s, *headers, Path(__file__)] + ([CSRC / "bh_march_exact.hip"] if src == "bh_march_exact_lat.hip" else [])
         if force or _stale(o, deps):
-            _run([HIPCC, *COMMON, *flags, "-c", str(s), "-o", str(o)])
+            jobs.append([HIPCC, *COMMON, *flags, "-c", str(s), "-o", str(o)])
         objs.append(o)
+    # the translation units compile independently: in parallel (BH_BUILD_JOBS, default min(cpus, 8))
+    n = int(os.environ.get("BH_BUILD_JOBS", "0")) or min(os.cpu_count() or 1, 8)
+    with ThreadPoolExecutor(max_workers=max(1, n)) as ex:
+        list(ex.map(_run, jobs))
     if force or _stale(LIB, objs):
         tmp = LIB.with_suffix(".so.tmp")
         _run([HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs)])

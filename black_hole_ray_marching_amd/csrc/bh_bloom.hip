@@ -22,8 +22,11 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdarg>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <type_traits>
 #include <utility>
 
@@ -494,7 +497,8 @@ constexpr int FP_FINAL = 44;  // the last up pass at res / 4: taps within +-12 t
 // on the general sampler's texels, the same bits.  Used by the up passes whose TapPlan / Up2Plan proofs
 // fail (frame sizes other than powers of two).
 // Entry per tap and column (then per tap and row): the UNCLAMPED floor f of the sampler's coordinate t
-// (t clamped to [-1, n] as sample_coord does, so f is in [-1, n]) and the weights fa = t - f,
+// (t clamped to [-1, n] as sample_coord does, so f is in [-1, n]) and the weights fa = t - f (in [0, 1]: a t just
+// below an integer rounds t - f up to 1),
 // ia = 1 - fa.  The block stages its footprint with clamp-to-edge addressing -- tile entry (ly, lx)
 // holds texel (clamp(lo_y + ly), clamp(lo_x + lx)) -- so sample()'s texels clamp(f) and clamp(f + 1)
 // are tile entries f - lo and f + 1 - lo: a tap's four reads are one base offset plus 0, 1, FP, FP + 1.
@@ -1948,6 +1952,271 @@ int std_tap_plan(const TapPlan& P) {
     return 0;
 }
 
+// ---- host-side bound checks of the kernels' index arithmetic ------------------------------------
+// Round 4's memory-access fault ("Bound checks") was a fix-up launch with a count read
+// from a freed plan record.  Every form a launcher can take stages a block's input footprint in an LDS
+// tile and reads it at offsets that a plan (or the kernel's own sampler arithmetic) gives; these checks
+// replay that arithmetic on the host, in the kernels' own f32 operations, per block and per tap along
+// each axis (every footprint here is separable), and require every staged extent to fit its tile, every
+// tile read to fall inside the staged extent, and every plan index and list entry to fall inside its
+// texture.  A separable or same-size plan that fails is never used (the pass takes the general form:
+// bh_bloom_sep_verify / bh_bloom_same_verify, called where the host builds the plans), and in the dry
+// mode of bh_bloom_check every launch of a chain runs its form's check instead of launching (the CPU
+// test over frame sizes and levels, tests/test_bloom_bounds.py).
+namespace {
+struct DryRun {
+    uint64_t launches = 0, checks = 0;
+    std::string fail;
+};
+thread_local DryRun* g_dry = nullptr;
+// Test hook (tests/test_bloom_bounds.py): the checks treat every tile as this many entries smaller, so a
+// footprint that fills its tile exactly must be reported -- the checks' own negative test.  0 in use.
+const int g_check_slack = [] {
+    const char* e = std::getenv("BH_BLOOM_CHECK_SLACK");
+    return e ? std::atoi(e) : 0;
+}();
+thread_local std::string* g_why = nullptr;  // where a failing check writes its message (first one kept)
+
+bool chk(bool ok, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+bool chk(bool ok, const char* fmt, ...) {
+    if (g_dry) ++g_dry->checks;
+    if (ok) return true;
+    std::string* w = g_dry ? &g_dry->fail : g_why;
+    if (w && w->empty()) {
+        char buf[256];
+        va_list ap;
+        va_start(ap, fmt);
+        std::vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        *w = buf;
+    }
+    return false;
+}
+float h_texcoord(uint32_t i, uint32_t n) { return ((float)i + 0.5f) / (float)n; }
+// Taps::du / dv on the host: (hx * m) * 3 with hx = 0.5 / res
+float h_tap(uint32_t res, int axis, int i) { return ((0.5f / (float)res) * (float)tap_m(axis, i)) * 3.0f; }
+float h_tap_min(uint32_t res, int axis) { return h_tap(res, axis, axis ? 6 : 0); }
+float h_tap_max(uint32_t res, int axis) { return h_tap(res, axis, axis ? 2 : 4); }
+int32_t h_floor(float t) { return (int32_t)floorf(t); }
+
+// One axis of up_sep_kernel (B = 16) / up_sepq_kernel (B = 32): the footprint the kernel derives from the
+// sampler arithmetic of its first and last column, c = hi - lo + 2 entries (floor .. floor + 1), which the
+// kernel cuts to FP -- the cut must never happen -- and for every tap and column of the block the plan's
+// floor f with both of its texels f - lo, f + 1 - lo inside those c entries.  e: the axis's [8][on] entries.
+bool sep_axis_ok(const SepEntry* e, uint32_t on, uint32_t tn, uint32_t res, int axis, uint32_t B, int FP) {
+    const float dmin = h_tap_min(res, axis), dmax = h_tap_max(res, axis);
+    for (uint32_t b = 0; b < on; b += B) {
+        const uint32_t l = std::min(b + B - 1u, on - 1u);
+        const int32_t lo = h_floor(h_sample_coord(h_texcoord(b, on) + dmin, tn));
+        const int32_t hi = h_floor(h_sample_coord(h_texcoord(l, on) + dmax, tn));
+        const int32_t c = hi - lo + 2;
+        if (!chk(c >= 2 && c <= FP - g_check_slack, "separable %s footprint of block %u: %d entries, tile side %d", axis ? "row" : "column",
+                 b, c, FP))
+            return false;
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t x = b; x <= l; ++x) {
+                const SepEntry& s = e[(size_t)i * on + x];
+                if (!chk(s.f >= -1 && s.f <= (int32_t)tn, "separable plan floor %d outside [-1, %u] (tap %d, %s %u)", s.f,
+                         tn, i, axis ? "row" : "column", x) ||
+                    !chk(s.f - lo >= 0 && s.f + 1 - lo <= c - 1,
+                         "separable tap %d of %s %u reads entries %d..%d of a %d-entry footprint", i, axis ? "row" : "column",
+                         x, s.f - lo, s.f + 1 - lo, c) ||
+                    !chk(s.fa >= 0.0f && s.fa <= 1.0f && s.ia == 1.0f - s.fa, "separable plan weight %g at %s %u", (double)s.fa,
+                         axis ? "row" : "column", x))
+                    return false;
+            }
+    }
+    return true;
+}
+// A tile of FP rows at stride FS, with a row-pair shift of (ly + p) >> 1 entries when shift = p + 1 (the quad
+// tiles: p = 0; bloom_yq_kernel: p up to 1): its largest entry for rows and columns below FP must stay below
+// the declared size.
+bool tile_ok(int FP, int FS, int shift, int size) {
+    const int last = (FP - 1) * FS + (shift ? (FP - 1 + shift - 1) >> 1 : 0) + (FP - 1);
+    return chk(FS >= FP && last < size, "tile FP %d stride %d: last entry %d of %d", FP, FS, last, size);
+}
+
+// One axis of with_source's (and up2_kernel's outer blocks') fallback: the kernel's tap_span over a block of
+// B pixels, and, when it fits FP, every tap's two clamped texels inside it.
+bool span_axis_ok(uint32_t on, uint32_t tn, uint32_t res, int axis, uint32_t B, int FP) {
+    const float dmin = h_tap_min(res, axis), dmax = h_tap_max(res, axis);
+    const int32_t hm = (int32_t)tn - 1;
+    auto clampi_h = [&](int32_t v) { return std::min(std::max(v, 0), hm); };
+    for (uint32_t b = 0; b < on; b += B) {
+        const uint32_t l = std::min(b + B - 1u, on - 1u);
+        const int32_t lo = clampi_h(h_floor(h_sample_coord(h_texcoord(b, on) + dmin, tn)));
+        const int32_t hi = clampi_h(h_floor(h_sample_coord(h_texcoord(l, on) + dmax, tn)) + 1);
+        const int32_t n = hi - lo + 1;
+        if (n > FP) continue;  // block-uniform: this block reads global memory through clamped indices
+        if (!chk(n <= FP - g_check_slack, "staged span of %s block %u: %d texels, tile side %d", axis ? "row" : "column",
+                 b, n, FP))
+            return false;
+        for (int i = 0; i < 8; ++i)
+            for (uint32_t x = b; x <= l; ++x) {
+                const int32_t f = h_floor(h_sample_coord(h_texcoord(x, on) + h_tap(res, axis, i), tn));
+                const int32_t x0 = clampi_h(f), x1 = clampi_h(f + 1);
+                if (!chk(x0 >= lo && x1 <= hi, "staged tap %d of %s %u reads texels %d..%d of span %d..%d", i,
+                         axis ? "row" : "column", x, x0, x1, lo, hi))
+                    return false;
+            }
+    }
+    return true;
+}
+
+// One axis of a TapPlan form over blocks of B pixels and a tile of side FP: the kernel takes the form when
+// hi - lo + B <= FP (launch-uniform), and then a pixel p of a block reads entries p - b + (o_i - lo) and
+// + half_i; otherwise the span fallback.
+bool tapplan_axis_ok(const TapPlan& P, uint32_t on, uint32_t tn, uint32_t res, int axis, uint32_t B, int FP) {
+    const int32_t lo = axis ? P.lo_y : P.lo_x, hi = axis ? P.hi_y : P.hi_x;
+    if (!P.valid || hi - lo + (int32_t)B > FP) return span_axis_ok(on, tn, res, axis, B, FP);
+    if (!chk(hi - lo + (int32_t)B <= FP - g_check_slack, "tap plan footprint %d of a %d tile", hi - lo + (int32_t)B, FP))
+        return false;
+    for (int i = 0; i < 8; ++i) {
+        const int32_t o = axis ? P.oy[i] : P.ox[i];
+        const int32_t h = (int32_t)(((axis ? P.hy : P.hx) >> i) & 1u);
+        if (!chk(o - lo >= 0 && (int32_t)B - 1 + o + h - lo <= hi - lo + (int32_t)B - 1,
+                 "tap plan tap %d offset %d (+%d) outside the footprint %d..%d", i, o, h, lo, hi))
+            return false;
+    }
+    return true;
+}
+
+// One axis of up2_kernel: blocks of 32 pixels staged when the span fits FP_UPQ; inside P's interior the quad
+// reads texels (x >> 1) + o[0] .. (x >> 1) + o[1] + 1 of every tap, which must lie in the span.
+bool up2_axis_ok(const Up2Plan& P, uint32_t on, uint32_t tn, uint32_t res, int axis, int FP) {
+    if (!span_axis_ok(on, tn, res, axis, 32u, FP)) return false;
+    const float dmin = h_tap_min(res, axis), dmax = h_tap_max(res, axis);
+    const int32_t hm = (int32_t)tn - 1;
+    const int32_t ilo = axis ? P.y_lo : P.x_lo, ihi = axis ? P.y_hi : P.x_hi;
+    for (uint32_t b = 0; b < on; b += 32u) {
+        const uint32_t l = std::min(b + 31u, on - 1u);
+        const int32_t lo = std::min(std::max(h_floor(h_sample_coord(h_texcoord(b, on) + dmin, tn)), 0), hm);
+        const int32_t hi = std::min(std::max(h_floor(h_sample_coord(h_texcoord(l, on) + dmax, tn)) + 1, 0), hm);
+        if (hi - lo + 1 > FP || (int32_t)b < ilo || (int32_t)b + 31 > ihi) continue;  // not an inner block
+        for (int i = 0; i < 8; ++i) {
+            const int32_t o0 = axis ? P.oy[0][i] : P.ox[0][i], o1 = axis ? P.oy[1][i] : P.ox[1][i];
+            for (uint32_t x = b; x <= l; x += 2u) {
+                const int32_t first = (int32_t)(x >> 1) + o0, last = (int32_t)(x >> 1) + o1 + 1;
+                if (!chk(first >= lo && last <= hi && first >= 0 && last <= hm,
+                         "2:1 quad tap %d of %s %u reads texels %d..%d of span %d..%d", i, axis ? "row" : "column", x,
+                         first, last, lo, hi))
+                    return false;
+            }
+        }
+    }
+    return true;
+}
+
+// The same-size plan (bh_bloom_same_plan) and its list of inexact columns, then rows: every texel index
+// inside the frame, weights in [0, 1], and the list exactly the columns / rows of nonzero weight, ascending
+// (the fused epilogues skip those pixels and fixup_kernel recomputes them: a missing entry leaves a pixel
+// unwritten, an extra one writes it twice with the same value).
+bool same_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, uint32_t nr,
+             bool with_list = true) {
+    if (!chk(nc <= w && nr <= h, "same-size plan: %u inexact columns of %u, %u rows of %u", nc, w, nr, h)) return false;
+    for (int axis = 0; axis < 2; ++axis) {
+        const uint32_t n = axis ? h : w, base = axis ? w : 0u, cnt = axis ? nr : nc;
+        const uint32_t* L = with_list ? list + (axis ? nc : 0u) : nullptr;
+        uint32_t k = 0;
+        for (uint32_t x = 0; x < n; ++x) {
+            const uint32_t e = plan[2u * (base + x)];
+            float wgt;
+            std::memcpy(&wgt, &plan[2u * (base + x) + 1u], 4);
+            const uint32_t x0 = e & 0xFFFFu, x1 = e >> 16;
+            if (!chk(x0 < n && x1 < n && wgt >= 0.0f && wgt <= 1.0f, "same-size plan %s %u: texels %u, %u, weight %g of %u",
+                     axis ? "row" : "column", x, x0, x1, (double)wgt, n))
+                return false;
+            if (wgt != 0.0f && with_list) {
+                if (!chk(k < cnt && L[k] == x, "same-size list: %s %u missing", axis ? "row" : "column", x)) return false;
+                ++k;
+            }
+        }
+        if (with_list && !chk(k == cnt, "same-size list: %u %s entries for %u inexact", cnt, axis ? "row" : "column", k)) return false;
+    }
+    return true;
+}
+}  // namespace
+
+// The separable up pass's launch form for a plan's extents (low 16 bits: 16x16 blocks, high: 32x32): the
+// quad kernel when its footprint fits a 28 / 40 / 60 tile, else the one-pixel kernel at 24 / 44, else none
+// (FP 0: the general pass).  One definition for the launcher and its check.
+struct SepForm {
+    int FP = 0, FS = 0;
+    bool quad = false, raw = false;
+};
+static const bool g_no_sepq = std::getenv("BH_BLOOM_NO_SEPQ") != nullptr;  // A/B: the one-pixel kernel
+static uint32_t env_u32(const char* name) {
+    const char* e = std::getenv(name);
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+}
+static SepForm sep_form(int ext, uint32_t ow, uint32_t oh) {
+    // A/B: BH_BLOOM_SEPQ_MIN_BLOCKS=n runs a pass of fewer than n quad blocks (32x32 pixels) with the
+    // one-pixel kernel (four times the blocks) when its footprint fits; BH_BLOOM_SEPQ_RAW bit 0 / bit 1
+    // stage the 28 / 40 tiles as raw words too (decoded per read)
+    static const uint32_t min_blocks = env_u32("BH_BLOOM_SEPQ_MIN_BLOCKS"), raw_mask = env_u32("BH_BLOOM_SEPQ_RAW");
+    const int e16 = ext & 0xFFFF, e32 = (ext >> 16) & 0xFFFF;
+    const int one = e16 <= 0 ? 0 : e16 <= 24 ? 24 : e16 <= 44 ? 44 : 0;
+    int q = g_no_sepq || e32 <= 0 ? 0 : e32 <= 28 ? 28 : e32 <= 40 ? 40 : e32 <= 60 ? 60 : 0;
+    const uint64_t qblocks = (uint64_t)((ow + 31u) / 32u) * ((oh + 31u) / 32u);
+    if (qblocks < min_blocks && one != 0) q = 0;
+    SepForm f;
+    if (q != 0) {
+        f.quad = true;
+        f.FP = q;
+        f.raw = q == 60 || (q == 28 && (raw_mask & 1u)) || (q == 40 && (raw_mask & 2u));
+        f.FS = f.raw ? (q == 60 ? BH_BLOOM_SEPQ_FS60 : 48) : (q == 28 ? 32 : 40);
+    } else if (one != 0) {
+        f.FP = one;
+        f.raw = one == 44;
+        f.FS = f.raw ? sep_stride<44, true>() : sep_stride<24, false>();
+    }
+    return f;
+}
+
+// bh_bloom_sep_plan's plan (host copy `plan`, extents `ext`) checked for the form bh_launch_bloom_sep takes:
+// false (and the reason in *why) when any block's footprint exceeds its tile or any read leaves it.
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_verify(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                        uint32_t th, uint32_t rx, uint32_t ry,
+                                                                        const uint32_t* plan, int ext, std::string* why) {
+    std::string* prev = g_why;
+    g_why = why;
+    const SepForm f = sep_form(ext, ow, oh);
+    const SepEntry* e = reinterpret_cast<const SepEntry*>(plan);
+    const uint32_t B = f.quad ? 32u : 16u;
+    const int size = f.quad ? f.FP * f.FS + f.FP / 2 : f.FP * f.FS;
+    // FP == 0: no staged form fits these extents, and the launcher refuses the plan (the general pass runs)
+    const bool ok = f.FP == 0 || (tile_ok(f.FP, f.FS, f.quad ? 1 : 0, size) && sep_axis_ok(e, ow, tw, rx, 0, B, f.FP) &&
+                                  sep_axis_ok(e + 8u * (size_t)ow, oh, th, ry, 1, B, f.FP));
+    g_why = prev;
+    return ok;
+}
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                         uint32_t nc, uint32_t nr, std::string* why) {
+    std::string* prev = g_why;
+    g_why = why;
+    const bool ok = same_ok(w, h, plan, plan + 2u * ((size_t)w + h), nc, nr);
+    g_why = prev;
+    return ok;
+}
+// Dry mode (bh_bloom_check): while it is on, the launchers below check their launch's form on the host and
+// return without launching; the plan pointers they receive are host copies.
+extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void) {
+    delete g_dry;
+    g_dry = new DryRun();
+}
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry_end(uint64_t* launches, uint64_t* checks,
+                                                                     std::string* fail) {
+    if (!g_dry) return false;
+    if (launches) *launches = g_dry->launches;
+    if (checks) *checks = g_dry->checks;
+    if (fail) *fail = g_dry->fail;
+    const bool ok = g_dry->fail.empty();
+    delete g_dry;
+    g_dry = nullptr;
+    return ok;
+}
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry(void) { return g_dry != nullptr; }
+
 // The separable plan of an 8-tap pass (see SepEntry / up_sep_kernel): 8 * (ow + oh) entries of 4 words
 // into `outp` (per tap and column, then per tap and row), from the kernel's own f32 arithmetic: texcoord
 // (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset, sample_coord and
@@ -1995,17 +2264,6 @@ extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t 
     return std::min(ext[0], 0x7FFF) | std::min(ext[1], 0x7FFF) << 16;  // up_sep_kernel's | up_sepq_kernel's
 }
 
-// The staged tile side of up_sep_kernel for a plan's footprint extent, or 0 (too large: the general pass)
-static int sep_tile(int ext) {
-    ext &= 0xFFFF;
-    return ext <= 0 ? 0 : ext <= 24 ? 24 : ext <= 44 ? 44 : 0;
-}
-// the quad kernel's staged side for the 32x32 block extent, or 0 (the one-pixel kernel); BH_BLOOM_NO_SEPQ: A/B
-static const bool g_no_sepq = std::getenv("BH_BLOOM_NO_SEPQ") != nullptr;
-static int sepq_tile(int ext) {
-    ext = (ext >> 16) & 0xFFFF;
-    return g_no_sepq || ext <= 0 ? 0 : ext <= 28 ? 28 : ext <= 40 ? 40 : ext <= 60 ? 60 : 0;
-}
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
                                                                         const uint8_t* buckets, const uint32_t* codes,
                                                                         const uint32_t* a, uint32_t aw, uint32_t ah,
@@ -2014,66 +2272,46 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
                                                                         uint32_t ow, uint32_t oh, hipStream_t s) {
+    const SepForm f = sep_form(ext, ow, oh);
+    if (f.FP == 0 || !sep) return (int)hipErrorInvalidValue;
+    if (g_dry) {  // the plan is a host copy: check the form's every read instead of launching
+        ++g_dry->launches;
+        return bh_bloom_sep_verify(ow, oh, aw, ah, rx, ry, sep, ext, nullptr) &&
+                       (epi == EPI_PLAIN || chk(same != nullptr, "separable epilogue without a same-size plan"))
+                   ? 0
+                   : (int)hipErrorInvalidValue;
+    }
     const Tables tb{lut, enc, buckets, codes};
     const CTex A{a, aw, ah}, O0{own0 ? own0 : a, ow, oh}, O1{own1 ? own1 : a, ow, oh};
     const SepEntry* P = reinterpret_cast<const SepEntry*>(sep);
     const uint2* S = reinterpret_cast<const uint2*>(same);
     const Tex O{out, ow, oh}, X{aux ? aux : out, ow, oh};
-    const dim3 g = grid_for(ow, oh);
+    const dim3 g = grid_for(ow, oh), gq((ow + 31u) / 32u, (oh + 31u) / 32u);
 #define BH_SEP(FP, E, RAW) \
     hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
 #define BH_SEPQ(FP, E, RAW, FS) \
     hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
-    // A/B: BH_BLOOM_SEPQ_MIN_BLOCKS=n runs a pass of fewer than n quad blocks (32x32 pixels) with the
-    // one-pixel kernel (four times the blocks) when its footprint fits
-    static const uint32_t min_blocks = [] {
-        const char* e = std::getenv("BH_BLOOM_SEPQ_MIN_BLOCKS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-    }();
-    const dim3 gq((ow + 31u) / 32u, (oh + 31u) / 32u);
-    const int fq = gq.x * gq.y < min_blocks && sep_tile(ext) != 0 ? 0 : sepq_tile(ext);
-    // A/B: BH_BLOOM_SEPQ_RAW bit 0 / bit 1 stage the 28 / 40 tiles as raw words too (decoded per read;
-    // 4x less LDS per block, so more blocks per CU, for 4 table reads per texel read)
-    static const uint32_t raw_mask = [] {
-        const char* e = std::getenv("BH_BLOOM_SEPQ_RAW");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
-    }();
-    if (fq == 28 && (raw_mask & 1u)) {
-        if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, true, 48); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, true, 48);
-        else BH_SEPQ(28, EPI_PLAIN, true, 48);
-        return (int)hipGetLastError();
-    }
-    if (fq == 40 && (raw_mask & 2u)) {
-        if (epi == EPI_Y) BH_SEPQ(40, EPI_Y, true, 48); else if (epi == EPI_FINAL) BH_SEPQ(40, EPI_FINAL, true, 48);
-        else BH_SEPQ(40, EPI_PLAIN, true, 48);
-        return (int)hipGetLastError();
-    }
-    if (fq == 28) {
-        if (epi == EPI_Y) BH_SEPQ(28, EPI_Y, false, 32); else if (epi == EPI_FINAL) BH_SEPQ(28, EPI_FINAL, false, 32);
-        else BH_SEPQ(28, EPI_PLAIN, false, 32);
-        return (int)hipGetLastError();
-    }
-    if (fq == 40) {
-        if (epi == EPI_Y) BH_SEPQ(40, EPI_Y, false, 40); else if (epi == EPI_FINAL) BH_SEPQ(40, EPI_FINAL, false, 40);
-        else BH_SEPQ(40, EPI_PLAIN, false, 40);
-        return (int)hipGetLastError();
-    }
-    if (fq == 60) {
-        constexpr int FS60 = BH_BLOOM_SEPQ_FS60;
-        if (epi == EPI_Y) BH_SEPQ(60, EPI_Y, true, FS60); else if (epi == EPI_FINAL) BH_SEPQ(60, EPI_FINAL, true, FS60);
-        else BH_SEPQ(60, EPI_PLAIN, true, FS60);
-        return (int)hipGetLastError();
-    }
-    const int fp = sep_tile(ext);
-    if (fp == 24) {
-        if (epi == EPI_Y) BH_SEP(24, EPI_Y, false); else if (epi == EPI_FINAL) BH_SEP(24, EPI_FINAL, false);
-        else BH_SEP(24, EPI_PLAIN, false);
-    } else if (fp == 44) {
-        if (epi == EPI_Y) BH_SEP(44, EPI_Y, true); else if (epi == EPI_FINAL) BH_SEP(44, EPI_FINAL, true);
-        else BH_SEP(44, EPI_PLAIN, true);
-    } else {
-        return (int)hipErrorInvalidValue;
-    }
+#define BH_EPI(LAUNCH, ...)                                                    \
+    do {                                                                       \
+        if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                       \
+        else if (epi == EPI_FINAL) LAUNCH(__VA_ARGS__, EPI_FINAL, _);          \
+        else LAUNCH(__VA_ARGS__, EPI_PLAIN, _);                                \
+    } while (0)
+#define BH_Q(FPv, RAWv, FSv, E, _) BH_SEPQ(FPv, E, RAWv, FSv)
+#define BH_1(FPv, RAWv, E, _) BH_SEP(FPv, E, RAWv)
+    // the instantiations sep_form can name (its FS follows from FP and raw)
+    if (f.quad && f.FP == 28 && f.raw) BH_EPI(BH_Q, 28, true, 48);
+    else if (f.quad && f.FP == 40 && f.raw) BH_EPI(BH_Q, 40, true, 48);
+    else if (f.quad && f.FP == 28) BH_EPI(BH_Q, 28, false, 32);
+    else if (f.quad && f.FP == 40) BH_EPI(BH_Q, 40, false, 40);
+    else if (f.quad && f.FP == 60) BH_EPI(BH_Q, 60, true, BH_BLOOM_SEPQ_FS60);
+    else if (f.FP == 24) BH_EPI(BH_1, 24, false);
+    else if (f.FP == 44) BH_EPI(BH_1, 44, true);
+    else return (int)hipErrorInvalidValue;
+#undef BH_1
+#undef BH_Q
+#undef BH_EPI
+#undef BH_SEPQ
 #undef BH_SEP
     return (int)hipGetLastError();
 }
@@ -2086,8 +2324,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
                                                                           uint32_t h, hipStream_t s) {
-    if (n_cols > w || n_rows > h || !list) return (int)hipErrorInvalidValue;  // the list of this frame's plan
+    if (n_cols > w || n_rows > h || !list || !same) return (int)hipErrorInvalidValue;  // the list of this frame's plan
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
+    if (g_dry) {
+        ++g_dry->launches;
+        return same_ok(w, h, same, list, n_cols, n_rows) && chk(list == same + 2u * ((size_t)w + h), "fix-up list "
+                                                                "is not its plan's")
+                   ? 0
+                   : (int)hipErrorInvalidValue;
+    }
     if (n == 0) return 0;
     const Tables tb{lut, enc, buckets, codes};
     const dim3 g((uint32_t)((n + 255u) / 256u));
@@ -2116,6 +2361,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const
                                                                           uint32_t mw, uint32_t mh, uint32_t* out,
                                                                           uint32_t ow, uint32_t oh, hipStream_t s) {
     if (mw == 0u || mh == 0u) return (int)hipErrorInvalidValue;
+    if (g_dry) {  // every index of down2_kernel is clamped to its texture (down_at): only the sizes to check
+        ++g_dry->launches;
+        return chk(aw > 0u && ah > 0u && ow > 0u && oh > 0u, "down2 of an empty texture") ? 0 : (int)hipErrorInvalidValue;
+    }
     hipLaunchKernelGGL(down2_kernel, grid_for(ow, oh), dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{a, aw, ah},
                        mw, mh, Tex{out, ow, oh});
     return (int)hipGetLastError();
@@ -2123,8 +2372,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const
 
 // The same-size plan of a w x h frame (remix_plan_kernel): per column, then per row, the two clamped
 // texels and the weight of a sample at the pixel's own texcoord ((x + 0.5) / n, sample_coord, floor).
+// Texel indices are 16-bit fields: w, h <= 65536.
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_plan(uint32_t w, uint32_t h, uint32_t* outp) {
-    if (w > 65535u || h > 65535u || w == 0u || h == 0u) return false;
+    if (w > 65536u || h > 65536u || w == 0u || h == 0u) return false;
     auto axis = [](uint32_t n, uint32_t x, uint32_t* o) {
         const float t = h_sample_coord(((float)x + 0.5f) / (float)n, n);
         const float f = floorf(t), wgt = t - f;
@@ -2144,6 +2394,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(
                                                                                const uint32_t* b, const uint32_t* plan,
                                                                                uint32_t* out, uint32_t w, uint32_t h,
                                                                                hipStream_t s) {
+    if (g_dry) {  // the plan's texel indices (host copy)
+        ++g_dry->launches;
+        return chk(plan != nullptr, "remix without a plan") && same_ok(w, h, plan, nullptr, 0u, 0u, false) ? 0
+                                                                                                                : (int)hipErrorInvalidValue;
+    }
     hipLaunchKernelGGL(remix_plan_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
                        CTex{a, w, h}, CTex{b, w, h}, reinterpret_cast<const uint2*>(plan), Tex{out, w, h});
     return (int)hipGetLastError();
@@ -2155,6 +2410,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan
                                                                                 const uint32_t* Bt, const uint32_t* plan,
                                                                                 uint32_t* out, uint32_t w, uint32_t h,
                                                                                 hipStream_t s) {
+    if (g_dry) {  // the plan's texel indices (host copy)
+        ++g_dry->launches;
+        return chk(plan != nullptr, "remix without a plan") && same_ok(w, h, plan, nullptr, 0u, 0u, false) ? 0
+                                                                                                       : (int)hipErrorInvalidValue;
+    }
     hipLaunchKernelGGL(remix2_plan_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
                        CTex{col, w, h}, CTex{Y, w, h}, CTex{Bt, w, h}, reinterpret_cast<const uint2*>(plan),
                        Tex{out, w, h});
@@ -2196,9 +2456,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     const CTex A{a, aw, ah}, B{b ? b : a, aw, ah};
     const Tex O{out, ow, oh};
     const TapPlan P = shader == SH_UP ? tap_plan(ow, oh, aw, ah, rx, ry) : TapPlan{};
-    const uint32_t pm = shader == SH_UP && !P.valid ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
+    const uint32_t pm = shader == SH_UP && !P.valid && !g_dry ? bh_bloom_point_mask(ow, oh, aw, ah, rx, ry) : 0u;
     if (shader == SH_UP && !P.valid && !g_no_up2) {
         const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
+        if (Q.valid && g_dry) {
+            ++g_dry->launches;
+            const bool ok = tile_ok(FP_UPQ, FS_UPQ, 0, FP_UPQ * FS_UPQ) && up2_axis_ok(Q, ow, aw, rx, 0, FP_UPQ) &&
+                            up2_axis_ok(Q, oh, ah, ry, 1, FP_UPQ);
+            return ok ? 0 : (int)hipErrorInvalidValue;
+        }
         if (Q.valid) {
             const dim3 g((ow + 31u) / 32u, (oh + 31u) / 32u);
             switch (std_up2_plan(Q)) {
@@ -2209,9 +2475,17 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
             return (int)hipGetLastError();
         }
     }
-    if (shader == SH_UP && !P.valid && sep && sep_tile(sep_ext) != 0 && !g_no_sep) {
+    if (shader == SH_UP && !P.valid && sep && sep_form(sep_ext, ow, oh).FP != 0 && !g_no_sep) {
         return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, rx, ry, sep, sep_ext, EPI_PLAIN, nullptr, nullptr,
                                    nullptr, out, nullptr, ow, oh, s);
+    }
+    if (g_dry) {  // pass_kernel: an up pass stages through with_source<FP_UP>; the others read clamped indices
+        ++g_dry->launches;
+        const bool ok = chk(aw > 0u && ah > 0u && ow > 0u && oh > 0u, "pass over an empty texture") &&
+                        (shader != SH_UP || (tile_ok(FP_UP, FP_UP, 0, FP_UP * FP_UP) &&
+                                             tapplan_axis_ok(P, ow, aw, rx, 0, 16u, FP_UP) &&
+                                             tapplan_axis_ok(P, oh, ah, ry, 1, 16u, FP_UP)));
+        return ok ? 0 : (int)hipErrorInvalidValue;
     }
     switch (shader) {
         case SH_COPY: hipLaunchKernelGGL(pass_kernel<SH_COPY>, grid_for(ow, oh), dim3(256), 0, s, tb, A, B, rx, ry, pm, P, O); break;
@@ -2228,7 +2502,16 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const flo
                                                                       uint32_t h, hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, w, h);
     static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
-    if (P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ) {
+    const bool quad = P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ;
+    if (g_dry) {  // the quad form's tile (row-pair shift) or with_source<FP_Y>
+        ++g_dry->launches;
+        const bool ok = quad ? tile_ok(FP_YQ, FS_YQ, 2, FP_YQ * FS_YQ + FP_YQ / 2 + 1) &&
+                                   tapplan_axis_ok(P, w, w, w, 0, 32u, FP_YQ) && tapplan_axis_ok(P, h, h, h, 1, 32u, FP_YQ)
+                             : tile_ok(FP_Y, FP_Y, 0, FP_Y * FP_Y) && tapplan_axis_ok(P, w, w, w, 0, 16u, FP_Y) &&
+                                   tapplan_axis_ok(P, h, h, h, 1, 16u, FP_Y);
+        return ok ? 0 : (int)hipErrorInvalidValue;
+    }
+    if (quad) {
         const dim3 g((w + 31u) / 32u, (h + 31u) / 32u);
         if (std_tap_plan(P) == 12)
             hipLaunchKernelGGL(bloom_yq_kernel<12>, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P,
@@ -2251,6 +2534,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
                                                                           uint32_t* out, uint32_t w, uint32_t h,
                                                                           hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, rx, ry);
+    if (g_dry) {  // with_source<FP_FINAL>: the TapPlan form (raw words) or the span fallback
+        ++g_dry->launches;
+        const bool ok = tile_ok(FP_FINAL, FP_FINAL, 0, FP_FINAL * FP_FINAL) &&
+                        tapplan_axis_ok(P, w, w, rx, 0, 16u, FP_FINAL) && tapplan_axis_ok(P, h, h, ry, 1, 16u, FP_FINAL);
+        return ok ? 0 : (int)hipErrorInvalidValue;
+    }
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, rx, ry);
     // the kernel's with_source takes the TapPlan form exactly when this holds (raw words staged)
     const bool plan = P.valid && P.hi_x - P.lo_x + 16 <= FP_FINAL && P.hi_y - P.lo_y + 16 <= FP_FINAL;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/bh_render.h"
 
 namespace bh {
@@ -279,6 +281,18 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan
                                                                                 const uint32_t* Bt, const uint32_t* plan,
                                                                                 uint32_t* out, uint32_t w, uint32_t h,
                                                                                 hipStream_t s);
+// host-side bound checks of the bloom kernels' index arithmetic (bh_bloom.hip): a separable plan for the form
+// bh_launch_bloom_sep takes, a same-size plan with its fix-up list; false with the first violation in *why.
+// Dry mode (bh_bloom_check): between begin and end the bloom launchers check their launch instead of launching.
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_verify(uint32_t ow, uint32_t oh, uint32_t tw,
+                                                                        uint32_t th, uint32_t rx, uint32_t ry,
+                                                                        const uint32_t* plan, int ext, std::string* why);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                         uint32_t nc, uint32_t nr, std::string* why);
+extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry_end(uint64_t* launches, uint64_t* checks,
+                                                                     std::string* fail);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry(void);
 // whether bh_launch_bloom_pass runs an up pass of this shape from its separable plan (bh_bloom.hip)
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_up_uses_sep(uint32_t ow, uint32_t oh, uint32_t aw,
                                                                          uint32_t ah, uint32_t rx, uint32_t ry);

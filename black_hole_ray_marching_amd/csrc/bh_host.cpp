@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <new>
 #include <string>
 #include <thread>
@@ -67,7 +68,14 @@ struct bh_ctx {
     // stream capture is never evicted (bh_graph_release clears the mark); others are evicted least
     // recently used beyond BH_BLOOM_SETS.
     // ext: the largest block footprint side (up passes); nc, nr: the inexact columns / rows (same plan)
-    struct SepPlan { std::array<uint32_t, 6> key; uint32_t* dev; int ext; uint32_t nc, nr; };
+    // host: the plan's host copy in bh_bloom_check's dry mode (dev then points into it; never freed as device memory)
+    struct SepPlan {
+        std::array<uint32_t, 6> key{};
+        uint32_t* dev = nullptr;
+        int ext = 0;
+        uint32_t nc = 0, nr = 0;
+        std::shared_ptr<std::vector<uint32_t>> host;
+    };
     struct BloomScratch {
         uint64_t key = 0;
         std::vector<uint32_t*> tex;
@@ -97,7 +105,8 @@ static std::atomic<uint64_t> g_partition_serial{0};
 static void free_frame_table(bh_ctx::FrameTable& t);
 static void free_bloom_scratch(bh_ctx::BloomScratch& b) {
     for (uint32_t* t : b.tex) (void)hipFree(t);
-    for (auto& p : b.sep_plans) (void)hipFree(p.dev);
+    for (auto& p : b.sep_plans)
+        if (!p.host) (void)hipFree(p.dev);
     b.tex.clear();
     b.sep_plans.clear();
 }
@@ -306,6 +315,7 @@ const char* bh_status_string(int st) {
         case BH_ERR_HIP: return "HIP runtime error";
         case BH_ERR_NO_DEVICE: return "no HIP device";
         case BH_ERR_OUT_OF_MEMORY: return "out of device memory";
+        case BH_ERR_INTERNAL: return "internal consistency check failed";
         default: return "unknown status";
     }
 }
@@ -670,48 +680,73 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 }
 
 // The separable plan of an up pass of this shape (bh_bloom_sep_plan), on the device, built at its first
-// use and kept with the scratch set (64 B per column and row); NULL if the shape does not fit the plan.
-// rx == 0: the same-size plan of the remixes (bh_bloom_same_plan, 8 B per column and row) followed by the
-// list of its inexact columns, then rows (the fused epilogues' fix-up pixels).  A capturing call never
-// builds one (bh_bloom refuses a set not prepared outside capture).
-// Returned by value (dev == nullptr on failure): the cache is a vector that later plans may reallocate.
-bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th,
-                         uint32_t rx, uint32_t ry, int* err) {
+// use and kept with the scratch set (64 B per column and row).  rx == 0: the same-size plan of the remixes
+// (bh_bloom_same_plan, 8 B per column and row) followed by the list of its inexact columns, then rows (the
+// fused epilogues' fix-up pixels).  Every plan is checked on the host before it is uploaded
+// (bh_bloom_sep_verify / bh_bloom_same_verify: every block footprint inside its LDS tile, every read and
+// index inside its tile and texture); a shape the builder refuses (texture sides above 65536) or whose
+// check fails gets a plan with dev == nullptr, cached like the others, and its pass runs the general
+// kernel -- with `dry_fail` (bh_bloom_check) a failed check is reported there instead.  In dry mode the
+// plan stays on the host (dev points into `host`).  A capturing call never builds one (bh_bloom refuses a
+// set not prepared outside capture).
+// Returned by value: the cache is a vector that later plans reallocate.  (Round 4's memory-access fault:
+// a pointer into it, held across the next call, read a freed record's fix-up counts)
+bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* dry_fail, uint32_t ow, uint32_t oh,
+                         uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry, int* err) {
     const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
     for (const auto& p : b->sep_plans)
         if (p.key == key) return p;
+    bh_ctx::SepPlan P;
+    P.key = key;
     if (capturing) {
         *err = (int)hipErrorStreamCaptureUnsupported;
-        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
+        return P;
     }
-    bh_ctx::SepPlan P{key, nullptr, 0, 0u, 0u};
-    std::vector<uint32_t> h;
+    auto h = std::make_shared<std::vector<uint32_t>>();
+    std::string why;
+    bool ok;
     if (rx) {
-        h.resize(32u * ((size_t)ow + oh));
-        P.ext = bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h.data());
+        h->resize(32u * ((size_t)ow + oh));
+        P.ext = bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h->data());
+        ok = P.ext >= 0 && bh_bloom_sep_verify(ow, oh, tw, th, rx, ry, h->data(), P.ext, &why);
     } else {
-        h.resize(2u * ((size_t)ow + oh));
-        P.ext = bh_bloom_same_plan(ow, oh, h.data()) ? 1 : -1;
-        std::vector<uint32_t> cols, rows;
-        for (uint32_t x = 0; x < ow; ++x)
-            if (h[2u * x + 1u] != 0u) cols.push_back(x);
-        for (uint32_t y = 0; y < oh; ++y)
-            if (h[2u * ((size_t)ow + y) + 1u] != 0u) rows.push_back(y);
-        P.nc = (uint32_t)cols.size();
-        P.nr = (uint32_t)rows.size();
-        h.insert(h.end(), cols.begin(), cols.end());
-        h.insert(h.end(), rows.begin(), rows.end());
+        h->resize(2u * ((size_t)ow + oh));
+        ok = bh_bloom_same_plan(ow, oh, h->data());
+        if (ok) {
+            std::vector<uint32_t> cols, rows;
+            for (uint32_t x = 0; x < ow; ++x)
+                if ((*h)[2u * x + 1u] != 0u) cols.push_back(x);
+            for (uint32_t y = 0; y < oh; ++y)
+                if ((*h)[2u * ((size_t)ow + y) + 1u] != 0u) rows.push_back(y);
+            P.nc = (uint32_t)cols.size();
+            P.nr = (uint32_t)rows.size();
+            h->insert(h->end(), cols.begin(), cols.end());
+            h->insert(h->end(), rows.begin(), rows.end());
+            ok = bh_bloom_same_verify(ow, oh, h->data(), P.nc, P.nr, &why);
+        }
     }
-    if (P.ext < 0) {
-        *err = (int)hipErrorInvalidValue;
-        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
+    if (!ok) {
+        if (dry_fail && !why.empty() && dry_fail->empty())
+            *dry_fail = "plan " + std::to_string(ow) + "x" + std::to_string(oh) + " <- " + std::to_string(tw) + "x" +
+                        std::to_string(th) + " res " + std::to_string(rx) + "x" + std::to_string(ry) + ": " + why;
+        bh_ctx::SepPlan none;
+        none.key = key;
+        b->sep_plans.push_back(none);
+        return none;
     }
-    hipError_t e = hipMalloc(&P.dev, h.size() * sizeof(uint32_t));
-    if (e == hipSuccess) e = hipMemcpy(P.dev, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        if (P.dev) (void)hipFree(P.dev);
-        *err = (int)e;
-        return bh_ctx::SepPlan{key, nullptr, 0, 0u, 0u};
+    if (dry_fail) {
+        P.host = h;
+        P.dev = h->data();
+    } else {
+        hipError_t e = hipMalloc(&P.dev, h->size() * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMemcpy(P.dev, h->data(), h->size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            if (P.dev) (void)hipFree(P.dev);
+            *err = (int)e;
+            bh_ctx::SepPlan none;
+            none.key = key;
+            return none;
+        }
     }
     b->sep_plans.push_back(P);
     return P;
@@ -722,13 +757,14 @@ struct BloomRun {
     bh_ctx::BloomScratch* B;
     bool capturing;
     hipStream_t s;
+    std::string* dry_fail;  // bh_bloom_check's dry mode: plans on the host, launches checked, not launched
     int err = 0;
     void pass(uint32_t sh, const uint32_t* a, uint32_t aw, uint32_t ah, const uint32_t* b, const uint32_t* res,
               uint32_t* out, uint32_t ow, uint32_t oh) {
         if (err != 0) return;
         bh_ctx::SepPlan sp{};
         if (sh == bh_bloom_shader_up && bh_bloom_up_uses_sep(ow, oh, aw, ah, res[0], res[1]))
-            sp = sep_plan(B, capturing, ow, oh, aw, ah, res[0], res[1], &err);
+            sp = sep_plan(B, capturing, dry_fail, ow, oh, aw, ah, res[0], res[1], &err);
         if (err == 0)
             err = bh_launch_bloom_pass(sh, c->lut, c->enc, c->enc_b, c->enc_e, a, aw, ah, b, res[0], res[1], out, ow, oh,
                                        sp.dev, sp.ext, s);
@@ -754,6 +790,126 @@ struct BloomRun {
     }
 };
 
+// bh_bloom's chain on scratch set B: the reference's passes one by one (literal) or the fused forms.
+// dry_fail (bh_bloom_check): the plans stay on the host and the launchers check their launch instead of
+// launching (bh_bloom.hip dry mode); the scratch pointers are then placeholders that nothing dereferences.
+int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string* dry_fail, const void* col,
+                const void* blackout, uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, void* out,
+                hipStream_t s) {
+    const BloomPlan P = bloom_plan(W, H, levels);
+    // AUTO: the fused chain when every same-size sample is exact (powers of two); the general fused chain
+    // when they are proven identities on stored texels (same_size_identity: the copies vanish, the remixes
+    // still sample through the same-size plan); else the literal pass list
+    const uint32_t wl = P.res[levels - 1][0], hl = P.res[levels - 1][1];
+    const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) && same_size_exact(wl) &&
+                       same_size_exact(hl);
+    const bool general = schedule == BH_BLOOM_AUTO && !fused && same_size_identity(W, H) && same_size_identity(wl, hl);
+    bh_ctx::SepPlan same;
+    uint32_t** T = B->tex.data();
+    uint32_t **copy_in = T, **remix_in0 = T + levels, **remix_in1 = T + 2 * levels;
+    uint32_t* blur_in = T[3 * levels];
+    uint32_t* final_in1 = T[3 * levels + 1];
+    uint32_t **down = T + 3 * levels + 2, **up = T + 4 * levels + 2;
+    const uint32_t* X = (const uint32_t*)blackout;
+    const uint32_t* C = (const uint32_t*)col;
+    uint32_t* O = (uint32_t*)out;
+    const uint32_t full[2] = {W, H};
+    BloomRun R{c, B, capturing, s, dry_fail};
+    const uint32_t L = levels - 1;
+    if (fused) {
+        // same-size passes are identities (same_size_identity): see bh_bloom.hip
+        const uint32_t* S = X;
+        if (levels > 1) {
+            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
+            S = copy_in[1];
+        }
+        const uint32_t* u_src = R.downs(S, levels, down, P);  // down[0] == S; up[levels-1] == down[levels-1]
+        for (uint32_t l = 0; l + 1 < levels; ++l) {
+            const uint32_t ti = levels - l - 2;
+            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
+                   P.res[ti][0], P.res[ti][1]);
+            u_src = up[ti];
+        }
+        if (R.err == 0)
+            R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, c->enc_e, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
+    } else if (general && (same = sep_plan(B, capturing, dry_fail, W, H, W, H, 0u, 0u, &R.err), same.dev != nullptr)) {
+        // general fused chain (same-size passes are identities, same_size_identity): U1 = up(X) at full
+        // size, Y = remix(X, U1) through the same-size plan, the blur's downsamples and upsamples from Y,
+        // B = its last up pass, out = remix(col, q(remix(Y, B))) through the plan.  The two full-size
+        // up passes with a separable plan carry the remixes as epilogues for the pixels whose column and
+        // row sample exactly (bh_bloom.hip up_sep_kernel, EPI_Y / EPI_FINAL) and a fix-up pass covers the
+        // inexact columns and rows; other plans run the plain pass and the plan remix kernels.
+        const uint32_t* plan = same.dev;
+        const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
+        // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
+        // fix-up of the inexact pixels -- or the plain pass and the remix kernel
+        auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
+                            uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
+            if (R.err != 0) return;
+            bh_ctx::SepPlan sp{};
+            if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
+                sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err);
+            if (R.err != 0) return;
+            if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
+                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, s) == 0) {
+                R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
+                                              plan, list, same.nc, same.nr, dst, W, H, s);
+                return;
+            }
+            R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);
+            if (R.err != 0) return;
+            R.err = epi == 1u ? bh_launch_bloom_remix_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, aux, plan, dst, W, H, s)
+                              : bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, own1, aux, plan, dst,
+                                                            W, H, s);
+        };
+        const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
+        if (levels > 1) {
+            fused_up(1u, X, W, H, full, remix_in1[0], X, nullptr, copy_in[1]);
+            S = copy_in[1];
+        }
+        const uint32_t* u_src = R.downs(S, levels, down, P);
+        for (uint32_t l = 0; l + 1 < levels; ++l) {
+            const uint32_t ti = levels - l - 2;
+            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
+                   P.res[ti][0], P.res[ti][1]);
+            u_src = up[ti];
+        }
+        const uint32_t uw = levels > 1 ? P.res[0][0] : W, uh = levels > 1 ? P.res[0][1] : H;  // up[0] is W x H
+        fused_up(2u, u_src, uw, uh, P.res[L], remix_in1[L], C, S, O);
+    } else if (R.err == 0) {
+        // literal: the reference's render passes in order (also the general chain's fallback when the host
+        // refuses its same-size plan) (oracle/bh_bloom_oracle.c, bho_bloom)
+        hipError_t e;
+        if (!dry_fail && (e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync(bloom)");
+        auto blur = [&](uint32_t lv, uint32_t* dst) {
+            // blurs[k] with `lv` levels; its input (down[0]) was written by the copy pass
+            for (uint32_t l = 1; l < lv; ++l)
+                R.pass(bh_bloom_shader_down, down[l - 1], P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1],
+                       down[l], P.res[l][0], P.res[l][1]);
+            R.pass(bh_bloom_shader_down, down[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1], nullptr, P.res[lv - 1],
+                   up[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1]);
+            for (uint32_t l = 0; l + 1 < lv; ++l)
+                R.pass(bh_bloom_shader_up, up[lv - l - 1], P.res[lv - l - 1][0], P.res[lv - l - 1][1], nullptr, P.res[l],
+                       up[lv - l - 2], P.res[lv - l - 2][0], P.res[lv - l - 2][1]);
+            R.pass(bh_bloom_shader_up, up[0], W, H, nullptr, P.res[lv - 1], dst, W, H);
+        };
+        for (uint32_t level = 0; level + 1 < levels; ++level) {
+            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, down[0], W, H);
+            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, remix_in0[0], W, H);
+            blur(1, remix_in1[0]);
+            R.pass(bh_bloom_shader_remix, remix_in0[0], W, H, remix_in1[0], full, copy_in[level + 1], W, H);
+        }
+        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, down[0], W, H);
+        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, remix_in0[L], W, H);
+        blur(levels, remix_in1[L]);
+        R.pass(bh_bloom_shader_remix, remix_in0[L], W, H, remix_in1[L], full, final_in1, W, H);
+        R.pass(bh_bloom_shader_remix, C, W, H, final_in1, full, O, W, H);
+        (void)blur_in;
+    }
+    if (R.err != 0) return hip_fail((hipError_t)R.err, "bloom launch");
+    return BH_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -769,13 +925,6 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     if (dev.err != hipSuccess) return hip_fail(dev.err, "hipSetDevice");
     hipStream_t s = (hipStream_t)stream;
     const BloomPlan P = bloom_plan(W, H, levels);
-    // AUTO: the fused chain when every same-size sample is exact (powers of two); the general fused chain
-    // when they are proven identities on stored texels (same_size_identity: the copies vanish, the remixes
-    // still sample through the same-size plan); else the literal pass list
-    const uint32_t wl = P.res[levels - 1][0], hl = P.res[levels - 1][1];
-    const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) && same_size_exact(wl) &&
-                       same_size_exact(hl);
-    const bool general = schedule == BH_BLOOM_AUTO && !fused && same_size_identity(W, H) && same_size_identity(wl, hl);
     // scratch: [0, 3*levels) copy_in / remix_in0 / remix_in1 (full), then blur_in, final_in1 (full),
     // then down[levels], up[levels] at res[l]
     const uint64_t key = ((uint64_t)W << 40) ^ ((uint64_t)H << 16) ^ levels;
@@ -822,109 +971,30 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
         B = &c->blooms.back();
     }
     B->last_use = ++c->bloom_clock;
-    uint32_t** T = B->tex.data();
-    uint32_t **copy_in = T, **remix_in0 = T + levels, **remix_in1 = T + 2 * levels;
-    uint32_t* blur_in = T[3 * levels];
-    uint32_t* final_in1 = T[3 * levels + 1];
-    uint32_t **down = T + 3 * levels + 2, **up = T + 4 * levels + 2;
-    const uint32_t* X = (const uint32_t*)blackout;
-    const uint32_t* C = (const uint32_t*)col;
-    uint32_t* O = (uint32_t*)out;
-    const uint32_t full[2] = {W, H};
-    BloomRun R{c, B, capturing, s};
-    const uint32_t L = levels - 1;
-    if (fused) {
-        // same-size passes are identities (same_size_identity): see bh_bloom.hip
-        const uint32_t* S = X;
-        if (levels > 1) {
-            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
-            S = copy_in[1];
-        }
-        const uint32_t* u_src = R.downs(S, levels, down, P);  // down[0] == S; up[levels-1] == down[levels-1]
-        for (uint32_t l = 0; l + 1 < levels; ++l) {
-            const uint32_t ti = levels - l - 2;
-            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
-                   P.res[ti][0], P.res[ti][1]);
-            u_src = up[ti];
-        }
-        if (R.err == 0)
-            R.err = bh_launch_bloom_final(c->lut, c->enc, c->enc_b, c->enc_e, C, S, u_src, P.res[L][0], P.res[L][1], O, W, H, s);
-    } else if (general) {
-        // general fused chain (same-size passes are identities, same_size_identity): U1 = up(X) at full
-        // size, Y = remix(X, U1) through the same-size plan, the blur's downsamples and upsamples from Y,
-        // B = its last up pass, out = remix(col, q(remix(Y, B))) through the plan.  The two full-size
-        // up passes with a separable plan carry the remixes as epilogues for the pixels whose column and
-        // row sample exactly (bh_bloom.hip up_sep_kernel, EPI_Y / EPI_FINAL) and a fix-up pass covers the
-        // inexact columns and rows; other plans run the plain pass and the plan remix kernels.
-        const bh_ctx::SepPlan same = sep_plan(B, capturing, W, H, W, H, 0u, 0u, &R.err);
-        const uint32_t* plan = same.dev;
-        const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
-        // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
-        // fix-up of the inexact pixels -- or the plain pass and the remix kernel
-        auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
-                            uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
-            if (R.err != 0) return;
-            bh_ctx::SepPlan sp{};
-            if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
-                sp = sep_plan(B, capturing, W, H, sw, sh, res[0], res[1], &R.err);
-            if (R.err != 0) return;
-            if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
-                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, s) == 0) {
-                R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
-                                              plan, list, same.nc, same.nr, dst, W, H, s);
-                return;
-            }
-            R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);
-            if (R.err != 0) return;
-            R.err = epi == 1u ? bh_launch_bloom_remix_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, aux, plan, dst, W, H, s)
-                              : bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, own1, aux, plan, dst,
-                                                            W, H, s);
-        };
-        const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
-        if (levels > 1) {
-            fused_up(1u, X, W, H, full, remix_in1[0], X, nullptr, copy_in[1]);
-            S = copy_in[1];
-        }
-        const uint32_t* u_src = R.downs(S, levels, down, P);
-        for (uint32_t l = 0; l + 1 < levels; ++l) {
-            const uint32_t ti = levels - l - 2;
-            R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],
-                   P.res[ti][0], P.res[ti][1]);
-            u_src = up[ti];
-        }
-        const uint32_t uw = levels > 1 ? P.res[0][0] : W, uh = levels > 1 ? P.res[0][1] : H;  // up[0] is W x H
-        fused_up(2u, u_src, uw, uh, P.res[L], remix_in1[L], C, S, O);
-    } else {
-        // literal: the reference's render passes in order (oracle/bh_bloom_oracle.c, bho_bloom)
-        if ((e = hipMemcpyAsync(copy_in[0], X, (size_t)W * H * 4u, hipMemcpyDeviceToDevice, s)) != hipSuccess)
-            return hip_fail(e, "hipMemcpyAsync(bloom)");
-        auto blur = [&](uint32_t lv, uint32_t* dst) {
-            // blurs[k] with `lv` levels; its input (down[0]) was written by the copy pass
-            for (uint32_t l = 1; l < lv; ++l)
-                R.pass(bh_bloom_shader_down, down[l - 1], P.res[l - 1][0], P.res[l - 1][1], nullptr, P.res[l - 1],
-                       down[l], P.res[l][0], P.res[l][1]);
-            R.pass(bh_bloom_shader_down, down[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1], nullptr, P.res[lv - 1],
-                   up[lv - 1], P.res[lv - 1][0], P.res[lv - 1][1]);
-            for (uint32_t l = 0; l + 1 < lv; ++l)
-                R.pass(bh_bloom_shader_up, up[lv - l - 1], P.res[lv - l - 1][0], P.res[lv - l - 1][1], nullptr, P.res[l],
-                       up[lv - l - 2], P.res[lv - l - 2][0], P.res[lv - l - 2][1]);
-            R.pass(bh_bloom_shader_up, up[0], W, H, nullptr, P.res[lv - 1], dst, W, H);
-        };
-        for (uint32_t level = 0; level + 1 < levels; ++level) {
-            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, down[0], W, H);
-            R.pass(bh_bloom_shader_copy, copy_in[0], W, H, nullptr, full, remix_in0[0], W, H);
-            blur(1, remix_in1[0]);
-            R.pass(bh_bloom_shader_remix, remix_in0[0], W, H, remix_in1[0], full, copy_in[level + 1], W, H);
-        }
-        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, down[0], W, H);
-        R.pass(bh_bloom_shader_copy, copy_in[L], W, H, nullptr, full, remix_in0[L], W, H);
-        blur(levels, remix_in1[L]);
-        R.pass(bh_bloom_shader_remix, remix_in0[L], W, H, remix_in1[L], full, final_in1, W, H);
-        R.pass(bh_bloom_shader_remix, C, W, H, final_in1, full, O, W, H);
-        (void)blur_in;
-    }
-    if (R.err != 0) return hip_fail((hipError_t)R.err, "bloom launch");
+    const int st = bloom_chain(c, B, capturing, nullptr, col, blackout, W, H, levels, schedule, out, s);
+    if (st != BH_OK) return st;
     if (!capturing) B->prepared |= 1u << schedule;
+    return BH_OK;
+}
+
+int bh_bloom_check(uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, uint64_t* out_launches) {
+    if (W == 0 || H == 0 || W > 65536u || H > 65536u || levels < 1 || levels > 12 || schedule > BH_BLOOM_LITERAL)
+        return bad_arg(__func__, __LINE__);
+    bh_ctx c;  // no device: nothing below allocates, uploads or launches
+    bh_ctx::BloomScratch B;
+    for (uint32_t i = 0; i < 5u * levels + 2u; ++i) B.tex.push_back(reinterpret_cast<uint32_t*>((uintptr_t)(i + 1u) << 20));
+    const void* in = reinterpret_cast<const void*>((uintptr_t)1 << 40);
+    std::string fail, dfail;
+    uint64_t launches = 0, checks = 0;
+    bh_bloom_dry_begin();
+    const int st = bloom_chain(&c, &B, false, &fail, in, in, W, H, levels, schedule, const_cast<void*>(in), nullptr);
+    const bool ok = bh_bloom_dry_end(&launches, &checks, &dfail);
+    if (out_launches) *out_launches = launches;
+    if (!ok || !fail.empty() || st != BH_OK) {
+        g_last_error = "bh_bloom_check " + std::to_string(W) + "x" + std::to_string(H) + " levels " +
+                       std::to_string(levels) + ": " + (!dfail.empty() ? dfail : !fail.empty() ? fail : g_last_error);
+        return BH_ERR_INTERNAL;
+    }
     return BH_OK;
 }
 

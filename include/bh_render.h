@@ -72,7 +72,8 @@ typedef enum {
     BH_ERR_UNSUPPORTED = -2,   /* valid for the reference but not implemented (e.g. non-default screen triangle) */
     BH_ERR_HIP = -3,           /* a HIP runtime call failed; see bh_last_error() */
     BH_ERR_NO_DEVICE = -4,     /* no HIP device / device index out of range */
-    BH_ERR_OUT_OF_MEMORY = -5
+    BH_ERR_OUT_OF_MEMORY = -5,
+    BH_ERR_INTERNAL = -6       /* a host-side consistency check failed (bh_bloom_check); see bh_last_error() */
 } bh_status;
 
 /* WGSL `Camera` (src/black_hole_maybe.wgsl:9-17), std140/encase layout, 112 bytes:
@@ -288,6 +289,14 @@ int bh_render_frames(bh_ctx* ctx, uint32_t n_frames, const bh_camera_uniform* ca
 #define BH_BLOOM_LITERAL 1u
 int bh_bloom(bh_ctx* ctx, const void* col_bgra8, const void* blackout_bgra8, uint32_t width, uint32_t height,
              uint32_t levels, uint32_t schedule, void* out_bgra8, void* hip_stream);
+
+/* Host only (no device needed): plan bh_bloom's chain for width x height, `levels`, `schedule` exactly as
+ * bh_bloom does -- the same schedule choice, plans and kernel forms -- and, instead of launching, check
+ * every launch's index arithmetic on the host: every block's staged footprint fits its LDS tile, every
+ * tile read falls inside the staged footprint, every plan index and fix-up list entry inside its texture
+ * (the kernels' own f32 sampler arithmetic, per block and tap).  BH_OK, or BH_ERR_INTERNAL with the first
+ * violation in bh_last_error().  *out_launches (optional) = the launches the chain makes. */
+int bh_bloom_check(uint32_t width, uint32_t height, uint32_t levels, uint32_t schedule, uint64_t* out_launches);
 
 /* Graph contract (see the top of this file): unpin every order state and bloom scratch set that a
  * capture marked, so that LRU eviction may free them again.  Call it only after destroying every HIP

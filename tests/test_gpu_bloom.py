@@ -48,7 +48,10 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # src/lib.rs:60-61): same-size passes proven identities, so AUTO
                                         # fuses them; the up passes take the separable plan (per-column /
                                         # per-row taps from the host); also thin frames
-                                        (1080, 1920, 3), (720, 1280, 3), (1080, 1920, 5), (7, 300, 3), (300, 7, 3)])
+                                        (1080, 1920, 3), (720, 1280, 3), (1080, 1920, 5), (7, 300, 3), (300, 7, 3),
+                                        # the 65536 side limit (a refused plan must fall back to
+                                        # the general kernel, not fail the call; tests/test_bloom_bounds.py)
+                                        (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
     """AUTO fuses the chain when its same-size passes are provably identities on stored texels (the
     host's same_size_identity: every size here, powers of two trivially) and runs the literal pass list
