@@ -33,11 +33,13 @@ from __future__ import annotations
 
 import argparse
 import datetime
+import gc
 import json
 import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -108,8 +110,14 @@ def parse(argv=None):
     p.add_argument("--transport", choices=["auto", "rgbm", "rgbm14"], default="auto",
                    help="N>1 shard layout: BH_LAYOUT_TILES_RGBM (6.125 B/pixel of RGBA16F) or BH_LAYOUT_TILES_RGBM14 "
                         "(5.375: the fp16 channels in [0, 1] take 14 bits); auto = rgbm14 for rgba16f")
-    p.add_argument("--deadline-s", type=float, default=900.0,
-                   help="self-launched N>1 run: stop every rank and exit non-zero after this many seconds")
+    p.add_argument("--deadline-s", type=float, default=420.0,
+                   help="self-launched N>1 run: stop every rank and exit non-zero after this many seconds "
+                        "(below the driver's 600 s limit, so that its error line is what the driver records; "
+                        "a healthy 8-rank run takes well under a minute)")
+    p.add_argument("--stall-s", type=float, default=90.0,
+                   help="per-rank watchdog: a rank that makes no progress (no launch issued, no batch "
+                        "synchronised) for this many seconds -- a kernel or a collective that does not "
+                        "return -- exits with status 125, and the launcher stops the others; 0 = off")
     p.add_argument("--pg-timeout-s", type=float, default=120.0,
                    help="torch.distributed process-group timeout (init and every collective)")
     p.add_argument("--plumbing", action="store_true",
@@ -146,6 +154,47 @@ def _free_port() -> int:
     port = s.getsockname()[1]
     s.close()
     return port
+
+
+class Watchdog:
+    """Ends this rank when it stops making progress: a daemon thread checks once a second that beat() was
+    called within `stall_s` seconds and otherwise prints what the rank was doing and exits the process with
+    status 125 (os._exit: the main thread may be blocked inside a HIP synchronise or a collective that never
+    returns).  The process-group timeout covers collectives only; this also covers a rank stuck in a kernel
+    or a calibration loop.  The launcher then stops the other ranks."""
+
+    EXIT = 125
+
+    def __init__(self, rank: int, stall_s: float):
+        self.rank, self.stall_s = rank, stall_s
+        self.t, self.what = time.monotonic(), "start"
+        self._done = threading.Event()
+        if stall_s > 0:
+            threading.Thread(target=self._run, name="bench-watchdog", daemon=True).start()
+
+    def beat(self, what: str | None = None) -> None:
+        self.t = time.monotonic()
+        if what:
+            self.what = what
+
+    def stop(self) -> None:
+        self._done.set()
+
+    def _run(self) -> None:
+        while not self._done.wait(1.0):
+            idle = time.monotonic() - self.t
+            if idle > self.stall_s:
+                print(f"bench: rank {self.rank}: no progress for {idle:.0f} s in '{self.what}' (a kernel or "
+                      f"collective that does not return); exiting with status {self.EXIT}", file=sys.stderr,
+                      flush=True)
+                os._exit(self.EXIT)
+
+
+_WD = Watchdog(0, 0.0)  # replaced per rank by main() / plumbing()
+
+
+def beat(what: str | None = None) -> None:
+    _WD.beat(what)
 
 
 def _stop(procs, live, grace_s: float = 10.0) -> None:
@@ -186,7 +235,10 @@ def launch_ranks(n: int, argv: list[str], deadline_s: float) -> int:
             live.discard(r)
             if c != 0 and rc == 0:
                 rc = c if c > 0 else 1
-                print(f"bench: rank {r} exited with status {c}; stopping the other ranks", file=sys.stderr)
+                why = " (its watchdog: no progress)" if c == Watchdog.EXIT else ""
+                print(f"bench: rank {r} exited with status {c}{why}; stopping the other ranks", file=sys.stderr)
+                print(json.dumps({"error": f"rank {r} of {n} exited with status {c}{why}; all ranks stopped",
+                                  "n_gpus": n}), flush=True)
                 _stop(procs, live)
                 live.clear()
         if live and time.monotonic() > t_end:
@@ -247,11 +299,14 @@ def plumbing(args, rank: int, n: int) -> int:
     import torch.distributed as dist
 
     from black_hole_ray_marching_amd import multigpu
+    global _WD
     if n > 1:
         dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.pg_timeout_s))
+    _WD = Watchdog(rank, args.stall_s)
     if os.environ.get("BH_PLUMBING_FAIL_RANK") == str(rank):  # test hook: a rank that dies mid-run
         raise SystemExit(f"plumbing: rank {rank} failing on request")
     if os.environ.get("BH_PLUMBING_HANG_RANK") == str(rank):  # test hook: a rank that hangs mid-run
+        beat("the hang test hook")
         while True:
             time.sleep(1.0)
     W, H = (args.width or 100), (args.height or 52)
@@ -282,6 +337,7 @@ def plumbing(args, rank: int, n: int) -> int:
 
     pipe = multigpu.GatherPipeline(lambda: torch.zeros((stride, tb), dtype=torch.uint8), rank, n, on_frame)
     for i in range(args.steps):
+        beat(f"plumbing frame {i}")
         c, z = frame(i)
         pack = multigpu.pack_rgbm14_numpy if p14 else multigpu.pack_rgbm_numpy
         pipe.buffer(i).copy_(torch.from_numpy(pack(c, z, rank, n, stride, weights)))
@@ -298,6 +354,7 @@ def plumbing(args, rank: int, n: int) -> int:
     if n > 1:
         dist.barrier()
         dist.destroy_process_group()
+    _WD.stop()
     return 0 if (rank != 0 or (len(ok) == args.steps and all(ok))) else 3
 
 
@@ -365,6 +422,9 @@ def main() -> int:
             dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout)
         if dist.get_world_size() != n:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, expected {n}")
+    global _WD
+    _WD = Watchdog(rank, args.stall_s)
+    beat("scene setup")
 
     if args.width and args.height:
         W, H = args.width, args.height
@@ -445,6 +505,15 @@ def main() -> int:
                                                      None, fmt=fmt, schedule=sched, **self.shard)
                                 for buf in (self.pipe.buffer(k) for k in range(self.pipe.depth))]
 
+            def close(self):
+                """Free this candidate's buffers now: on_frame (a bound method) held by the pipeline is a
+                reference cycle, and its receive buffers and prepared batches would otherwise stay
+                allocated until the cyclic GC happens to run."""
+                self.pipe.on_frame = None
+                self.pipe = self.batches = self.part = None
+                gc.collect()
+                torch.cuda.empty_cache()
+
             def on_frame(self, i, gathered):  # issued on the pipeline's side stream (current stream here)
                 # gathered: (n * D * stride, tb), rank k's block of D frames at k * D * stride
                 st = self.stride
@@ -458,6 +527,7 @@ def main() -> int:
                                              stream=torch.cuda.current_stream(dev), rows_in_flight=UNPACK_ROWS_IN_FLIGHT)
 
             def step(self, k):  # one untimed batch (render + exchange), k = its pipeline index
+                beat(f"calibration batch {k}")
                 self.batches[k % len(self.batches)].render(n=D, stream=stream)
                 self.launch_frames[k] = D
                 self.pipe.submit(k)
@@ -482,6 +552,7 @@ def main() -> int:
                 torch.cuda.synchronize(dev)
                 dist.barrier()
                 ms.append((time.perf_counter() - t_c) / CALIBRATE_STEPS * 1e3)
+                rig.close()
                 del rig
             pick = [ratios[int(np.argmin(ms))]]
             dist.broadcast_object_list(pick, src=0)
@@ -540,6 +611,7 @@ def main() -> int:
         stream = cap_stream  # the timing events bracket the replays on the stream they run on
 
     def render(nf):
+        beat(f"launch {launch_no[0]}")
         if graph is not None and nf == D:
             with torch.cuda.stream(stream):  # replay on the capture stream (its order state)
                 graph.replay()
@@ -632,6 +704,7 @@ def main() -> int:
         dist.all_gather_object(ranks, mine)
 
     gather_ok = None
+    beat("after the timed region")
     if args.verify_gather and sharded and rank == 0:
         # every frame of the last batch against a single-GPU render of that frame's camera
         ref_c = torch.empty((H, W, 4), dtype=ch_dtype, device=dev)
@@ -639,6 +712,7 @@ def main() -> int:
         first = frame_no[0] - D  # frame index of the last batch's first frame
         gather_ok = True
         for f in range(D):
+            beat(f"verify frame {f}")
             if args.camera_path == "orbit":
                 scene.render_frames([ref_c], [ref_b], cameras=[orbit[first + f]], fmt=fmt, stream=stream,
                                     schedule=sched)
@@ -676,6 +750,7 @@ def main() -> int:
     px_shape = (H, W) if not sharded else (stride * 64,)  # the layout's pixel index space
     nm = 1 if args.camera_path == "fixed" else D  # orbit: every frame of a launch (own cameras), averaged
     frame_no[0] = 0
+    beat("step counts")
     nrk_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
     steps_bufs = [torch.zeros(px_shape, dtype=torch.int16, device=dev) for _ in range(nm)]
     launch(nm, dbg_n_rk=nrk_bufs, dbg_steps=steps_bufs)
@@ -784,13 +859,16 @@ def main() -> int:
         if args.no_cpu or sharded:
             result["cpu_baseline"] = None
         else:
+            beat("cpu baseline and parity")
             result["cpu_baseline"], result["parity"] = _cpu_leg(scene, sky, W, H, cap, args, dev, stream, sched, fmt)
         if gather_ok is not None:
             result["gather_verified_bit_exact"] = gather_ok
         print(json.dumps(result), flush=True)
     if sharded:
+        beat("final barrier")
         dist.barrier()
         dist.destroy_process_group()
+    _WD.stop()
     return 0
 
 
@@ -799,6 +877,7 @@ EXTRA_SINGLE_FRAMES = 24
 EXTRA_ORBIT_LAUNCHES = 4
 CLOCK_STRIDE = 256   # one wave in 256 of a march launch samples the shader clock
 CALIBRATE_WARM, CALIBRATE_STEPS = 2, 3   # batches per candidate partition of --root-ratio calibrate
+RANK0_FRAME_BYTES = 64 << 30  # rank 0's budget for the D frames of a batch in flight (of 288 GB of HBM)
 PEAK_MHZ = 2400.0    # the shader clock behind the 157.3 TFLOP/s FP32 peak (1024 SIMDs x 32 lanes x 2 x 2.4 GHz)
 
 
@@ -810,6 +889,7 @@ def _leg(fn, launches: int, frames_per_launch: int, scene, clk_row, stream, dev,
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for a, b in ev:
+        beat("extra leg")
         a.record(stream)
         fn()
         b.record(stream)
@@ -854,7 +934,11 @@ def auto_frames_per_launch(n: int, W: int, H: int, cap: int) -> int:
     the one-GPU frame 4.08; profiles/r04/n_gt_1/rank0_D.jsonl); the receive buffers grow with D (rank 0
     at N = 8: ~6 GB of 288)."""
     if n > 1:
-        return 64
+        # capped by rank 0's bytes per frame in flight (ADVICE r4): its two row-major targets (RGBA16F) and
+        # its share of the two receive slots (RGBM14 tiles of every rank); 64 up to ~70 Mpix frames
+        tiles = ((W + 7) // 8) * ((H + 7) // 8)
+        per_frame = 2 * W * H * 8 + 2 * tiles * 344
+        return int(max(1, min(64, RANK0_FRAME_BYTES // per_frame)))
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
     D = 32
     while D < bh_max_frames() and tiles * D < (1 << 19):

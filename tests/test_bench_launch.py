@@ -67,6 +67,45 @@ def test_process_group_timeout_ends_a_wedged_collective():
     assert all(d.get("gather_verified_bit_exact") is not True for d in lines)
 
 
+def test_watchdog_ends_a_stalled_rank_well_inside_the_driver_limit():
+    """A rank that stops making progress (here: the hang hook; on the node, a kernel or a collective that
+    never returns) exits through its watchdog after --stall-s, and the launcher stops the rest and prints
+    one {"error": ...} line -- long before the deadline and the driver's 600 s."""
+    import time
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e["BH_PLUMBING_HANG_RANK"] = "1"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--plumbing", "--steps", "3",
+                        "--stall-s", "4", "--deadline-s", "300", "--pg-timeout-s", "300"],
+                       capture_output=True, text=True, timeout=200, env=e, cwd=str(ROOT))
+    took = time.monotonic() - t0
+    assert r.returncode != 0
+    assert took < 100, took
+    errs = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"error"')]
+    assert len(errs) == 1 and "watchdog" in errs[0]["error"], r.stdout[-2000:] + r.stderr[-2000:]
+    assert "no progress" in r.stderr
+    assert not any(x.startswith('{"metric"') for x in r.stdout.splitlines())
+
+
+def test_default_deadline_is_below_the_driver_limit():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    a = bench.parse([])
+    assert 0 < a.deadline_s <= 450 and 0 < a.stall_s < a.deadline_s
+
+
+def test_frames_per_launch_is_capped_by_rank0_bytes():
+    """N > 1: 64 frames per batch, fewer when rank 0's targets and receive slots of a batch would pass the
+    byte budget (16384 x 8192 frames at 64 would not fit)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+    assert bench.auto_frames_per_launch(8, 8192, 4096, 512) == 64
+    D = bench.auto_frames_per_launch(8, 16384, 8192, 512)
+    assert 1 <= D < 64
+    per_frame = 2 * 16384 * 8192 * 8 + 2 * (16384 // 8) * (8192 // 8) * 344
+    assert D * per_frame <= bench.RANK0_FRAME_BYTES
+
+
 def test_world_size_mismatch_is_refused():
     rc, lines, err = _bench("--gpus", "2", "--plumbing", env={"WORLD_SIZE": "3", "RANK": "0"})
     assert rc != 0 and not lines

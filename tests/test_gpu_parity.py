@@ -147,26 +147,54 @@ def test_exact_bitexact_camera_at_horizon(torch_cuda, scene_small, sky_small, ca
     assert fates[bh.BH_FATE_ESCAPE] > 0 and (fates[bh.BH_FATE_BLACKOUT] > 0) == (over.get("blackout_eh", 1) != 0)
 
 
-@pytest.mark.parametrize("cam,W,H,cap,flags,over", CASES)
+def _grazing(cam, over):
+    """Scenes whose rays mostly graze the photon sphere: camera E zooms on the shadow edge, and a hole of
+    rs >= 8 puts the critical impact parameter (3 sqrt(3) / 2 rs = 20.8 at rs = 8) beyond camera B's distance
+    (20.2), so the shadow fills the frame."""
+    return cam == "E" or over.get("rs", 0.0) >= 8.0
+
+
+FAST_XFAIL = ("BH_MATH_FAST does not meet SURVEY §8c's fate/n_rk bar on grazing scenes: its v_rsq / v_rcp "
+              "cores and FMA contraction differ from the IEEE ops by an ulp, and near the photon sphere the "
+              "step map is chaotic, so an ulp becomes a different step count, fate or exit direction (on the box: "
+              "10 of 2560 rays at rs = 8, a fate-matched escaped ray's colour by 0.074).  Exact mode, the headline, "
+              "is bit-exact there (test_exact_bitexact); DESIGN.md §4")
+
+
+@pytest.mark.parametrize("cam,W,H,cap,flags,over", [
+    pytest.param(*c, marks=pytest.mark.xfail(reason=FAST_XFAIL, strict=False)) if _grazing(c[0], c[5]) else c
+    for c in CASES])
 def test_fast_tolerance(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over):
+    """The fast mode's documented bar on every case: fate/n_rk equal on >= FAST_MATCH_MIN of pixels (or at
+    most 2 pixels differ), |delta| < FAST_TOL on matched escaped pixels.  The grazing cases are expected to
+    miss it (xfail with the recorded cause); test_fast_grazing_envelope bounds how far they miss."""
     cu, U = camera_uniform(cam, W, H), uniforms(**over)
     g = gpu_render(torch_cuda, scene_small, cu, U, W, H, cap, flags, bh.BH_MATH_FAST)
     o = oracle_render(cu, U, sky_small, W, H, cap, flags)
     frac, dmax, match = fast_stats(g, o)
-    # camera E zooms on the shadow edge: half its rays graze the photon sphere, where the fast
-    # path's ulp-level differences flip step counts much more often; so does a hole of rs >= 8, whose
-    # shadow fills most of the small frame (on the box: 10 of 2560 rays differ at rs = 8, and a matched
-    # escaped ray's colour by 0.074)
-    grazing = cam == "E" or over.get("rs", 0.0) >= 8.0
-    need = 0.98 if grazing else FAST_MATCH_MIN
-    assert frac >= need or (~match).sum() <= 2, f"fate/n_rk match {frac:.5f}"
-    if not grazing:  # grazing escaped rays: chaotic, no |delta| bound
-        assert dmax < FAST_TOL, f"max |delta| on matched escaped pixels {dmax:.3g}"
+    assert frac >= FAST_MATCH_MIN or (~match).sum() <= 2, f"fate/n_rk match {frac:.5f}"
+    assert dmax < FAST_TOL, f"max |delta| on matched escaped pixels {dmax:.3g}"
     # blackout target is the pure per-pixel function of col (:365-368)
     gc, gb = g[0], g[1]
     keep = ~(((gc[..., 0] * gc[..., 0] + gc[..., 1] * gc[..., 1]) + gc[..., 2] * gc[..., 2]) < 1.0)
     exp = np.where(keep[..., None], gc, np.array([0, 0, 0, 1], np.float32))
     assert np.array_equal(gb, exp)
+
+
+@pytest.mark.parametrize("cam,W,H,cap,flags,over", [c for c in CASES if _grazing(c[0], c[5])])
+def test_fast_grazing_envelope(torch_cuda, scene_small, sky_small, cam, W, H, cap, flags, over):
+    """How far the fast mode misses on grazing scenes, bounded so that a regression still fails: fate/n_rk
+    equal on >= 98 % of pixels, and at most 1 % of the matched escaped pixels above FAST_TOL (ADVICE r4:
+    an explicit looser bound instead of none)."""
+    cu, U = camera_uniform(cam, W, H), uniforms(**over)
+    g = gpu_render(torch_cuda, scene_small, cu, U, W, H, cap, flags, bh.BH_MATH_FAST)
+    o = oracle_render(cu, U, sky_small, W, H, cap, flags)
+    frac, _, match = fast_stats(g, o)
+    assert frac >= 0.98, f"fate/n_rk match {frac:.5f}"
+    d = np.abs(g[0][..., :3] - o[0][..., :3]).max(axis=-1)
+    sel = match & (o[3] != bh.BH_FATE_CAP)
+    over_tol = float((d[sel] >= FAST_TOL).mean()) if sel.any() else 0.0
+    assert over_tol <= 0.01, f"{over_tol:.4f} of matched escaped pixels above {FAST_TOL}"
 
 
 def test_fp16_output_is_rne_of_exact(torch_cuda, scene_small, sky_small):
