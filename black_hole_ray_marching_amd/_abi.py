@@ -113,7 +113,8 @@ SIGNATURES = {
                                        C.POINTER(C.c_int)]),
     "bh_bloom": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_void_p, C.c_void_p]),
-    "bh_bloom_check": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64)]),
+    "bh_bloom_check": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.c_char_p,
+                                 C.c_size_t]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
     "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "bh_graph_release": (C.c_int, [C.c_void_p]),

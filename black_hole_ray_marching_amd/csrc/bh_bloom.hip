@@ -740,6 +740,19 @@ __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry
 #endif
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
+// Diagnostic build (-DBH_BLOOM_PHASES=1, tools/probe_bloom_phases.py): every wave of up_sepq_kernel adds the
+// shader cycles of its phases to its kernel's slot (FP 28 / 40 / 60): [0] waves, [1] lifetime, [2] start ->
+// footprint and own-texel loads issued + tables staged, [3] -> tile decoded and written + barrier, [4] -> the
+// 8 taps computed, [5] -> epilogue stored.
+#ifndef BH_BLOOM_PHASES
+#define BH_BLOOM_PHASES 0
+#endif
+#if BH_BLOOM_PHASES
+__device__ unsigned long long g_bloom_phase[3][8];
+#define BP_T(i) (bp[i] = (uint32_t)__builtin_amdgcn_s_memtime())
+#else
+#define BP_T(i) do {} while (0)
+#endif
 template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>()>
 __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
                                                       const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
@@ -749,6 +762,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
     // the lanes instead of every second one (2-way bank conflicts)
     __shared__ QEntry colp[8][2][16], rowp[8][2][16];
+#if BH_BLOOM_PHASES
+    uint32_t bp[5];
+#endif
+    BP_T(0);
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
     const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
@@ -805,6 +822,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             m = min(m, min(o0[b][c], o1[b][c]));
         }
     load_tables(tb, L);
+    BP_T(1);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
@@ -819,7 +837,18 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         m = min(m, raw[r]);
     }
     const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
-    if (!in[0][0]) return;  // the quad's first pixel outside: the whole quad is
+    BP_T(2);
+#if BH_BLOOM_PHASES
+    bp[3] = bp[2];
+#endif
+    if (!in[0][0]) {  // the quad's first pixel outside: the whole quad is
+#if BH_BLOOM_PHASES
+        goto phases;
+#else
+        return;
+#endif
+    }
+    {
     auto run = [&](auto A1c) {
         constexpr bool A1 = decltype(A1c)::value;
         auto texel = [&](int32_t o) {
@@ -914,6 +943,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             asm volatile("" ::"v"(s[0][0].r), "v"(s[0][1].r), "v"(s[1][0].r), "v"(s[1][1].r));
             __builtin_amdgcn_sched_barrier(0);
         }
+        BP_T(3);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -940,7 +970,33 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     };
     if (a1) run(std::true_type{});
     else run(std::false_type{});
+    }
+#if BH_BLOOM_PHASES
+phases:
+    BP_T(4);
+    {
+        const uint32_t lane = threadIdx.x & 63u;
+        if (lane == 0u) {
+            const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
+            unsigned long long* P = g_bloom_phase[FP == 28 ? 0 : FP == 40 ? 1 : 2];
+            atomicAdd(P + 0, 1ull);
+            atomicAdd(P + 1, (unsigned long long)(t_end - bp[0]));
+            for (int i = 0; i < 4; ++i) atomicAdd(P + 2 + i, (unsigned long long)(bp[i + 1] - bp[i]));
+        }
+    }
+#endif
 }
+
+#if BH_BLOOM_PHASES
+extern "C" int bh_bloom_phases_read(unsigned long long* out24, int reset) {
+    if (hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_bloom_phase), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bloom_phase), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 // ---- remixes of the chain at any proven-identity size (general fused schedule) ----------------------
 // On frames whose same-size passes are identities on stored texels (the host's same_size_identity, e.g.
@@ -1967,6 +2023,7 @@ namespace {
 struct DryRun {
     uint64_t launches = 0, checks = 0;
     std::string fail;
+    std::string plan;  // one line per launch: its form, output size, input size, resolution uniform
 };
 thread_local DryRun* g_dry = nullptr;
 // Test hook (tests/test_bloom_bounds.py): the checks treat every tile as this many entries smaller, so a
@@ -1991,6 +2048,14 @@ bool chk(bool ok, const char* fmt, ...) {
         *w = buf;
     }
     return false;
+}
+// the dry run's launch list (bh_bloom_check): "form ow oh tw th rx ry"
+void note_launch(const char* form, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry) {
+    if (!g_dry) return;
+    ++g_dry->launches;
+    char buf[128];
+    std::snprintf(buf, sizeof buf, "%s %u %u %u %u %u %u\n", form, ow, oh, tw, th, rx, ry);
+    g_dry->plan += buf;
 }
 float h_texcoord(uint32_t i, uint32_t n) { return ((float)i + 0.5f) / (float)n; }
 // Taps::du / dv on the host: (hx * m) * 3 with hx = 0.5 / res
@@ -2205,11 +2270,12 @@ extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void) {
     g_dry = new DryRun();
 }
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry_end(uint64_t* launches, uint64_t* checks,
-                                                                     std::string* fail) {
+                                                                     std::string* fail, std::string* plan) {
     if (!g_dry) return false;
     if (launches) *launches = g_dry->launches;
     if (checks) *checks = g_dry->checks;
     if (fail) *fail = g_dry->fail;
+    if (plan) *plan = g_dry->plan;
     const bool ok = g_dry->fail.empty();
     delete g_dry;
     g_dry = nullptr;
@@ -2275,7 +2341,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     const SepForm f = sep_form(ext, ow, oh);
     if (f.FP == 0 || !sep) return (int)hipErrorInvalidValue;
     if (g_dry) {  // the plan is a host copy: check the form's every read instead of launching
-        ++g_dry->launches;
+        char form[32];
+        std::snprintf(form, sizeof form, "%s%d%s/%u", f.quad ? "sepq" : "sep", f.FP, f.raw ? "r" : "", epi);
+        note_launch(form, ow, oh, aw, ah, rx, ry);
         return bh_bloom_sep_verify(ow, oh, aw, ah, rx, ry, sep, ext, nullptr) &&
                        (epi == EPI_PLAIN || chk(same != nullptr, "separable epilogue without a same-size plan"))
                    ? 0
@@ -2327,7 +2395,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
     if (n_cols > w || n_rows > h || !list || !same) return (int)hipErrorInvalidValue;  // the list of this frame's plan
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
     if (g_dry) {
-        ++g_dry->launches;
+        note_launch(epi == EPI_Y ? "fixup/1" : "fixup/2", w, h, n_cols, n_rows, 0u, 0u);
         return same_ok(w, h, same, list, n_cols, n_rows) && chk(list == same + 2u * ((size_t)w + h), "fix-up list "
                                                                 "is not its plan's")
                    ? 0
@@ -2362,7 +2430,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const
                                                                           uint32_t ow, uint32_t oh, hipStream_t s) {
     if (mw == 0u || mh == 0u) return (int)hipErrorInvalidValue;
     if (g_dry) {  // every index of down2_kernel is clamped to its texture (down_at): only the sizes to check
-        ++g_dry->launches;
+        note_launch("down2", ow, oh, aw, ah, mw, mh);
         return chk(aw > 0u && ah > 0u && ow > 0u && oh > 0u, "down2 of an empty texture") ? 0 : (int)hipErrorInvalidValue;
     }
     hipLaunchKernelGGL(down2_kernel, grid_for(ow, oh), dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{a, aw, ah},
@@ -2395,7 +2463,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(
                                                                                uint32_t* out, uint32_t w, uint32_t h,
                                                                                hipStream_t s) {
     if (g_dry) {  // the plan's texel indices (host copy)
-        ++g_dry->launches;
+        note_launch("remix_plan", w, h, w, h, w, h);
         return chk(plan != nullptr, "remix without a plan") && same_ok(w, h, plan, nullptr, 0u, 0u, false) ? 0
                                                                                                                 : (int)hipErrorInvalidValue;
     }
@@ -2411,7 +2479,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan
                                                                                 uint32_t* out, uint32_t w, uint32_t h,
                                                                                 hipStream_t s) {
     if (g_dry) {  // the plan's texel indices (host copy)
-        ++g_dry->launches;
+        note_launch("remix2_plan", w, h, w, h, w, h);
         return chk(plan != nullptr, "remix without a plan") && same_ok(w, h, plan, nullptr, 0u, 0u, false) ? 0
                                                                                                        : (int)hipErrorInvalidValue;
     }
@@ -2460,7 +2528,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     if (shader == SH_UP && !P.valid && !g_no_up2) {
         const Up2Plan Q = up2_plan(ow, oh, aw, ah, rx, ry);
         if (Q.valid && g_dry) {
-            ++g_dry->launches;
+            note_launch(std_up2_plan(Q) == 12 ? "up2_12" : std_up2_plan(Q) == 3 ? "up2_3" : "up2_0", ow, oh, aw, ah, rx, ry);
             const bool ok = tile_ok(FP_UPQ, FS_UPQ, 0, FP_UPQ * FS_UPQ) && up2_axis_ok(Q, ow, aw, rx, 0, FP_UPQ) &&
                             up2_axis_ok(Q, oh, ah, ry, 1, FP_UPQ);
             return ok ? 0 : (int)hipErrorInvalidValue;
@@ -2480,7 +2548,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
                                    nullptr, out, nullptr, ow, oh, s);
     }
     if (g_dry) {  // pass_kernel: an up pass stages through with_source<FP_UP>; the others read clamped indices
-        ++g_dry->launches;
+        note_launch(shader == SH_UP ? (P.valid ? "pass_up_tap" : "pass_up") : shader == SH_COPY ? "pass_copy"
+                    : shader == SH_DOWN ? "pass_down" : "pass_remix", ow, oh, aw, ah, rx, ry);
         const bool ok = chk(aw > 0u && ah > 0u && ow > 0u && oh > 0u, "pass over an empty texture") &&
                         (shader != SH_UP || (tile_ok(FP_UP, FP_UP, 0, FP_UP * FP_UP) &&
                                              tapplan_axis_ok(P, ow, aw, rx, 0, 16u, FP_UP) &&
@@ -2504,7 +2573,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const flo
     static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
     const bool quad = P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ;
     if (g_dry) {  // the quad form's tile (row-pair shift) or with_source<FP_Y>
-        ++g_dry->launches;
+        note_launch(quad ? (std_tap_plan(P) == 12 ? "yq12" : "yq0") : "y1", w, h, w, h, w, h);
         const bool ok = quad ? tile_ok(FP_YQ, FS_YQ, 2, FP_YQ * FS_YQ + FP_YQ / 2 + 1) &&
                                    tapplan_axis_ok(P, w, w, w, 0, 32u, FP_YQ) && tapplan_axis_ok(P, h, h, h, 1, 32u, FP_YQ)
                              : tile_ok(FP_Y, FP_Y, 0, FP_Y * FP_Y) && tapplan_axis_ok(P, w, w, w, 0, 16u, FP_Y) &&
@@ -2535,7 +2604,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const
                                                                           hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, rx, ry);
     if (g_dry) {  // with_source<FP_FINAL>: the TapPlan form (raw words) or the span fallback
-        ++g_dry->launches;
+        note_launch(P.valid ? (std_tap_plan(P) == 48 ? "final48" : "final0") : "final", w, h, w, h, rx, ry);
         const bool ok = tile_ok(FP_FINAL, FP_FINAL, 0, FP_FINAL * FP_FINAL) &&
                         tapplan_axis_ok(P, w, w, rx, 0, 16u, FP_FINAL) && tapplan_axis_ok(P, h, h, ry, 1, 16u, FP_FINAL);
         return ok ? 0 : (int)hipErrorInvalidValue;

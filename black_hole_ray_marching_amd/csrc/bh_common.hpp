@@ -291,7 +291,7 @@ extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint3
                                                                          uint32_t nc, uint32_t nr, std::string* why);
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry_end(uint64_t* launches, uint64_t* checks,
-                                                                     std::string* fail);
+                                                                     std::string* fail, std::string* plan);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry(void);
 // whether bh_launch_bloom_pass runs an up pass of this shape from its separable plan (bh_bloom.hip)
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_up_uses_sep(uint32_t ow, uint32_t oh, uint32_t aw,

@@ -977,19 +977,25 @@ int bh_bloom(bh_ctx* c, const void* col, const void* blackout, uint32_t W, uint3
     return BH_OK;
 }
 
-int bh_bloom_check(uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, uint64_t* out_launches) {
+int bh_bloom_check(uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, uint64_t* out_launches, char* out_plan,
+                   size_t plan_len) {
     if (W == 0 || H == 0 || W > 65536u || H > 65536u || levels < 1 || levels > 12 || schedule > BH_BLOOM_LITERAL)
         return bad_arg(__func__, __LINE__);
     bh_ctx c;  // no device: nothing below allocates, uploads or launches
     bh_ctx::BloomScratch B;
     for (uint32_t i = 0; i < 5u * levels + 2u; ++i) B.tex.push_back(reinterpret_cast<uint32_t*>((uintptr_t)(i + 1u) << 20));
     const void* in = reinterpret_cast<const void*>((uintptr_t)1 << 40);
-    std::string fail, dfail;
+    std::string fail, dfail, plan;
     uint64_t launches = 0, checks = 0;
     bh_bloom_dry_begin();
     const int st = bloom_chain(&c, &B, false, &fail, in, in, W, H, levels, schedule, const_cast<void*>(in), nullptr);
-    const bool ok = bh_bloom_dry_end(&launches, &checks, &dfail);
+    const bool ok = bh_bloom_dry_end(&launches, &checks, &dfail, &plan);
     if (out_launches) *out_launches = launches;
+    if (out_plan && plan_len) {
+        const size_t n = std::min(plan.size(), plan_len - 1);
+        std::memcpy(out_plan, plan.data(), n);
+        out_plan[n] = '\0';
+    }
     if (!ok || !fail.empty() || st != BH_OK) {
         g_last_error = "bh_bloom_check " + std::to_string(W) + "x" + std::to_string(H) + " levels " +
                        std::to_string(levels) + ": " + (!dfail.empty() ? dfail : !fail.empty() ? fail : g_last_error);

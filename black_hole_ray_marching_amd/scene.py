@@ -186,6 +186,21 @@ def shard_tile_count(width: int, height: int, shard_index: int, shard_count: int
     return int(n)
 
 
+def bloom_check(width: int, height: int, levels: int = 3, schedule: int = 0) -> list[tuple]:
+    """bh_bloom_check (host only, no device): plan bh_bloom's chain for this frame size and check every
+    launch's index arithmetic on the host (DESIGN.md §7b "Bound checks"); raises BhError on a violation.
+    Returns the chain's launches as (form, ow, oh, tw, th, rx, ry) tuples, in launch order."""
+    lib = load()
+    n = C.c_uint64()
+    buf = C.create_string_buffer(1 << 16)
+    check(lib.bh_bloom_check(width, height, levels, schedule, C.byref(n), buf, len(buf)), "bh_bloom_check")
+    out = []
+    for line in buf.value.decode().splitlines():
+        f = line.split()
+        out.append((f[0], *map(int, f[1:])))
+    return out
+
+
 def _ptr(t) -> int | None:
     if t is None:
         return None

@@ -295,8 +295,11 @@ int bh_bloom(bh_ctx* ctx, const void* col_bgra8, const void* blackout_bgra8, uin
  * every launch's index arithmetic on the host: every block's staged footprint fits its LDS tile, every
  * tile read falls inside the staged footprint, every plan index and fix-up list entry inside its texture
  * (the kernels' own f32 sampler arithmetic, per block and tap).  BH_OK, or BH_ERR_INTERNAL with the first
- * violation in bh_last_error().  *out_launches (optional) = the launches the chain makes. */
-int bh_bloom_check(uint32_t width, uint32_t height, uint32_t levels, uint32_t schedule, uint64_t* out_launches);
+ * violation in bh_last_error().  *out_launches (optional) = the launches the chain makes; out_plan (optional,
+ * plan_len bytes, NUL-terminated, truncated) = one line per launch: "form ow oh tw th rx ry" (the kernel form,
+ * its output and input sizes and resolution uniform; tools/bloom_roofline.py reads it). */
+int bh_bloom_check(uint32_t width, uint32_t height, uint32_t levels, uint32_t schedule, uint64_t* out_launches,
+                   char* out_plan, size_t plan_len);
 
 /* Graph contract (see the top of this file): unpin every order state and bloom scratch set that a
  * capture marked, so that LRU eviction may free them again.  Call it only after destroying every HIP

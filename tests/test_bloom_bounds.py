@@ -26,7 +26,7 @@ ROOT = Path(__file__).resolve().parent.parent
 def _check(W, H, levels, schedule=bh.BH_BLOOM_AUTO):
     lib = bh.load()
     n = C.c_uint64()
-    st = lib.bh_bloom_check(W, H, levels, schedule, C.byref(n))
+    st = lib.bh_bloom_check(W, H, levels, schedule, C.byref(n), None, 0)
     return st, n.value, (lib.bh_last_error().decode() if st else "")
 
 
@@ -104,7 +104,7 @@ def test_the_65536_limit_plans_and_passes_the_checks(W, H, schedule):
 def test_arguments_outside_the_contract_are_rejected():
     lib = bh.load()
     for W, H, lv, s in ((0, 8, 3, 0), (8, 0, 3, 0), (65537, 8, 3, 0), (8, 8, 0, 0), (8, 8, 13, 0), (8, 8, 3, 2)):
-        assert lib.bh_bloom_check(W, H, lv, s, None) == _abi.BH_ERR_INVALID_ARG
+        assert lib.bh_bloom_check(W, H, lv, s, None, None, 0) == _abi.BH_ERR_INVALID_ARG
 
 
 def test_the_checks_catch_a_footprint_that_overfills_its_tile():
@@ -114,7 +114,7 @@ def test_the_checks_catch_a_footprint_that_overfills_its_tile():
     code = ("import ctypes as C, black_hole_ray_marching_amd as bh\n"
             "lib = bh.load()\n"
             "bad = [(W, H) for W, H in ((1920, 1080), (1280, 720), (4096, 2048), (7, 300))\n"
-            "       if lib.bh_bloom_check(W, H, 3, 0, None) != 0]\n"
+            "       if lib.bh_bloom_check(W, H, 3, 0, None, None, 0) != 0]\n"
             "print(len(bad), lib.bh_last_error().decode())\n")
     env = dict(os.environ, BH_BLOOM_CHECK_SLACK="1", BH_NO_TORCH_PRELOAD="1", PYTHONPATH=str(ROOT))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=ROOT, timeout=120)
