@@ -1415,10 +1415,17 @@ int bh_partition_map(uint32_t width, uint32_t height, uint32_t S, const uint32_t
     const std::vector<uint32_t> owner = partition_owners(S, weights);
     if (owner.empty()) return bad_arg(__func__, __LINE__);
     const uint32_t M = (uint32_t)owner.size(), tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
+    // A/B only (BH_PARTITION_SB=s, tools/probe_rank0.py): the interleave over s x s tile super-blocks instead of
+    // single tiles (a shard's consecutive tiles then neighbour each other in the frame)
+    static const uint32_t sb = [] {
+        const char* e = std::getenv("BH_PARTITION_SB");
+        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1ul;
+        return (uint32_t)(v >= 1ul && v <= 64ul ? v : 1ul);
+    }();
     std::vector<uint32_t> next(S, 0);
     for (uint32_t ty = 0; ty < ty_n; ++ty)
         for (uint32_t tx = 0; tx < tx_n; ++tx) {
-            const uint32_t k = owner[(tx + 3ull * ty) % M];
+            const uint32_t k = owner[(tx / sb + 3ull * (ty / sb)) % M];
             const size_t t = (size_t)ty * tx_n + tx;
             if (owner_out) owner_out[t] = k;
             if (index_out) index_out[t] = next[k];

@@ -27,6 +27,7 @@ def main():
     p.add_argument("--transport", choices=["rgbm", "rgbm14"], default="rgbm14")
     p.add_argument("--side-priority", default="0", help="comma list: the unpack stream's priority (0 normal, -1 high)")
     p.add_argument("--render-streams", type=int, default=1, help="launches alternate over this many streams")
+    p.add_argument("--tag", default="", help="copied into every line (e.g. the A/B variant)")
     a = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
@@ -98,12 +99,13 @@ def main():
                     run(2, K1, True, False)
                 r0 = run(a.it, 0, True, True)
                 r1 = run(a.it, K1, True, False)
-                out = {"n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
+                out = {"tag": a.tag, "n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
                        "transport": a.transport, "tile_bytes": tb, "side_priority": sp, "render_streams": a.render_streams,
                        "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": (counts + counts)[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),
                        "predicted_frame_ms": round(max(r0, r1), 4)}
+                out["rank1_ns_per_tile"] = round(r1 * 1e6 / counts[K1], 4)
                 print(json.dumps(out), flush=True)
                 scene.close()
             if part:
