@@ -21,15 +21,45 @@ import argparse
 import json
 
 
+def frontier(one_gpu_ms: float, k: int, n: int = 8, tiles: int = 131072, unpack_ms: float = 0.0365):
+    """What N = 8 needs for a given speedup, from the model alone: for each link rate, shard per-tile cost and
+    transport size, the best rank-0 share s0 (fine grid) and the predicted ms per frame (drain included).
+    Rank 0 renders s0 of the tiles and unpacks every frame (unpack_ms, not overlapped: DESIGN.md §7); the
+    others render (1 - s0) / (n - 1) each; rank 0 receives (1 - s0) of the frame over n - 1 links."""
+    print(f"frontier: N = {n}, {tiles} tiles, rank-0 unpack {unpack_ms} ms/frame, K = {k}; 7x needs "
+          f"<= {one_gpu_ms / 7:.4f} ms/frame")
+    print("| link GB/s per direction | shard ns/tile | transport B/px | best s0 | render | ingress | predicted | vs 1 GPU |")
+    print("|---|---|---|---|---|---|---|---|")
+    for link in (76.8, 153.6, float("inf")):
+        for ns in (4.36, 4.20, 4.07):
+            for bpp in (5.375, 4.8, 4.3):
+                best = None
+                for i in range(0, 401):
+                    s0 = i / 2000.0
+                    r0 = ns * 1e-6 * tiles * s0 + unpack_ms
+                    r1 = ns * 1e-6 * tiles * (1.0 - s0) / (n - 1)
+                    ing = 0.0 if link == float("inf") else (1.0 - s0) * tiles * 64 * bpp / ((n - 1) * link * 1e9) * 1e3
+                    st = max(r0, r1, ing)
+                    pr = st + (ing + unpack_ms) / k
+                    if best is None or pr < best[0]:
+                        best = (pr, s0, max(r0, r1), ing)
+                pr, s0, rr, ing = best
+                print(f"| {link} | {ns} | {bpp} | {s0:.3f} | {rr:.4f} | {ing:.4f} | {pr:.4f} | {one_gpu_ms / pr:.2f}x |")
+
+
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("probe")
+    p.add_argument("probe", nargs="?", default="")
+    p.add_argument("--frontier", action="store_true", help="print the model's requirement table (no probe file)")
     p.add_argument("--one-gpu-ms", type=float, required=True)
     p.add_argument("--k", type=int, default=20)
     p.add_argument("--link-gbps", type=float, default=76.8)
     p.add_argument("--link-eff", type=float, default=1.0)
     p.add_argument("--rebalance", action="store_true")
     a = p.parse_args()
+    if a.frontier:
+        frontier(a.one_gpu_ms, a.k)
+        return
     rows = [json.loads(x) for x in open(a.probe) if x.startswith("{")]
     print(f"one GPU {a.one_gpu_ms} ms/frame, K = {a.k}, link {a.link_gbps} GB/s x {a.link_eff} per direction")
     print("| N | D | transport | weights | render (ms) | ingress (ms) | binds | predicted ms/frame | Gpix/s | vs 1 GPU |")
