@@ -1,7 +1,10 @@
 """Post-processing chain (bh_bloom) on one GPU: time per frame of the Kawase
 bloom + remix over a 4096x2048 BGRA8 frame (the march kernel's own two targets), HIP events on the
-stream, fused (AUTO) and literal schedules; HBM roofline with the chain's algorithmic bytes
-(read col + blackout, write the surface: 12 B/pixel).
+stream, fused (AUTO) and literal schedules.  `roofline` (tools/bloom_roofline.py): the chain's
+reference arithmetic in flop-equivalents against the FP32 VALU peak, its algorithmic bytes (read col +
+blackout, write the surface: 12 B/pixel) against HBM, and -- when a committed rocprofv3 PMC summary of this
+frame size exists (profiles/r05/bloom_roof/roofline<W>.json) -- the hardware's VALU-issue, LDS and HBM busy
+fractions, time-weighted over the fused chain's kernels.
     python tools/bench_bloom.py [--width 4096 --height 2048 --levels 3 --steps 100]"""
 import argparse
 import json
@@ -14,6 +17,24 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import torch  # noqa: E402
 
 import black_hole_ray_marching_amd as bh  # noqa: E402
+from tools.bloom_roofline import chain_roofline  # noqa: E402
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def hardware_busy(W, H):
+    """Time-weighted VALU / LDS busy and HBM fraction of the fused chain's kernels from the committed PMC summary."""
+    f = ROOT / "profiles" / "r05" / "bloom_roof" / f"roofline{W}.json"
+    if not f.exists():
+        return None
+    d = json.loads(f.read_text())
+    if d.get("height") != H or "kernels" not in d:
+        return None
+    t = sum(k["us"] * k["launches_per_chain"] for k in d["kernels"])
+    out = {"source": str(f.relative_to(ROOT)), "kernel_us_per_chain": round(t, 2)}
+    for key in ("valu_busy", "lds_busy", "hbm_frac"):
+        out[key] = round(sum(k.get(key, 0.0) * k["us"] * k["launches_per_chain"] for k in d["kernels"]) / t, 3)
+    return out
 
 p = argparse.ArgumentParser()
 p.add_argument("--width", type=int, default=4096)
@@ -43,11 +64,17 @@ for name, sched in (("auto", bh.BH_BLOOM_AUTO), ("literal", bh.BH_BLOOM_LITERAL)
     torch.cuda.synchronize()
     ms = np.array([a.elapsed_time(b) for a, b in ev])
     alg = W * H * 12
-    print(json.dumps({"bloom_schedule": name, "width": W, "height": H, "levels": args.levels,
-                      "avg_ms": round(float(ms.mean()), 5), "min_ms": round(float(ms.min()), 5),
-                      "mpix_per_s": round(W * H / (ms.mean() / 1e3) / 1e6, 1),
-                      "roofline_hbm": {"bound": "hbm", "achieved": round(alg / (ms.mean() / 1e3) / 1e9, 1),
-                                       "peak": 8000.0, "unit": "GB/s",
-                                       "frac": round(alg / (ms.mean() / 1e3) / 1e9 / 8000.0, 4),
-                                       "algorithmic_bytes": alg,
-                                       "note": "read col + blackout, write the surface (BGRA8)"}}))
+    line = {"bloom_schedule": name, "width": W, "height": H, "levels": args.levels,
+            "avg_ms": round(float(ms.mean()), 5), "min_ms": round(float(ms.min()), 5),
+            "mpix_per_s": round(W * H / (ms.mean() / 1e3) / 1e6, 1),
+            "roofline_hbm": {"bound": "hbm", "achieved": round(alg / (ms.mean() / 1e3) / 1e9, 1),
+                             "peak": 8000.0, "unit": "GB/s",
+                             "frac": round(alg / (ms.mean() / 1e3) / 1e9 / 8000.0, 4),
+                             "algorithmic_bytes": alg,
+                             "note": "read col + blackout, write the surface (BGRA8)"}}
+    if name == "auto":
+        line["roofline"] = chain_roofline(W, H, args.levels, float(ms.mean()))
+        hw = hardware_busy(W, H)
+        if hw:
+            line["roofline"]["hardware"] = hw
+    print(json.dumps(line))
