@@ -51,7 +51,8 @@ TU_FLAGS = {
     # no SLP vectorisation: packed-FP32 forms of the filter's adjacent channel ops cost more than the
     # scalar ops on gfx950 (a v_pk op issues slower than two scalar ones, plus the shuffles and hazard
     # nops around it) and hold more VGPRs
-    "bh_bloom.hip": ["-ffp-contract=off", "-fno-slp-vectorize", "-mllvm", "-enable-post-misched=0"],
+    "bh_bloom.hip": ["-ffp-contract=off", "-fno-slp-vectorize", "-mllvm", "-enable-post-misched=0",
+                     "-mllvm", "-pragma-unroll-threshold=200000"],  # the quad pass's 8 taps x 9 read forms
     "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
 }

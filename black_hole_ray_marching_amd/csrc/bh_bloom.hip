@@ -28,6 +28,7 @@
 #include <cstring>
 #include <string>
 #include <type_traits>
+#include <vector>
 #include <utility>
 
 #include "bh_common.hpp"
@@ -730,6 +731,11 @@ __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry
 #endif
 // The raw 60-word tile's row stride (A/B; any stride keeps the quad rows' bank parity: the next quad row
 // is 2 FS + 1 words further, an odd number).  64 instead of 80: 15 KiB of tile instead of 19
+// BH_BLOOM_SEPQ_AXIS: a tap whose floor steps are wave-uniform along one axis only shares that axis's texels
+// (xgen / ygen below) instead of reading each pixel's four (A/B switch)
+#ifndef BH_BLOOM_SEPQ_AXIS
+#define BH_BLOOM_SEPQ_AXIS 0  // measured slower (1920x1080 chain 0.1239 -> 0.1261 ms, profiles/r05/bloom_fix/)
+#endif
 #ifndef BH_BLOOM_SEPQ_FS60
 #define BH_BLOOM_SEPQ_FS60 64
 #endif
@@ -740,33 +746,50 @@ __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry
 #endif
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
-// Diagnostic build (-DBH_BLOOM_PHASES=1, tools/probe_bloom_phases.py): every wave of up_sepq_kernel adds the
-// shader cycles of its phases to its kernel's slot (FP 28 / 40 / 60): [0] waves, [1] lifetime, [2] start ->
-// footprint and own-texel loads issued + tables staged, [3] -> tile decoded and written + barrier, [4] -> the
-// 8 taps computed, [5] -> epilogue stored.
+// Diagnostic build (-DBH_BLOOM_PHASES=1, tools/probe_bloom_phases.py): every wave of up_sepq_kernel writes
+// one record (plain stores, no atomics: a shared counter's contention would stretch what it measures) into
+// the launch's slot of g_bp_rec -- slot g_bp_slot, which the launcher sets in stream order before each
+// quad launch: [0] global start and [1] end (s_memrealtime, 100 MHz, low 32 bits), [2..5] shader cycles of
+// start -> footprint, own-texel and table loads issued + tables staged, -> tile written + barrier, -> the 8
+// taps, -> epilogue stored; [6] cycles start -> end; [7] FP.  Wave 0 of block 0 also writes the slot's header.
 #ifndef BH_BLOOM_PHASES
 #define BH_BLOOM_PHASES 0
 #endif
 #if BH_BLOOM_PHASES
-__device__ unsigned long long g_bloom_phase[3][8];
+constexpr uint32_t BP_SLOTS = 8, BP_MAXW = 40960;
+__device__ uint32_t g_bp_slot;
+__device__ uint32_t g_bp_rec[BP_SLOTS][BP_MAXW][8];
+__device__ uint32_t g_bp_hdr[BP_SLOTS][4];  // FP, EPI, grid blocks, output width
 #define BP_T(i) (bp[i] = (uint32_t)__builtin_amdgcn_s_memtime())
 #else
 #define BP_T(i) do {} while (0)
 #endif
-template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>()>
+// FIX (EPI_Y only): the block also recomputes its inexact pixels whose same-size sample stays inside the
+// block -- S(X) from the staged tile, S(U1) from the block's own U words exchanged through LDS after a
+// barrier -- so the fix-up pass keeps only the columns and rows whose sample crosses a block edge (none for
+// the grid origin the host picks, bh_bloom_same_plan_org).  org: the block grid's origin, blocks start at
+// 32 k - (org & 0xFFFF) columns and 32 k - (org >> 16) rows (even offsets: a quad never straddles the frame
+// edge).
+template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>(), bool FIX = false>
 __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
                                                       const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
-                                                      const uint2* __restrict__ same, Tex aux) {
+                                                      const uint2* __restrict__ same, Tex aux, uint32_t org) {
+    static_assert(!FIX || EPI == EPI_Y, "the in-block fix is EPI_Y's");
     __shared__ Lds L;
     __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS + FP / 2];
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
     // the lanes instead of every second one (2-way bank conflicts)
     __shared__ QEntry colp[8][2][16], rowp[8][2][16];
+    __shared__ uint32_t ublk[FIX ? 32 : 1][FIX ? 33 : 1];  // the block's U words (FIX)
 #if BH_BLOOM_PHASES
     uint32_t bp[5];
+    const uint32_t bp_real0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
 #endif
     BP_T(0);
-    const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
+    // the block's first column / row (negative for the first block of a grid with an origin offset: wrapped,
+    // so x < ow fails for the columns left of the frame) and the first ones inside the frame
+    const uint32_t bx = xcd_block().x * 32u - (org & 0xFFFFu), by = xcd_block().y * 32u - (org >> 16);
+    const uint32_t bxf = (int32_t)bx < 0 ? 0u : bx, byf = (int32_t)by < 0 ? 0u : by;
     const uint32_t ow = EPI == EPI_PLAIN ? out.w : aux.w, oh = EPI == EPI_PLAIN ? out.h : aux.h;
     const uint32_t qx = threadIdx.x & 15u, qy = threadIdx.x >> 4;
     const uint32_t x0 = bx + 2u * qx, y0 = by + 2u * qy;  // the quad's first pixel
@@ -774,9 +797,9 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     const crm::Rcp Rw = crm::rcp_refined((float)ow), Rh = crm::rcp_refined((float)oh);
     const Taps k(rx, ry);
     const uint32_t xl = min(bx + 31u, ow - 1u), yl = min(by + 31u, oh - 1u);
-    const int32_t lo_x = (int32_t)floorf(sample_coord(texcoord(bx, Rw) + k.du_min(), a.w));
+    const int32_t lo_x = (int32_t)floorf(sample_coord(texcoord(bxf, Rw) + k.du_min(), a.w));
     const int32_t hi_x = (int32_t)floorf(sample_coord(texcoord(xl, Rw) + k.du_max(), a.w));
-    const int32_t lo_y = (int32_t)floorf(sample_coord(texcoord(by, Rh) + k.dv_min(), a.h));
+    const int32_t lo_y = (int32_t)floorf(sample_coord(texcoord(byf, Rh) + k.dv_min(), a.h));
     const int32_t hi_y = (int32_t)floorf(sample_coord(texcoord(yl, Rh) + k.dv_max(), a.h));
     const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // the host sizes FP: no cut
     constexpr int R = (FP * FP + 255) / 256;
@@ -793,10 +816,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     for (int h = 0; h < 2; ++h) {
         const uint32_t i = (threadIdx.x >> 5) & 7u, j = threadIdx.x & 31u;
         if (h == 0) {
-            const SepEntry e = sep[i * ow + min(bx + j, ow - 1u)];
+            const SepEntry e = sep[i * ow + (uint32_t)clampi((int32_t)(bx + j), 0, (int32_t)ow - 1)];
             colp[i][j & 1u][j >> 1] = q_entry(e.f - lo_x, 0, e);
         } else {
-            const SepEntry e = sep[8u * ow + i * oh + min(by + j, oh - 1u)];
+            const SepEntry e = sep[8u * ow + i * oh + (uint32_t)clampi((int32_t)(by + j), 0, (int32_t)oh - 1)];
             const int32_t ly = e.f - lo_y;
             rowp[i][j & 1u][j >> 1] = q_entry(ly * FS + (ly >> 1), ly, e);
         }
@@ -804,6 +827,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     // own texels of the epilogue (four pixels), loaded before the tables, used last
     uint32_t o0[2][2], o1[2][2];
     bool in[2][2], exact[2][2];
+    uint2 scx[2] = {}, scy[2] = {};  // same-size plan entries of the quad's columns and rows (FIX)
     uint32_t m = 0xFF000000u;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -817,7 +841,13 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             if constexpr (EPI != EPI_PLAIN) {
                 o0[b][c] = own0.px[pix];
                 if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
-                exact[b][c] = in[b][c] && same[in[b][c] ? x : 0u].y == 0u && same[ow + (in[b][c] ? y : 0u)].y == 0u;
+                if constexpr (FIX) {
+                    if (b == 0) scx[c] = same[in[b][c] ? x : 0u];
+                    if (c == 0) scy[b] = same[ow + (in[b][c] ? y : 0u)];
+                    exact[b][c] = in[b][c] && scx[c].y == 0u && scy[b].y == 0u;
+                } else {
+                    exact[b][c] = in[b][c] && same[in[b][c] ? x : 0u].y == 0u && same[ow + (in[b][c] ? y : 0u)].y == 0u;
+                }
             }
             m = min(m, min(o0[b][c], o1[b][c]));
         }
@@ -841,7 +871,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
 #if BH_BLOOM_PHASES
     bp[3] = bp[2];
 #endif
-    if (!in[0][0]) {  // the quad's first pixel outside: the whole quad is
+    // a quad whose first pixel is outside is outside as a whole (even origin offsets); it has no taps, but
+    // with FIX its lanes still meet the block's barrier
+    const bool live = in[0][0];
+    if (!FIX && !live) {
 #if BH_BLOOM_PHASES
         goto phases;
 #else
@@ -870,6 +903,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             q.a = A1 ? 1.0f : (t00.w * ia + t10.w * fa) * ib + (t01.w * ia + t11.w * fa) * fb;
             return q;
         };
+        if (live) {
         F4 s[2][2];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -877,8 +911,9 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             const QEntry rT = rowp[i][0][qy], rB = rowp[i][1][qy];
             const int32_t dx = cR.f - cL.f, dy = rB.pad - rT.pad;  // the two columns' / rows' floor steps
             const int32_t dx0 = __builtin_amdgcn_readfirstlane(dx), dy0 = __builtin_amdgcn_readfirstlane(dy);
-            const bool uni = __builtin_amdgcn_ballot_w64((dx != dx0) | (dy != dy0)) == 0ull && (dx0 == 0 || dx0 == 1) &&
-                             (dy0 == 0 || dy0 == 1);
+            const bool ux = __builtin_amdgcn_ballot_w64(dx != dx0) == 0ull && (dx0 == 0 || dx0 == 1);
+            const bool uy = __builtin_amdgcn_ballot_w64(dy != dy0) == 0ull && (dy0 == 0 || dy0 == 1);
+            const bool uni = ux && uy;
             const int32_t o = cL.f + rT.f;
             const int32_t d1 = FS + (rT.pad & 1), d2 = 2 * FS + 1;  // the window's rows 1 and 2
             auto window = [&](auto DXc, auto DYc) {
@@ -925,10 +960,54 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                     }
 #endif
             };
+            // one axis uniform: the other axis's two pixels read their own texel pairs (per-lane offsets), the
+            // uniform axis shares its rows (columns) as in the window -- 4 (2 + DY) or (2 + DX) 4 reads, not 16
+            auto xgen = [&](auto DYc) {  // rows uniform (step DY), columns per lane: cL.f, cR.f
+                constexpr int DY = decltype(DYc)::value;
+                const int32_t oR = cR.f + rT.f;
+                float4 t0[4], t1[4];
+                t0[0] = texel(o); t0[1] = texel(o + 1); t0[2] = texel(oR); t0[3] = texel(oR + 1);
+                t1[0] = texel(o + d1); t1[1] = texel(o + d1 + 1); t1[2] = texel(oR + d1); t1[3] = texel(oR + d1 + 1);
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    acc(s[0][c], lerp(t0[2 * c], t0[2 * c + 1], t1[2 * c], t1[2 * c + 1], c ? cR : cL, rT), i);
+                if constexpr (DY == 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    t0[0] = texel(o + d2); t0[1] = texel(o + d2 + 1); t0[2] = texel(oR + d2); t0[3] = texel(oR + d2 + 1);
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        acc(s[1][c], lerp(t1[2 * c], t1[2 * c + 1], t0[2 * c], t0[2 * c + 1], c ? cR : cL, rB), i);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c)
+                        acc(s[1][c], lerp(t0[2 * c], t0[2 * c + 1], t1[2 * c], t1[2 * c + 1], c ? cR : cL, rB), i);
+                }
+            };
+            auto ygen = [&](auto DXc) {  // columns uniform (step DX), rows per lane: rT, rB
+                constexpr int DX = decltype(DXc)::value;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const QEntry& re = b ? rB : rT;
+                    const int32_t ob = cL.f + re.f, dn = FS + (re.pad & 1);
+                    float4 t0[2 + DX], t1[2 + DX];
+#pragma unroll
+                    for (int c = 0; c < 2 + DX; ++c) { t0[c] = texel(ob + c); t1[c] = texel(ob + dn + c); }
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const int ca = c ? DX : 0;
+                        acc(s[b][c], lerp(t0[ca], t0[ca + 1], t1[ca], t1[ca + 1], c ? cR : cL, re), i);
+                    }
+                    if (b == 0) __builtin_amdgcn_sched_barrier(0);
+                }
+            };
             if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 0 && dy0 == 1) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 1 && dy0 == 0) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
             else if (uni && dx0 == 0 && dy0 == 0) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+            else if (BH_BLOOM_SEPQ_AXIS && uy && dy0 == 1) xgen(std::integral_constant<int, 1>{});
+            else if (BH_BLOOM_SEPQ_AXIS && uy) xgen(std::integral_constant<int, 0>{});
+            else if (BH_BLOOM_SEPQ_AXIS && ux && dx0 == 1) ygen(std::integral_constant<int, 1>{});
+            else if (BH_BLOOM_SEPQ_AXIS && ux) ygen(std::integral_constant<int, 0>{});
             else {
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
@@ -956,6 +1035,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 } else {
                     const uint32_t ue = enc(L, u);
                     aux.px[pix] = ue;
+                    if constexpr (FIX) ublk[2u * qy + b][2u * qx + c] = ue;
                     if (exact[b][c]) {
                         const F4 uq = dec<A1>(L, ue);
                         if constexpr (EPI == EPI_Y) {
@@ -967,6 +1047,39 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                     }
                 }
             }
+        }  // live
+        if constexpr (FIX) {
+            // Y = remix(S(X), S(U1)) at the inexact pixels whose sample's texels (those of nonzero weight) lie
+            // in this block: fixup_gather_kernel<EPI_Y>'s arithmetic, each texel from LDS (a texel of weight 0
+            // enters the lerp as t * 0 == +0 for any finite t >= 0, as the fix-up's unread 0 does)
+            __syncthreads();
+            if (live) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (!in[b][c] || exact[b][c]) continue;
+                        const uint2 ex = scx[c], ey = scy[b];
+                        const float fa = __uint_as_float(ex.y), fb = __uint_as_float(ey.y);
+                        const int32_t u0 = (int32_t)(ex.x & 0xFFFFu) - (int32_t)bx, v0 = (int32_t)(ey.x & 0xFFFFu) - (int32_t)by;
+                        const int32_t u1 = fa != 0.0f ? (int32_t)(ex.x >> 16) - (int32_t)bx : u0;
+                        const int32_t v1 = fb != 0.0f ? (int32_t)(ey.x >> 16) - (int32_t)by : v0;
+                        if ((uint32_t)u0 > 31u || (uint32_t)u1 > 31u || (uint32_t)v0 > 31u || (uint32_t)v1 > 31u)
+                            continue;  // crosses the block edge: the fix-up pass's (residual list)
+                        auto X = [&](int32_t u, int32_t v) {
+                            const int32_t ly = v + (int32_t)by - lo_y, lx = u + (int32_t)bx - lo_x;
+                            return texel(ly * FS + lx + (ly >> 1));
+                        };
+                        auto U = [&](int32_t u, int32_t v) {
+                            const F4 d = dec<A1>(L, ublk[v][u]);
+                            return make_float4(d.r, d.g, d.b, d.a);
+                        };
+                        const F4 sx = lerp_plan(X(u0, v0), X(u1, v0), X(u0, v1), X(u1, v1), fa, fb);
+                        const F4 su = lerp_plan(U(u0, v0), U(u1, v0), U(u0, v1), U(u1, v1), fa, fb);
+                        out.px[(y0 + b) * ow + x0 + c] = enc(L, remix(sx, su));
+                    }
+            }
+        }
     };
     if (a1) run(std::true_type{});
     else run(std::false_type{});
@@ -975,27 +1088,41 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
 phases:
     BP_T(4);
     {
-        const uint32_t lane = threadIdx.x & 63u;
-        if (lane == 0u) {
-            const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
-            unsigned long long* P = g_bloom_phase[FP == 28 ? 0 : FP == 40 ? 1 : 2];
-            atomicAdd(P + 0, 1ull);
-            atomicAdd(P + 1, (unsigned long long)(t_end - bp[0]));
-            for (int i = 0; i < 4; ++i) atomicAdd(P + 2 + i, (unsigned long long)(bp[i + 1] - bp[i]));
+        const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
+        const uint32_t real_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        const uint32_t lane = threadIdx.x & 63u, slot = g_bp_slot % BP_SLOTS;
+        const uint32_t wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (threadIdx.x >> 6);
+        if (lane < 8u && wave < BP_MAXW) {
+            uint32_t v = FP;
+            v = lane == 0u ? bp_real0 : lane == 1u ? real_end : lane == 6u ? t_end - bp[0] : v;
+            for (int i = 0; i < 4; ++i) v = lane == 2u + i ? bp[i + 1] - bp[i] : v;
+            g_bp_rec[slot][wave][lane] = v;
         }
+        if (wave == 0u && lane < 4u)
+            g_bp_hdr[slot][lane] = lane == 0u ? FP : lane == 1u ? EPI : lane == 2u ? gridDim.x * gridDim.y : ow;
     }
 #endif
 }
 
 #if BH_BLOOM_PHASES
-extern "C" int bh_bloom_phases_read(unsigned long long* out24, int reset) {
-    if (hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_bloom_phase), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long z[24] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bloom_phase), z, sizeof z) != hipSuccess) return -1;
-    }
-    return 0;
+static uint32_t g_bp_next = 0;
+// the next quad launch's record slot, in stream order (a pageable source: staged before the call returns)
+static void bp_next_slot(hipStream_t s) {
+    const uint32_t v = g_bp_next++;
+    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_bp_slot), &v, 4, 0, hipMemcpyHostToDevice, s);
 }
+// records of the last `slots` quad launches: hdr [BP_SLOTS][4], rec [BP_SLOTS][BP_MAXW][8]; returns the number
+// of launches so far (resets the count when reset != 0)
+extern "C" int bh_bloom_phases_read(uint32_t* hdr, uint32_t* rec, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(hdr, HIP_SYMBOL(g_bp_hdr), sizeof(uint32_t) * BP_SLOTS * 4) != hipSuccess) return -1;
+    if (rec && hipMemcpyFromSymbol(rec, HIP_SYMBOL(g_bp_rec), sizeof(uint32_t) * BP_SLOTS * BP_MAXW * 8) != hipSuccess)
+        return -1;
+    const int n = (int)g_bp_next;
+    if (reset) g_bp_next = 0;
+    return n;
+}
+extern "C" uint32_t bh_bloom_phases_geometry(void) { return BP_SLOTS << 24 | BP_MAXW; }
 #endif
 
 // ---- remixes of the chain at any proven-identity size (general fused schedule) ----------------------
@@ -2068,15 +2195,23 @@ int32_t h_floor(float t) { return (int32_t)floorf(t); }
 // sampler arithmetic of its first and last column, c = hi - lo + 2 entries (floor .. floor + 1), which the
 // kernel cuts to FP -- the cut must never happen -- and for every tap and column of the block the plan's
 // floor f with both of its texels f - lo, f + 1 - lo inside those c entries.  e: the axis's [8][on] entries.
-bool sep_axis_ok(const SepEntry* e, uint32_t on, uint32_t tn, uint32_t res, int axis, uint32_t B, int FP) {
+// off: the block grid's origin offset (blocks start at B k - off; the quad kernel's org), own: the block's own
+// columns must lie in its footprint too (the FIX epilogue reads them from the tile).
+bool sep_axis_ok(const SepEntry* e, uint32_t on, uint32_t tn, uint32_t res, int axis, uint32_t B, int FP, uint32_t off = 0,
+                 bool own = false) {
     const float dmin = h_tap_min(res, axis), dmax = h_tap_max(res, axis);
-    for (uint32_t b = 0; b < on; b += B) {
-        const uint32_t l = std::min(b + B - 1u, on - 1u);
+    if (!chk(off < B && off % 2u == 0u, "block grid origin %u for %u-pixel blocks", off, B)) return false;
+    for (int64_t bs = -(int64_t)off; bs < (int64_t)on; bs += B) {
+        const uint32_t b = (uint32_t)std::max<int64_t>(bs, 0);
+        const uint32_t l = (uint32_t)std::min<int64_t>(bs + B - 1, (int64_t)on - 1);
         const int32_t lo = h_floor(h_sample_coord(h_texcoord(b, on) + dmin, tn));
         const int32_t hi = h_floor(h_sample_coord(h_texcoord(l, on) + dmax, tn));
         const int32_t c = hi - lo + 2;
         if (!chk(c >= 2 && c <= FP - g_check_slack, "separable %s footprint of block %u: %d entries, tile side %d", axis ? "row" : "column",
                  b, c, FP))
+            return false;
+        if (own && !chk((int32_t)b - lo >= 0 && (int32_t)l - lo <= c - 1,
+                        "in-block fix: %s block %u..%u outside its footprint %d + %d", axis ? "row" : "column", b, l, lo, c))
             return false;
         for (int i = 0; i < 8; ++i)
             for (uint32_t x = b; x <= l; ++x) {
@@ -2189,7 +2324,8 @@ bool same_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list,
             std::memcpy(&wgt, &plan[2u * (base + x) + 1u], 4);
             const uint32_t x0 = e & 0xFFFFu, x1 = e >> 16;
             if (!chk(x0 < n && x1 < n && wgt >= 0.0f && wgt <= 1.0f, "same-size plan %s %u: texels %u, %u, weight %g of %u",
-                     axis ? "row" : "column", x, x0, x1, (double)wgt, n))
+                     axis ? "row" : "column", x, x0, x1, (double)wgt, n) ||
+                !chk(wgt != 0.0f || x0 == x, "same-size plan: exact %s %u samples texel %u", axis ? "row" : "column", x, x0))
                 return false;
             if (wgt != 0.0f && with_list) {
                 if (!chk(k < cnt && L[k] == x, "same-size list: %s %u missing", axis ? "row" : "column", x)) return false;
@@ -2200,7 +2336,67 @@ bool same_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list,
     }
     return true;
 }
+// Whether inexact column (row) x of an n-pixel axis samples a texel outside its 32-pixel block of a grid at
+// origin off: such a column's pixels are the fix-up pass's, the others up_sepq_kernel's in-block fix (FIX).
+bool same_crosses(const uint32_t* plan, uint32_t base, uint32_t x, uint32_t off) {
+    const uint32_t e = plan[2u * (base + x)], wbits = plan[2u * (base + x) + 1u];
+    if (wbits == 0u) return false;  // exact: its own texel (same_ok)
+    const uint32_t blk = (x + off) / 32u;
+    return ((e & 0xFFFFu) + off) / 32u != blk || ((e >> 16) + off) / 32u != blk;
+}
+// The residual list at origin org: the crossing columns, then rows, ascending -- exactly what it must hold
+bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, uint32_t nr, uint32_t org) {
+    if (!chk(nc <= w && nr <= h && (org & 0xFFFFu) < 32u && (org >> 16) < 32u && org % 2u == 0u && (org >> 16) % 2u == 0u,
+             "residual list: %u columns of %u, %u rows of %u, origin %u,%u", nc, w, nr, h, org & 0xFFFFu, org >> 16))
+        return false;
+    for (int axis = 0; axis < 2; ++axis) {
+        const uint32_t n = axis ? h : w, base = axis ? w : 0u, cnt = axis ? nr : nc, off = axis ? org >> 16 : org & 0xFFFFu;
+        const uint32_t* L = list + (axis ? nc : 0u);
+        uint32_t k = 0;
+        for (uint32_t x = 0; x < n; ++x)
+            if (same_crosses(plan, base, x, off)) {
+                if (!chk(k < cnt && L[k] == x, "residual list: crossing %s %u missing", axis ? "row" : "column", x)) return false;
+                ++k;
+            }
+        if (!chk(k == cnt, "residual list: %u %s entries for %u crossing", cnt, axis ? "row" : "column", k)) return false;
+    }
+    return true;
+}
 }  // namespace
+
+// The quad grid's origin for the in-block fix of a same-size plan (bh_bloom_same_plan): per axis the even
+// offset in [0, 32) with the fewest inexact columns (rows) whose sample crosses a block edge (ties: the
+// smallest) among the offsets that keep the axis's block count -- an extra column of blocks can start a
+// further round of resident blocks (1920 wide: 60 -> 61 blocks, 2074 blocks over the 2048 slots of 8 per CU),
+// dearer than a fix-up launch over a few residual columns -- as org = ox | oy << 16; the crossing ones into
+// cols / rows when given.
+extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                          std::vector<uint32_t>* cols,
+                                                                          std::vector<uint32_t>* rows) {
+    uint32_t org = 0;
+    for (int axis = 0; axis < 2; ++axis) {
+        const uint32_t n = axis ? h : w, base = axis ? w : 0u;
+        uint32_t best = 0, best_n = UINT32_MAX;
+        const uint32_t blocks = (n + 31u) / 32u;
+        for (uint32_t off = 0; off < 32u && best_n != 0u; off += 2u) {
+            if ((n + off + 31u) / 32u != blocks) break;  // offsets only grow the count
+            uint32_t c = 0;
+            for (uint32_t x = 0; x < n && c < best_n; ++x) c += same_crosses(plan, base, x, off) ? 1u : 0u;
+            if (c < best_n) { best_n = c; best = off; }
+        }
+        org |= best << (axis ? 16 : 0);
+        std::vector<uint32_t>* out = axis ? rows : cols;
+        if (out) {
+            out->clear();
+            for (uint32_t x = 0; x < n; ++x)
+                if (same_crosses(plan, base, x, best)) out->push_back(x);
+        }
+    }
+    return org;
+}
+
+// whether bh_launch_bloom_sep runs a plan of these extents with the quad kernel (the in-block fix's form)
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh);
 
 // The separable up pass's launch form for a plan's extents (low 16 bits: 16x16 blocks, high: 32x32): the
 // quad kernel when its footprint fits a 28 / 40 / 60 tile, else the one-pixel kernel at 24 / 44, else none
@@ -2238,20 +2434,28 @@ static SepForm sep_form(int ext, uint32_t ow, uint32_t oh) {
     return f;
 }
 
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh) {
+    return sep_form(ext, ow, oh).quad;
+}
+
 // bh_bloom_sep_plan's plan (host copy `plan`, extents `ext`) checked for the form bh_launch_bloom_sep takes:
 // false (and the reason in *why) when any block's footprint exceeds its tile or any read leaves it.
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_verify(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                         uint32_t th, uint32_t rx, uint32_t ry,
-                                                                        const uint32_t* plan, int ext, std::string* why) {
+                                                                        const uint32_t* plan, int ext, uint32_t org, bool fix,
+                                                                        std::string* why) {
     std::string* prev = g_why;
     g_why = why;
     const SepForm f = sep_form(ext, ow, oh);
     const SepEntry* e = reinterpret_cast<const SepEntry*>(plan);
     const uint32_t B = f.quad ? 32u : 16u;
     const int size = f.quad ? f.FP * f.FS + f.FP / 2 : f.FP * f.FS;
+    // the one-pixel kernel has no grid origin and no in-block fix
+    const uint32_t ox = f.quad ? org & 0xFFFFu : 0u, oy = f.quad ? org >> 16 : 0u;
+    const bool own = fix && f.quad;
     // FP == 0: no staged form fits these extents, and the launcher refuses the plan (the general pass runs)
-    const bool ok = f.FP == 0 || (tile_ok(f.FP, f.FS, f.quad ? 1 : 0, size) && sep_axis_ok(e, ow, tw, rx, 0, B, f.FP) &&
-                                  sep_axis_ok(e + 8u * (size_t)ow, oh, th, ry, 1, B, f.FP));
+    const bool ok = f.FP == 0 || (tile_ok(f.FP, f.FS, f.quad ? 1 : 0, size) && sep_axis_ok(e, ow, tw, rx, 0, B, f.FP, ox, own) &&
+                                  sep_axis_ok(e + 8u * (size_t)ow, oh, th, ry, 1, B, f.FP, oy, own));
     g_why = prev;
     return ok;
 }
@@ -2287,11 +2491,11 @@ extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry(void) { retur
 // into `outp` (per tap and column, then per tap and row), from the kernel's own f32 arithmetic: texcoord
 // (x + 0.5) / n (the division core is IEEE division in its domain), the tap offset, sample_coord and
 // floor.  Returns the largest 16x16 block footprint along either axis (the staged tile's side of
-// up_sep_kernel) in the low 16 bits and the largest 32x32 block footprint (up_sepq_kernel) in the high
-// ones, or -1 (texture sides above 65535).
+// up_sep_kernel) in the low 16 bits and the largest 32x32 block footprint (up_sepq_kernel, its grid at
+// origin org) in the high ones, or -1 (texture sides above 65535).
 extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                      uint32_t th, uint32_t rx, uint32_t ry,
-                                                                     uint32_t* outp) {
+                                                                     uint32_t* outp, uint32_t org) {
     if (tw > 65535u || th > 65535u || tw == 0u || th == 0u || ow == 0u || oh == 0u) return -1;
     const float hx = 0.5f / (float)rx, hy = 0.5f / (float)ry;
     auto axis = [](uint32_t on, uint32_t tn, float d, uint32_t x, uint32_t* o) {
@@ -2316,8 +2520,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t 
         for (int ax = 0; ax < 2; ++ax) {
             const uint32_t n = ax ? oh : ow;
             const size_t base = ax ? 8u * (size_t)ow : 0u;
-            for (uint32_t b = 0; b < n; b += B) {
-                const uint32_t l = std::min(b + B - 1u, n - 1u);
+            const int64_t off = q ? (ax ? org >> 16 : org & 0xFFFFu) : 0;
+            for (int64_t bs = -off; bs < (int64_t)n; bs += B) {
+                const uint32_t b = (uint32_t)std::max<int64_t>(bs, 0);
+                const uint32_t l = (uint32_t)std::min<int64_t>(bs + B - 1, (int64_t)n - 1);
                 int32_t lo = INT_MAX, hi = INT_MIN;
                 for (int i = 0; i < 8; ++i) {
                     lo = std::min(lo, fl(base + (size_t)i * n + b));
@@ -2337,14 +2543,18 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         const uint32_t* sep, int ext, uint32_t epi,
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
-                                                                        uint32_t ow, uint32_t oh, hipStream_t s) {
+                                                                        uint32_t ow, uint32_t oh, uint32_t org, bool fix,
+                                                                        hipStream_t s) {
     const SepForm f = sep_form(ext, ow, oh);
     if (f.FP == 0 || !sep) return (int)hipErrorInvalidValue;
+    // the grid origin and the in-block fix are the quad kernel's; the fix only with the Y epilogue
+    if (!f.quad) org = 0u;
+    fix = fix && f.quad && epi == EPI_Y;
     if (g_dry) {  // the plan is a host copy: check the form's every read instead of launching
         char form[32];
-        std::snprintf(form, sizeof form, "%s%d%s/%u", f.quad ? "sepq" : "sep", f.FP, f.raw ? "r" : "", epi);
+        std::snprintf(form, sizeof form, "%s%d%s/%u%s", f.quad ? "sepq" : "sep", f.FP, f.raw ? "r" : "", epi, fix ? "f" : "");
         note_launch(form, ow, oh, aw, ah, rx, ry);
-        return bh_bloom_sep_verify(ow, oh, aw, ah, rx, ry, sep, ext, nullptr) &&
+        return bh_bloom_sep_verify(ow, oh, aw, ah, rx, ry, sep, ext, org, fix, nullptr) &&
                        (epi == EPI_PLAIN || chk(same != nullptr, "separable epilogue without a same-size plan"))
                    ? 0
                    : (int)hipErrorInvalidValue;
@@ -2354,18 +2564,30 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     const SepEntry* P = reinterpret_cast<const SepEntry*>(sep);
     const uint2* S = reinterpret_cast<const uint2*>(same);
     const Tex O{out, ow, oh}, X{aux ? aux : out, ow, oh};
-    const dim3 g = grid_for(ow, oh), gq((ow + 31u) / 32u, (oh + 31u) / 32u);
+    const dim3 g = grid_for(ow, oh), gq((ow + (org & 0xFFFFu) + 31u) / 32u, (oh + (org >> 16) + 31u) / 32u);
 #define BH_SEP(FP, E, RAW) \
     hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
-#define BH_SEPQ(FP, E, RAW, FS) \
-    hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
+#if BH_BLOOM_PHASES
+#define BH_BP_SLOT() bp_next_slot(s)
+#else
+#define BH_BP_SLOT() (void)0
+#endif
+#define BH_SEPQ(FP, E, RAW, FS, FX)                                                                                  \
+    do {                                                                                                             \
+        BH_BP_SLOT();                                                                                                \
+        hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS, FX>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X, \
+                           org);                                                                                     \
+    } while (0)
 #define BH_EPI(LAUNCH, ...)                                                    \
     do {                                                                       \
-        if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                       \
+        if (epi == EPI_Y && fix) LAUNCH(__VA_ARGS__, EPI_Y, true);             \
+        else if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                  \
         else if (epi == EPI_FINAL) LAUNCH(__VA_ARGS__, EPI_FINAL, _);          \
         else LAUNCH(__VA_ARGS__, EPI_PLAIN, _);                                \
     } while (0)
-#define BH_Q(FPv, RAWv, FSv, E, _) BH_SEPQ(FPv, E, RAWv, FSv)
+#define BH_Q(FPv, RAWv, FSv, E, FX) BH_SEPQ(FPv, E, RAWv, FSv, BH_FIX_##FX)
+#define BH_FIX_true true
+#define BH_FIX__ false
 #define BH_1(FPv, RAWv, E, _) BH_SEP(FPv, E, RAWv)
     // the instantiations sep_form can name (its FS follows from FP and raw)
     if (f.quad && f.FP == 28 && f.raw) BH_EPI(BH_Q, 28, true, 48);
@@ -2377,6 +2599,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     else if (f.FP == 44) BH_EPI(BH_1, 44, true);
     else return (int)hipErrorInvalidValue;
 #undef BH_1
+#undef BH_FIX_true
+#undef BH_FIX__
 #undef BH_Q
 #undef BH_EPI
 #undef BH_SEPQ
@@ -2391,15 +2615,19 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* c, const uint32_t* same,
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
-                                                                          uint32_t h, hipStream_t s) {
+                                                                          uint32_t h, int32_t residual_org, hipStream_t s) {
     if (n_cols > w || n_rows > h || !list || !same) return (int)hipErrorInvalidValue;  // the list of this frame's plan
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
     if (g_dry) {
-        note_launch(epi == EPI_Y ? "fixup/1" : "fixup/2", w, h, n_cols, n_rows, 0u, 0u);
-        return same_ok(w, h, same, list, n_cols, n_rows) && chk(list == same + 2u * ((size_t)w + h), "fix-up list "
-                                                                "is not its plan's")
-                   ? 0
-                   : (int)hipErrorInvalidValue;
+        // residual_org < 0: the list of every inexact column and row, right after the plan; else the residual
+        // list of the in-block fix at that grid origin (crossing columns and rows only)
+        note_launch(epi == EPI_Y ? (residual_org < 0 ? "fixup/1" : "fixup/1r") : "fixup/2", w, h, n_cols, n_rows, 0u, 0u);
+        const bool ok = residual_org < 0
+                            ? same_ok(w, h, same, list, n_cols, n_rows) &&
+                                  chk(list == same + 2u * ((size_t)w + h), "fix-up list is not its plan's")
+                            : same_ok(w, h, same, nullptr, 0u, 0u, false) &&
+                                  residual_ok(w, h, same, list, n_cols, n_rows, (uint32_t)residual_org);
+        return ok ? 0 : (int)hipErrorInvalidValue;
     }
     if (n == 0) return 0;
     const Tables tb{lut, enc, buckets, codes};
@@ -2545,7 +2773,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     }
     if (shader == SH_UP && !P.valid && sep && sep_form(sep_ext, ow, oh).FP != 0 && !g_no_sep) {
         return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, rx, ry, sep, sep_ext, EPI_PLAIN, nullptr, nullptr,
-                                   nullptr, out, nullptr, ow, oh, s);
+                                   nullptr, out, nullptr, ow, oh, 0u, false, s);
     }
     if (g_dry) {  // pass_kernel: an up pass stages through with_source<FP_UP>; the others read clamped indices
         note_launch(shader == SH_UP ? (P.valid ? "pass_up_tap" : "pass_up") : shader == SH_COPY ? "pass_copy"

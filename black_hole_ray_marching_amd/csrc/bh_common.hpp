@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/bh_render.h"
 
@@ -243,7 +244,7 @@ constexpr uint32_t bh_bloom_shader_copy = 0, bh_bloom_shader_down = 1, bh_bloom_
 // block footprint side (or -1)
 extern "C" __attribute__((visibility("hidden"))) int bh_bloom_sep_plan(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                      uint32_t th, uint32_t rx, uint32_t ry,
-                                                                     uint32_t* outp);
+                                                                     uint32_t* outp, uint32_t org);
 // an up pass from its separable plan with an epilogue (bh_bloom.hip SepEpi: 0 plain, 1 Y, 2 final)
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const float* lut, const float* enc,
                                                                         const uint8_t* buckets, const uint32_t* codes,
@@ -252,14 +253,15 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         const uint32_t* sep, int ext, uint32_t epi,
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
-                                                                        uint32_t ow, uint32_t oh, hipStream_t s);
+                                                                        uint32_t ow, uint32_t oh, uint32_t org, bool fix,
+                                                                        hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const float* lut, const float* enc,
                                                                           const uint8_t* buckets, const uint32_t* codes,
                                                                           uint32_t epi, const uint32_t* a, const uint32_t* b,
                                                                           const uint32_t* c, const uint32_t* same,
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
-                                                                          uint32_t h, hipStream_t s);
+                                                                          uint32_t h, int32_t residual_org, hipStream_t s);
 // two downsamples a -> mw x mh -> out in one pass (the intermediate level not stored)
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const float* lut, const float* enc,
                                                                           const uint8_t* buckets, const uint32_t* codes,
@@ -286,7 +288,13 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan
 // Dry mode (bh_bloom_check): between begin and end the bloom launchers check their launch instead of launching.
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_verify(uint32_t ow, uint32_t oh, uint32_t tw,
                                                                         uint32_t th, uint32_t rx, uint32_t ry,
-                                                                        const uint32_t* plan, int ext, std::string* why);
+                                                                        const uint32_t* plan, int ext, uint32_t org, bool fix,
+                                                                        std::string* why);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh);
+// the quad grid origin of the in-block fix for a same-size plan, and its residual (crossing) columns / rows
+extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                          std::vector<uint32_t>* cols,
+                                                                          std::vector<uint32_t>* rows);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                          uint32_t nc, uint32_t nr, std::string* why);
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void);

@@ -70,10 +70,13 @@ struct bh_ctx {
     // ext: the largest block footprint side (up passes); nc, nr: the inexact columns / rows (same plan)
     // host: the plan's host copy in bh_bloom_check's dry mode (dev then points into it; never freed as device memory)
     struct SepPlan {
-        std::array<uint32_t, 6> key{};
+        std::array<uint32_t, 8> key{};  // ow, oh, tw, th, rx, ry, grid origin, in-block fix
         uint32_t* dev = nullptr;
         int ext = 0;
         uint32_t nc = 0, nr = 0;
+        // same-size plan: the quad grid origin of the in-block fix and its residual (crossing) columns / rows,
+        // listed after the full list
+        uint32_t org = 0, nrc = 0, nrr = 0;
         std::shared_ptr<std::vector<uint32_t>> host;
     };
     struct BloomScratch {
@@ -692,8 +695,8 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 // Returned by value: the cache is a vector that later plans reallocate.  (Round 4's memory-access fault:
 // a pointer into it, held across the next call, read a freed record's fix-up counts)
 bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* dry_fail, uint32_t ow, uint32_t oh,
-                         uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry, int* err) {
-    const std::array<uint32_t, 6> key{ow, oh, tw, th, rx, ry};
+                         uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry, int* err, uint32_t org = 0, bool fix = false) {
+    const std::array<uint32_t, 8> key{ow, oh, tw, th, rx, ry, org, fix ? 1u : 0u};
     for (const auto& p : b->sep_plans)
         if (p.key == key) return p;
     bh_ctx::SepPlan P;
@@ -707,8 +710,8 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
     bool ok;
     if (rx) {
         h->resize(32u * ((size_t)ow + oh));
-        P.ext = bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h->data());
-        ok = P.ext >= 0 && bh_bloom_sep_verify(ow, oh, tw, th, rx, ry, h->data(), P.ext, &why);
+        P.ext = bh_bloom_sep_plan(ow, oh, tw, th, rx, ry, h->data(), org);
+        ok = P.ext >= 0 && bh_bloom_sep_verify(ow, oh, tw, th, rx, ry, h->data(), P.ext, org, fix, &why);
     } else {
         h->resize(2u * ((size_t)ow + oh));
         ok = bh_bloom_same_plan(ow, oh, h->data());
@@ -723,6 +726,14 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
             h->insert(h->end(), cols.begin(), cols.end());
             h->insert(h->end(), rows.begin(), rows.end());
             ok = bh_bloom_same_verify(ow, oh, h->data(), P.nc, P.nr, &why);
+            if (ok) {  // the in-block fix's grid origin and residual list (checked where the fix-up launches)
+                std::vector<uint32_t> rc, rr;
+                P.org = bh_bloom_same_org(ow, oh, h->data(), &rc, &rr);
+                P.nrc = (uint32_t)rc.size();
+                P.nrr = (uint32_t)rr.size();
+                h->insert(h->end(), rc.begin(), rc.end());
+                h->insert(h->end(), rr.begin(), rr.end());
+            }
         }
     }
     if (!ok) {
@@ -841,19 +852,28 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
         // inexact columns and rows; other plans run the plain pass and the plan remix kernels.
         const uint32_t* plan = same.dev;
         const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
+        const uint32_t* residual = list ? list + same.nc + same.nr : nullptr;
+        // A/B: BH_BLOOM_NO_FIX runs the Y epilogue without the in-block fix (every inexact pixel in the fix-up)
+        static const bool no_fix = std::getenv("BH_BLOOM_NO_FIX") != nullptr;
         // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
         // fix-up of the inexact pixels -- or the plain pass and the remix kernel
         auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
                             uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
             if (R.err != 0) return;
             bh_ctx::SepPlan sp{};
+            // the Y epilogue's in-block fix (quad kernel): its grid at the same-size plan's origin, and the fix-up
+            // pass over the residual list only
+            const bool fix = epi == 1u && !no_fix;
+            const uint32_t org = fix ? same.org : 0u;
             if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
-                sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err);
+                sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err, org, fix);
             if (R.err != 0) return;
             if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
-                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, s) == 0) {
+                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, org, fix, s) == 0) {
+                const bool fixed = fix && bh_bloom_sep_is_quad(sp.ext, W, H);
                 R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
-                                              plan, list, same.nc, same.nr, dst, W, H, s);
+                                              plan, fixed ? residual : list, fixed ? same.nrc : same.nc,
+                                              fixed ? same.nrr : same.nr, dst, W, H, fixed ? (int32_t)same.org : -1, s);
                 return;
             }
             R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);

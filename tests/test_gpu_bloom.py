@@ -49,6 +49,10 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # fuses them; the up passes take the separable plan (per-column /
                                         # per-row taps from the host); also thin frames
                                         (1080, 1920, 3), (720, 1280, 3), (1080, 1920, 5), (7, 300, 3), (300, 7, 3),
+                                        # the Y epilogue's in-block fix with a residual fix-up list (1366: 6
+                                        # inexact columns cross a block edge at every origin that keeps 43
+                                        # block columns) and a nonzero grid origin (720 rows: 14)
+                                        (768, 1366, 3),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
                                         (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
@@ -68,7 +72,10 @@ def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
 
 
 @pytest.mark.parametrize("H,W,levels,sparse", [(128, 256, 3, False), (256, 512, 3, False), (120, 200, 3, False),
-                                               (256, 512, 3, True), (512, 1024, 3, True)])
+                                               (256, 512, 3, True), (512, 1024, 3, True),
+                                               # the general fused chain's quad passes and in-block fix
+                                               # with alpha below 255 (no opaque-block form)
+                                               (1080, 1920, 3, False), (720, 1280, 3, True), (768, 1366, 3, False)])
 def test_bloom_bitexact_any_alpha(torch_cuda, sky_small, H, W, levels, sparse):
     """Inputs with every alpha byte (the march writes 255, but bh_bloom takes any BGRA8 texels): the
     exact fma forms of the standard-plan kernels (acc_scaled, clerp, remix) rest on the products by

@@ -45,7 +45,7 @@ FUSED_WORK = {  # bh_bloom_check form of the fused chain -> the reference passes
     "final48": ("up", "remix", "remix"), "final0": ("up", "remix", "remix"), "final": ("up", "remix", "remix"),
     "up2_12": ("up",), "up2_3": ("up",), "up2_0": ("up",), "pass_up": ("up",), "pass_up_tap": ("up",),
     "pass_down": ("down",), "pass_copy": ("copy",), "pass_remix": ("remix",), "remix_plan": ("remix",),
-    "remix2_plan": ("remix", "remix"), "fixup/1": (), "fixup/2": (),
+    "remix2_plan": ("remix", "remix"), "fixup/1": (), "fixup/1r": (), "fixup/2": (),
 }
 
 
@@ -57,7 +57,7 @@ def minimal_ops(launches):
     total = 0
     for form, ow, oh, tw, th, rx, ry in launches:
         if form.startswith("sep"):
-            kinds = {"0": ("up",), "1": ("up", "remix"), "2": ("up", "remix", "remix")}[form.split("/")[1]]
+            kinds = {"0": ("up",), "1": ("up", "remix"), "2": ("up", "remix", "remix")}[form.split("/")[1][0]]
         elif form == "down2":
             total += OPS["down"] * rx * ry  # the intermediate level (mw x mh)
             kinds = ("down",)
@@ -90,7 +90,8 @@ def form_of(name):
     n = name.split("(")[0]
     if "up_sepq_kernel<" in n:
         a = n.split("<")[1].rstrip(">").split(",")
-        return f"sepq{int(a[0])}{'r' if a[2].strip() == 'true' else ''}/{int(a[1].strip().rstrip('u'))}"
+        fix = "f" if len(a) > 4 and a[4].strip() == "true" else ""
+        return f"sepq{int(a[0])}{'r' if a[2].strip() == 'true' else ''}/{int(a[1].strip().rstrip('u'))}{fix}"
     if "up_sep_kernel<" in n:
         a = n.split("<")[1].rstrip(">").split(",")
         return f"sep{int(a[0])}{'r' if a[2].strip() == 'true' else ''}/{int(a[1].strip().rstrip('u'))}"
