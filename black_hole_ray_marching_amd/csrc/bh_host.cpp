@@ -43,6 +43,12 @@ struct bh_ctx {
         uint64_t last_use = 0;
         bool valid = false;                  // costs and histogram agree (false: start afresh)
         bool captured = false;               // used by a launch captured into a graph: never evicted
+        // Which frames the buffers describe (frame_cost_key): the costs in tile_cost (and the histogram the
+        // counters hold of them, always pending) are those of a frame with key cost_key; the current order
+        // was built from costs with key order_key.  A launch whose frame 0 has the key of both (a repeated
+        // frame: a fixed camera) needs neither the order build nor new costs -- the march's step counts, and
+        // so the costs, are a function of that key.
+        uint64_t cost_key = 0, order_key = ~0ull;
         uint8_t* tile_cost = nullptr;
         uint32_t* order = nullptr;
         uint32_t* counters = nullptr;        // ORDER_WORDS words (bh_common.hpp)
@@ -1183,6 +1189,28 @@ static void frame_args(const bh_camera_uniform* cam, float rs, const bh_render_d
     F->dbg_n_rk = d->dbg_n_rk; F->dbg_fate = d->dbg_fate; F->dbg_steps = d->dbg_steps;
 }
 
+// What a frame's per-tile costs (the march's step counts) depend on: the camera, the shader uniforms and the
+// launch shape -- FNV-1a over those fields' bits (padding and the unused bg_brightness left out).  The
+// outputs, their format and the sky do not change a step count.
+static uint64_t frame_cost_key(const bh_camera_uniform* cam, const bh_uniforms* U, const bh_render_desc* d) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        const unsigned char* b = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    };
+    mix(cam->pos, sizeof(float) * 3);
+    for (int k = 0; k < 3; ++k) mix(cam->world_tri[k], sizeof(float) * 3);
+    for (int k = 0; k < 3; ++k) mix(cam->screen_tri[k], sizeof(float) * 3);
+    mix(&U->rs, 4); mix(&U->delta_time_mult, 4); mix(&U->blackout_eh, 4); mix(&U->max_dist, 4);
+    mix(&U->distortion_power, 4);
+    const uint64_t pser = d->partition ? d->partition->serial : 0u;
+    const uint32_t f[9] = {d->width, d->height, d->max_iters, d->scene_flags, d->math, d->layout, d->shard_index,
+                           d->shard_count, d->schedule};
+    mix(f, sizeof f);
+    mix(&pser, sizeof pser);
+    return h | 1u;  // never 0: 0 marks the fresh state's all-zero costs
+}
+
 static bool same_launch(const bh_render_desc* a, const bh_render_desc* b) {
     return a->width == b->width && a->height == b->height && a->max_iters == b->max_iters &&
            a->scene_flags == b->scene_flags && a->format == b->format && a->math == b->math &&
@@ -1328,13 +1356,30 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
             if (he == hipSuccess) he = hipMemsetAsync(os->tile_cost, 0, nt, s);
             if (he != hipSuccess) return hip_fail(he, "temporal order reset");
             os->valid = true;
+            os->cost_key = 0u;
+            os->order_key = ~0ull;
         }
-        int oe = bh_launch_build_order(os->tile_cost, a.n_tiles, a.order_block, a.order_centre, os->counters,
-                                       os->order, s);
-        if (oe != 0) { os->valid = false; return hip_fail((hipError_t)oe, "order kernels"); }
+        // The order build consumes the histogram the last march accumulated (and zeroes the counters), and
+        // the march accumulates the next: at every launch boundary the counters hold the histogram of the
+        // costs in tile_cost, also across graph replays, which repeat a captured launch as it was.  A launch
+        // whose frame repeats the one the order was learned from (its key equals both the order's and the
+        // costs') skips the pair: no build, and a march that writes no costs -- the pending histogram still
+        // describes the unchanged costs.  The host's keys only decide the skip; a replay that changed the
+        // buffers behind them costs at most a stale order, never a disagreement.  BH_ORDER_ALWAYS (A/B):
+        // build and write on every launch, as before round 5.
+        static const bool always = std::getenv("BH_ORDER_ALWAYS") != nullptr;
+        const uint64_t key = frame_cost_key(&cams[0], U, d);
+        const bool repeat = !always && os->order_key == os->cost_key && os->cost_key == key;
+        if (!repeat) {
+            int oe = bh_launch_build_order(os->tile_cost, a.n_tiles, a.order_block, a.order_centre, os->counters,
+                                           os->order, s);
+            if (oe != 0) { os->valid = false; return hip_fail((hipError_t)oe, "order kernels"); }
+            os->order_key = os->cost_key;
+            os->cost_key = key;
+        }
         a.order = os->order;
-        a.tile_cost = os->tile_cost;
-        a.order_tot = os->counters;
+        a.tile_cost = repeat ? nullptr : os->tile_cost;
+        a.order_tot = repeat ? nullptr : os->counters;
     }
     int e = d->math != BH_MATH_EXACT ? bh_launch_march_fast(a, sched, c->counters, c->grid_fast, s)
             : march_variant_issue_order(d, a.n_tiles, a.n_frames, c->cus)

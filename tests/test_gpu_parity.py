@@ -408,6 +408,63 @@ def test_temporal_order_is_a_permutation_across_blocks(torch_cuda, sky_small, W,
     scene.close()
 
 
+def test_repeated_frames_skip_the_order_build_and_stay_exact(torch_cuda, sky_small):
+    """A launch whose frame repeats the one the dispatch order was learned from runs no order build and
+    writes no costs (bh_host.cpp, OrderState::order_key); every path keeps the counters holding the
+    histogram of the stored costs, also in graphs captured either way (a march alone, or build + writing
+    march) and replayed between eager renders of other cameras.  Every frame covers every tile once
+    (NaN-filled targets, a partial last order block) and equals the static order's bytes."""
+    torch = torch_cuda
+    W, H, cap = 1496, 1000, 64
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
+    s = torch.cuda.Stream()
+    refs = {}
+    for cam in ("A", "B", "E"):
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        st = torch.full((H, W, 4), float("nan"), device="cuda")
+        scene.render(st, None, schedule=bh.BH_SCHED_TILE | bh.BH_SCHED_FLAG_STATIC_ORDER, stream=s)
+        torch.cuda.synchronize()
+        assert not torch.isnan(st).any()
+        refs[cam] = st.view(torch.int32).clone()
+    out = torch.empty((H, W, 4), device="cuda")
+
+    def eager(cam, i):
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        out.fill_(float("nan"))
+        scene.render(out, None, stream=s)
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), refs[cam]), f"eager {cam} #{i}"
+
+    def captured(cam, replays):
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            scene.render(out, None, stream=s)
+        for r in range(replays):
+            out.fill_(float("nan"))
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out.view(torch.int32), refs[cam]), f"replay {cam} #{r}"
+        return g
+
+    for i in range(3):
+        eager("A", i)            # build + write twice (fresh costs, then A's), then a repeat: neither
+    gA = captured("A", 3)        # a repeat captured: a march that writes nothing
+    eager("B", 0)                # build (from A's costs) + write B's
+    gB = captured("B", 3)        # build (from B's costs) + writing march, per replay
+    for i, cam in enumerate(["A", "A", "E", "B", "B", "B", "A"]):
+        eager(cam, i)
+    for g, cam in ((gA, "A"), (gB, "B")):
+        scene.camera_uniform = camera_uniform(cam, W, H)
+        out.fill_(float("nan"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.view(torch.int32), refs[cam]), f"late replay {cam}"
+    eager("E", 9)
+    scene.close()
+
+
 @pytest.mark.parametrize("cam", ["A", "B"])
 def test_cycle_fast_forward_is_exact(torch_cuda, cam):
     """The tile schedule advances rays caught in an exact period-1/2 cycle straight to the cap
