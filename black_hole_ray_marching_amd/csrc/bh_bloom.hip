@@ -2366,20 +2366,21 @@ bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* l
 
 // The quad grid's origin for the in-block fix of a same-size plan (bh_bloom_same_plan): per axis the even
 // offset in [0, 32) with the fewest inexact columns (rows) whose sample crosses a block edge (ties: the
-// smallest) among the offsets that keep the axis's block count -- an extra column of blocks can start a
-// further round of resident blocks (1920 wide: 60 -> 61 blocks, 2074 blocks over the 2048 slots of 8 per CU),
-// dearer than a fix-up launch over a few residual columns -- as org = ox | oy << 16; the crossing ones into
-// cols / rows when given.
+// smallest), as org = ox | oy << 16; the crossing ones into cols / rows when given.  An offset may add a
+// column (row) of blocks: at 1920 x 1080 offset 8 (61 block columns, no residual) measured 0.1234 ms per
+// chain against 0.1265 for offset 0 (60 columns and a fix-up launch over the one crossing column)
+// (profiles/r05/bloom_org/).  BH_BLOOM_ORG_KEEP (A/B): only offsets that keep the block count.
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                           std::vector<uint32_t>* cols,
                                                                           std::vector<uint32_t>* rows) {
+    static const bool grow = std::getenv("BH_BLOOM_ORG_KEEP") == nullptr;
     uint32_t org = 0;
     for (int axis = 0; axis < 2; ++axis) {
         const uint32_t n = axis ? h : w, base = axis ? w : 0u;
         uint32_t best = 0, best_n = UINT32_MAX;
         const uint32_t blocks = (n + 31u) / 32u;
         for (uint32_t off = 0; off < 32u && best_n != 0u; off += 2u) {
-            if ((n + off + 31u) / 32u != blocks) break;  // offsets only grow the count
+            if ((n + off + 31u) / 32u != blocks && !grow) break;  // offsets only grow the count
             uint32_t c = 0;
             for (uint32_t x = 0; x < n && c < best_n; ++x) c += same_crosses(plan, base, x, off) ? 1u : 0u;
             if (c < best_n) { best_n = c; best = off; }

@@ -49,9 +49,9 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # fuses them; the up passes take the separable plan (per-column /
                                         # per-row taps from the host); also thin frames
                                         (1080, 1920, 3), (720, 1280, 3), (1080, 1920, 5), (7, 300, 3), (300, 7, 3),
-                                        # the Y epilogue's in-block fix with a residual fix-up list (1366: 6
-                                        # inexact columns cross a block edge at every origin that keeps 43
-                                        # block columns) and a nonzero grid origin (720 rows: 14)
+                                        # the Y epilogue's in-block fix with a residual fix-up list (1366: at
+                                        # every grid origin some inexact columns cross a block edge; 3 at the
+                                        # best) and nonzero grid origins (1920: 8, 720 rows: 14)
                                         (768, 1366, 3),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
