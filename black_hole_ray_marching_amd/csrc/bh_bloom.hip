@@ -770,17 +770,37 @@ __device__ uint32_t g_bp_hdr[BP_SLOTS][4];  // FP, EPI, grid blocks, output widt
 // the grid origin the host picks, bh_bloom_same_plan_org).  org: the block grid's origin, blocks start at
 // 32 k - (org & 0xFFFF) columns and 32 k - (org >> 16) rows (even offsets: a quad never straddles the frame
 // edge).
+// With EPI_FINAL (FIX2 below) the fix reaches two texels: out = remix(S(col), S(F)) with F = q(remix(S(Y),
+// S(B))) at the sample's texels, each of them exact (F is then the exact epilogue's own z) or itself sampled
+// -- B from the block's words, Y and col from the block's own words, all through LDS.  Its three barriers
+// come after the taps, so the dead tile holds the B, Y and F words and the dead plan entries the col words.
+constexpr uint32_t FIX_WORDS = 32u * 33u;  // one padded 32 x 32 array of words
+template <int FP, bool RAW, int FS>
+constexpr bool sepq_fix2_fits() {
+    return sizeof(std::conditional_t<RAW, uint32_t, float4>) * (FP * FS + FP / 2) >= 3u * FIX_WORDS * 4u;
+}
 template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>(), bool FIX = false>
 __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
                                                       const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
                                                       const uint2* __restrict__ same, Tex aux, uint32_t org) {
-    static_assert(!FIX || EPI == EPI_Y, "the in-block fix is EPI_Y's");
+    // FIX2: the final epilogue's fix (an instantiation whose tile cannot hold its words never takes it; the
+    // host does not request it there, bh_bloom_sep_fix_ok)
+    constexpr bool FIX1 = FIX && EPI == EPI_Y, FIX2 = FIX && EPI == EPI_FINAL && sepq_fix2_fits<FP, RAW, FS>();
+    using TileT = std::conditional_t<RAW, uint32_t, float4>;
     __shared__ Lds L;
-    __shared__ std::conditional_t<RAW, uint32_t, float4> tile[FP * FS + FP / 2];
+    __shared__ __attribute__((aligned(16))) unsigned char tile_mem[sizeof(TileT) * (FP * FS + FP / 2)];
+    TileT* const tile = reinterpret_cast<TileT*>(tile_mem);
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
     // the lanes instead of every second one (2-way bank conflicts)
-    __shared__ QEntry colp[8][2][16], rowp[8][2][16];
-    __shared__ uint32_t ublk[FIX ? 32 : 1][FIX ? 33 : 1];  // the block's U words (FIX)
+    __shared__ __attribute__((aligned(16))) QEntry cr[2][8][2][16];
+    auto& colp = cr[0];
+    auto& rowp = cr[1];
+    static_assert(sizeof(cr) >= 32u * 32u * 4u, "FIX2's col words");
+    __shared__ uint32_t ublk[FIX1 ? 32 : 1][FIX1 ? 33 : 1];  // the block's U words (FIX1)
+    __shared__ uint32_t okc[FIX2 ? 32 : 1], okr[FIX2 ? 32 : 1];  // FIX2: F of the block column / row computable
+    // FIX2: the same-size plan entries of the block's columns and rows, staged with the footprint (in registers
+    // across the taps they pushed the final pass past its 80 VGPRs into scratch)
+    __shared__ uint2 sce[FIX2 ? 32 : 1], sre[FIX2 ? 32 : 1];
 #if BH_BLOOM_PHASES
     uint32_t bp[5];
     const uint32_t bp_real0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -824,10 +844,14 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             rowp[i][j & 1u][j >> 1] = q_entry(ly * FS + (ly >> 1), ly, e);
         }
     }
+    if constexpr (FIX2) {  // every block column's and row's entry (clamped: one outside the frame is never read)
+        if (threadIdx.x < 32u) sce[threadIdx.x] = same[clampi((int32_t)(bx + threadIdx.x), 0, (int32_t)ow - 1)];
+        else if (threadIdx.x < 64u) sre[threadIdx.x - 32u] = same[ow + clampi((int32_t)(by + threadIdx.x - 32u), 0, (int32_t)oh - 1)];
+    }
     // own texels of the epilogue (four pixels), loaded before the tables, used last
     uint32_t o0[2][2], o1[2][2];
     bool in[2][2], exact[2][2];
-    uint2 scx[2] = {}, scy[2] = {};  // same-size plan entries of the quad's columns and rows (FIX)
+    uint2 scx[2] = {}, scy[2] = {};  // same-size plan entries of the quad's columns and rows (FIX1)
     uint32_t m = 0xFF000000u;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -841,7 +865,9 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             if constexpr (EPI != EPI_PLAIN) {
                 o0[b][c] = own0.px[pix];
                 if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
-                if constexpr (FIX) {
+                if constexpr (FIX2) {
+                    // exact[] after the staging barrier, from sce / sre
+                } else if constexpr (FIX1) {
                     if (b == 0) scx[c] = same[in[b][c] ? x : 0u];
                     if (c == 0) scy[b] = same[ow + (in[b][c] ? y : 0u)];
                     exact[b][c] = in[b][c] && scx[c].y == 0u && scy[b].y == 0u;
@@ -867,14 +893,21 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         m = min(m, raw[r]);
     }
     const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+    if constexpr (FIX2) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) exact[b][c] = in[b][c] && sce[2u * qx + c].y == 0u && sre[2u * qy + b].y == 0u;
+    }
     BP_T(2);
 #if BH_BLOOM_PHASES
     bp[3] = bp[2];
 #endif
     // a quad whose first pixel is outside is outside as a whole (even origin offsets); it has no taps, but
-    // with FIX its lanes still meet the block's barrier
+    // with FIX its lanes still meet the block's barriers
     const bool live = in[0][0];
-    if (!FIX && !live) {
+    uint32_t bw[2][2] = {}, fw[2][2] = {};  // FIX2: the quad's B words and (exact pixels) F words
+    if (!FIX1 && !FIX2 && !live) {
 #if BH_BLOOM_PHASES
         goto phases;
 #else
@@ -1035,20 +1068,104 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 } else {
                     const uint32_t ue = enc(L, u);
                     aux.px[pix] = ue;
-                    if constexpr (FIX) ublk[2u * qy + b][2u * qx + c] = ue;
+                    if constexpr (FIX1) ublk[2u * qy + b][2u * qx + c] = ue;
+                    if constexpr (FIX2) bw[b][c] = ue;
                     if (exact[b][c]) {
                         const F4 uq = dec<A1>(L, ue);
                         if constexpr (EPI == EPI_Y) {
                             out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), uq));
                         } else {
-                            const F4 z = quant<A1>(L, remix(dec<A1>(L, o1[b][c]), uq));
-                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), z));
+                            // z = q(Y + 0.5 B): F at this exact pixel, kept as its word for FIX2
+                            const uint32_t zq = enc(L, remix(dec<A1>(L, o1[b][c]), uq));
+                            if constexpr (FIX2) fw[b][c] = zq;
+                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), dec<A1>(L, zq)));
                         }
                     }
                 }
             }
         }  // live
-        if constexpr (FIX) {
+        if constexpr (FIX2) {
+            // the taps of every wave are done: the tile and the plan entries are dead
+            __syncthreads();
+            scx[0] = sce[2u * qx]; scx[1] = sce[2u * qx + 1u];
+            scy[0] = sre[2u * qy]; scy[1] = sre[2u * qy + 1u];
+            uint32_t(*const ub)[33] = reinterpret_cast<uint32_t(*)[33]>(tile_mem);
+            uint32_t(*const yb)[33] = ub + 32;
+            uint32_t(*const fb_)[33] = ub + 64;
+            uint32_t(*const cb)[32] = reinterpret_cast<uint32_t(*)[32]>(&cr[0][0][0][0]);
+            // a block column's (row's) F is computable here when it is exact or its sample's texels lie in
+            // the block (nonzero weights only)
+            auto axis_ok = [&](uint2 e, int32_t b0) {
+                if (e.y == 0u) return true;
+                return (uint32_t)((int32_t)(e.x & 0xFFFFu) - b0) <= 31u && (uint32_t)((int32_t)(e.x >> 16) - b0) <= 31u;
+            };
+            if (live) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (!in[b][c]) continue;
+                        const uint32_t py = 2u * qy + b, px = 2u * qx + c;
+                        ub[py][px] = bw[b][c];
+                        yb[py][px] = o1[b][c];
+                        cb[py][px] = o0[b][c];
+                        if (exact[b][c]) fb_[py][px] = fw[b][c];
+                    }
+            }
+            // every lane, live or not: a block row (column) outside the frame still has in-frame columns (rows)
+            if (qy == 0u) { okc[2u * qx] = axis_ok(scx[0], (int32_t)bx); okc[2u * qx + 1u] = axis_ok(scx[1], (int32_t)bx); }
+            if (qx == 0u) { okr[2u * qy] = axis_ok(scy[0], (int32_t)by); okr[2u * qy + 1u] = axis_ok(scy[1], (int32_t)by); }
+            __syncthreads();
+            // the sample's block-relative texels of one axis (a weight-0 texel repeats the first: t * 0 == +0)
+            auto texels = [&](uint2 e, int32_t b0, int32_t& t0, int32_t& t1, float& w) {
+                w = __uint_as_float(e.y);
+                t0 = (int32_t)(e.x & 0xFFFFu) - b0;
+                t1 = w != 0.0f ? (int32_t)(e.x >> 16) - b0 : t0;
+            };
+            auto D = [&](uint32_t w) {
+                const F4 d = dec<A1>(L, w);
+                return make_float4(d.r, d.g, d.b, d.a);
+            };
+            // F = q(remix(S(Y), S(B))) at this lane's inexact pixels whose F is computable
+            if (live) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (!in[b][c] || exact[b][c]) continue;
+                        const uint32_t py = 2u * qy + b, px = 2u * qx + c;
+                        if (okc[px] == 0u || okr[py] == 0u) continue;
+                        int32_t u0, u1, v0, v1;
+                        float fa, fb;
+                        texels(scx[c], (int32_t)bx, u0, u1, fa);
+                        texels(scy[b], (int32_t)by, v0, v1, fb);
+                        const F4 sy = lerp_plan(D(yb[v0][u0]), D(yb[v0][u1]), D(yb[v1][u0]), D(yb[v1][u1]), fa, fb);
+                        const F4 sb = lerp_plan(D(ub[v0][u0]), D(ub[v0][u1]), D(ub[v1][u0]), D(ub[v1][u1]), fa, fb);
+                        fb_[py][px] = enc(L, remix(sy, sb));
+                    }
+            }
+            __syncthreads();
+            // out = remix(S(col), S(F)) at the inexact pixels whose sample's texels lie in the block and have
+            // a computable F (fixup_gather_kernel<EPI_FINAL>'s arithmetic); the rest: the fix-up pass's
+            if (live) {
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        if (!in[b][c] || exact[b][c]) continue;
+                        int32_t u0, u1, v0, v1;
+                        float fa, fb;
+                        texels(scx[c], (int32_t)bx, u0, u1, fa);
+                        texels(scy[b], (int32_t)by, v0, v1, fb);
+                        if ((uint32_t)u0 > 31u || (uint32_t)u1 > 31u || (uint32_t)v0 > 31u || (uint32_t)v1 > 31u) continue;
+                        if (okc[u0] == 0u || okc[u1] == 0u || okr[v0] == 0u || okr[v1] == 0u) continue;
+                        const F4 sc = lerp_plan(D(cb[v0][u0]), D(cb[v0][u1]), D(cb[v1][u0]), D(cb[v1][u1]), fa, fb);
+                        const F4 sf = lerp_plan(D(fb_[v0][u0]), D(fb_[v0][u1]), D(fb_[v1][u0]), D(fb_[v1][u1]), fa, fb);
+                        out.px[(y0 + b) * ow + x0 + c] = enc(L, remix(sc, sf));
+                    }
+            }
+        }
+        if constexpr (FIX1) {
             // Y = remix(S(X), S(U1)) at the inexact pixels whose sample's texels (those of nonzero weight) lie
             // in this block: fixup_gather_kernel<EPI_Y>'s arithmetic, each texel from LDS (a texel of weight 0
             // enters the lerp as t * 0 == +0 for any finite t >= 0, as the fix-up's unread 0 does)
@@ -2338,14 +2455,24 @@ bool same_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list,
 }
 // Whether inexact column (row) x of an n-pixel axis samples a texel outside its 32-pixel block of a grid at
 // origin off: such a column's pixels are the fix-up pass's, the others up_sepq_kernel's in-block fix (FIX).
-bool same_crosses(const uint32_t* plan, uint32_t base, uint32_t x, uint32_t off) {
+// reach2 (the final epilogue's fix): also when a sampled texel is itself inexact and samples outside the block.
+bool same_crosses(const uint32_t* plan, uint32_t base, uint32_t x, uint32_t off, bool reach2 = false) {
     const uint32_t e = plan[2u * (base + x)], wbits = plan[2u * (base + x) + 1u];
     if (wbits == 0u) return false;  // exact: its own texel (same_ok)
     const uint32_t blk = (x + off) / 32u;
-    return ((e & 0xFFFFu) + off) / 32u != blk || ((e >> 16) + off) / 32u != blk;
+    const uint32_t t[2] = {e & 0xFFFFu, e >> 16};  // both of nonzero weight (0 < w < 1)
+    for (uint32_t u : t) {
+        if ((u + off) / 32u != blk) return true;
+        if (reach2 && plan[2u * (base + u) + 1u] != 0u) {
+            const uint32_t eu = plan[2u * (base + u)];
+            if (((eu & 0xFFFFu) + off) / 32u != blk || ((eu >> 16) + off) / 32u != blk) return true;
+        }
+    }
+    return false;
 }
 // The residual list at origin org: the crossing columns, then rows, ascending -- exactly what it must hold
-bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, uint32_t nr, uint32_t org) {
+bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, uint32_t nr, uint32_t org,
+                 bool reach2) {
     if (!chk(nc <= w && nr <= h && (org & 0xFFFFu) < 32u && (org >> 16) < 32u && org % 2u == 0u && (org >> 16) % 2u == 0u,
              "residual list: %u columns of %u, %u rows of %u, origin %u,%u", nc, w, nr, h, org & 0xFFFFu, org >> 16))
         return false;
@@ -2354,7 +2481,7 @@ bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* l
         const uint32_t* L = list + (axis ? nc : 0u);
         uint32_t k = 0;
         for (uint32_t x = 0; x < n; ++x)
-            if (same_crosses(plan, base, x, off)) {
+            if (same_crosses(plan, base, x, off, reach2)) {
                 if (!chk(k < cnt && L[k] == x, "residual list: crossing %s %u missing", axis ? "row" : "column", x)) return false;
                 ++k;
             }
@@ -2372,32 +2499,40 @@ bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* l
 // (profiles/r05/bloom_org/).  BH_BLOOM_ORG_KEEP (A/B): only offsets that keep the block count.
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                           std::vector<uint32_t>* cols,
-                                                                          std::vector<uint32_t>* rows) {
+                                                                          std::vector<uint32_t>* rows,
+                                                                          std::vector<uint32_t>* cols2,
+                                                                          std::vector<uint32_t>* rows2) {
     static const bool grow = std::getenv("BH_BLOOM_ORG_KEEP") == nullptr;
     uint32_t org = 0;
     for (int axis = 0; axis < 2; ++axis) {
         const uint32_t n = axis ? h : w, base = axis ? w : 0u;
-        uint32_t best = 0, best_n = UINT32_MAX;
+        // fewest crossings of the final epilogue's fix (reach 2), then of the Y epilogue's, then the offset
+        uint64_t best_n = UINT64_MAX;
+        uint32_t best = 0;
         const uint32_t blocks = (n + 31u) / 32u;
         for (uint32_t off = 0; off < 32u && best_n != 0u; off += 2u) {
             if ((n + off + 31u) / 32u != blocks && !grow) break;  // offsets only grow the count
-            uint32_t c = 0;
-            for (uint32_t x = 0; x < n && c < best_n; ++x) c += same_crosses(plan, base, x, off) ? 1u : 0u;
-            if (c < best_n) { best_n = c; best = off; }
+            uint64_t c2 = 0, c1 = 0;
+            for (uint32_t x = 0; x < n; ++x) {
+                c2 += same_crosses(plan, base, x, off, true) ? 1u : 0u;
+                c1 += same_crosses(plan, base, x, off) ? 1u : 0u;
+            }
+            if ((c2 << 32 | c1) < best_n) { best_n = c2 << 32 | c1; best = off; }
         }
         org |= best << (axis ? 16 : 0);
-        std::vector<uint32_t>* out = axis ? rows : cols;
-        if (out) {
+        for (int r = 0; r < 2; ++r) {
+            std::vector<uint32_t>* out = r ? (axis ? rows2 : cols2) : (axis ? rows : cols);
+            if (!out) continue;
             out->clear();
             for (uint32_t x = 0; x < n; ++x)
-                if (same_crosses(plan, base, x, best)) out->push_back(x);
+                if (same_crosses(plan, base, x, best, r == 1)) out->push_back(x);
         }
     }
     return org;
 }
 
 // whether bh_launch_bloom_sep runs a plan of these extents with the quad kernel (the in-block fix's form)
-extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_fix_ok(int ext, uint32_t ow, uint32_t oh, uint32_t epi);
 
 // The separable up pass's launch form for a plan's extents (low 16 bits: 16x16 blocks, high: 32x32): the
 // quad kernel when its footprint fits a 28 / 40 / 60 tile, else the one-pixel kernel at 24 / 44, else none
@@ -2435,8 +2570,16 @@ static SepForm sep_form(int ext, uint32_t ow, uint32_t oh) {
     return f;
 }
 
-extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh) {
-    return sep_form(ext, ow, oh).quad;
+// whether bh_launch_bloom_sep runs a plan of these extents with epilogue epi in the in-block fix form: the
+// quad kernel, and for the final epilogue a tile large enough for its words (sepq_fix2_fits)
+static bool sep_fix_form(const SepForm& f, uint32_t epi) {
+    if (!f.quad) return false;
+    if (epi == EPI_Y) return true;
+    const size_t tile = (f.raw ? 4u : 16u) * (size_t)(f.FP * f.FS + f.FP / 2);
+    return epi == EPI_FINAL && tile >= 3u * FIX_WORDS * 4u;
+}
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_fix_ok(int ext, uint32_t ow, uint32_t oh, uint32_t epi) {
+    return sep_fix_form(sep_form(ext, ow, oh), epi);
 }
 
 // bh_bloom_sep_plan's plan (host copy `plan`, extents `ext`) checked for the form bh_launch_bloom_sep takes:
@@ -2548,9 +2691,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         hipStream_t s) {
     const SepForm f = sep_form(ext, ow, oh);
     if (f.FP == 0 || !sep) return (int)hipErrorInvalidValue;
-    // the grid origin and the in-block fix are the quad kernel's; the fix only with the Y epilogue
+    // the grid origin and the in-block fix are the quad kernel's (the fix with the Y or final epilogue)
     if (!f.quad) org = 0u;
-    fix = fix && f.quad && epi == EPI_Y;
+    fix = fix && sep_fix_form(f, epi);
     if (g_dry) {  // the plan is a host copy: check the form's every read instead of launching
         char form[32];
         std::snprintf(form, sizeof form, "%s%d%s/%u%s", f.quad ? "sepq" : "sep", f.FP, f.raw ? "r" : "", epi, fix ? "f" : "");
@@ -2583,6 +2726,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     do {                                                                       \
         if (epi == EPI_Y && fix) LAUNCH(__VA_ARGS__, EPI_Y, true);             \
         else if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                  \
+        else if (epi == EPI_FINAL && fix) LAUNCH(__VA_ARGS__, EPI_FINAL, true); \
         else if (epi == EPI_FINAL) LAUNCH(__VA_ARGS__, EPI_FINAL, _);          \
         else LAUNCH(__VA_ARGS__, EPI_PLAIN, _);                                \
     } while (0)
@@ -2622,12 +2766,13 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
     if (g_dry) {
         // residual_org < 0: the list of every inexact column and row, right after the plan; else the residual
         // list of the in-block fix at that grid origin (crossing columns and rows only)
-        note_launch(epi == EPI_Y ? (residual_org < 0 ? "fixup/1" : "fixup/1r") : "fixup/2", w, h, n_cols, n_rows, 0u, 0u);
+        note_launch(residual_org < 0 ? (epi == EPI_Y ? "fixup/1" : "fixup/2") : (epi == EPI_Y ? "fixup/1r" : "fixup/2r"), w, h,
+                    n_cols, n_rows, 0u, 0u);
         const bool ok = residual_org < 0
                             ? same_ok(w, h, same, list, n_cols, n_rows) &&
                                   chk(list == same + 2u * ((size_t)w + h), "fix-up list is not its plan's")
                             : same_ok(w, h, same, nullptr, 0u, 0u, false) &&
-                                  residual_ok(w, h, same, list, n_cols, n_rows, (uint32_t)residual_org);
+                                  residual_ok(w, h, same, list, n_cols, n_rows, (uint32_t)residual_org, epi == EPI_FINAL);
         return ok ? 0 : (int)hipErrorInvalidValue;
     }
     if (n == 0) return 0;

@@ -290,11 +290,13 @@ extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_verify(uint32
                                                                         uint32_t th, uint32_t rx, uint32_t ry,
                                                                         const uint32_t* plan, int ext, uint32_t org, bool fix,
                                                                         std::string* why);
-extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_is_quad(int ext, uint32_t ow, uint32_t oh);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_sep_fix_ok(int ext, uint32_t ow, uint32_t oh, uint32_t epi);
 // the quad grid origin of the in-block fix for a same-size plan, and its residual (crossing) columns / rows
 extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                           std::vector<uint32_t>* cols,
-                                                                          std::vector<uint32_t>* rows);
+                                                                          std::vector<uint32_t>* rows,
+                                                                          std::vector<uint32_t>* cols2,
+                                                                          std::vector<uint32_t>* rows2);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                          uint32_t nc, uint32_t nr, std::string* why);
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void);

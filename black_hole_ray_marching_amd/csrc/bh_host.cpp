@@ -82,7 +82,7 @@ struct bh_ctx {
         uint32_t nc = 0, nr = 0;
         // same-size plan: the quad grid origin of the in-block fix and its residual (crossing) columns / rows,
         // listed after the full list
-        uint32_t org = 0, nrc = 0, nrr = 0;
+        uint32_t org = 0, nrc = 0, nrr = 0, nrc2 = 0, nrr2 = 0;  // residual lists of the Y / final epilogue
         std::shared_ptr<std::vector<uint32_t>> host;
     };
     struct BloomScratch {
@@ -733,12 +733,13 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
             h->insert(h->end(), rows.begin(), rows.end());
             ok = bh_bloom_same_verify(ow, oh, h->data(), P.nc, P.nr, &why);
             if (ok) {  // the in-block fix's grid origin and residual list (checked where the fix-up launches)
-                std::vector<uint32_t> rc, rr;
-                P.org = bh_bloom_same_org(ow, oh, h->data(), &rc, &rr);
+                std::vector<uint32_t> rc, rr, rc2, rr2;
+                P.org = bh_bloom_same_org(ow, oh, h->data(), &rc, &rr, &rc2, &rr2);
                 P.nrc = (uint32_t)rc.size();
                 P.nrr = (uint32_t)rr.size();
-                h->insert(h->end(), rc.begin(), rc.end());
-                h->insert(h->end(), rr.begin(), rr.end());
+                P.nrc2 = (uint32_t)rc2.size();
+                P.nrr2 = (uint32_t)rr2.size();
+                for (const auto* v : {&rc, &rr, &rc2, &rr2}) h->insert(h->end(), v->begin(), v->end());
             }
         }
     }
@@ -859,8 +860,12 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
         const uint32_t* plan = same.dev;
         const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
         const uint32_t* residual = list ? list + same.nc + same.nr : nullptr;
-        // A/B: BH_BLOOM_NO_FIX runs the Y epilogue without the in-block fix (every inexact pixel in the fix-up)
+        const uint32_t* residual2 = residual ? residual + same.nrc + same.nrr : nullptr;
+        // The Y epilogue's in-block fix is on (BH_BLOOM_NO_FIX: off, A/B); the final epilogue's (FIX2) only with
+        // BH_BLOOM_FIX2 -- measured slower than its fix-up pass (1920x1080 0.1237 -> 0.1256 ms: three block
+        // barriers in the chain's longest-lived waves; profiles/r05/bloom_fix2/)
         static const bool no_fix = std::getenv("BH_BLOOM_NO_FIX") != nullptr;
+        static const bool fix2 = std::getenv("BH_BLOOM_FIX2") != nullptr;
         // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
         // fix-up of the inexact pixels -- or the plain pass and the remix kernel
         auto fused_up = [&](uint32_t epi, const uint32_t* src, uint32_t sw, uint32_t sh, const uint32_t* res,
@@ -869,17 +874,19 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
             bh_ctx::SepPlan sp{};
             // the Y epilogue's in-block fix (quad kernel): its grid at the same-size plan's origin, and the fix-up
             // pass over the residual list only
-            const bool fix = epi == 1u && !no_fix;
+            const bool fix = epi == 1u ? !no_fix : fix2;
             const uint32_t org = fix ? same.org : 0u;
             if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
                 sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err, org, fix);
             if (R.err != 0) return;
             if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
                                               sp.ext, epi, own0, own1, plan, dst, aux, W, H, org, fix, s) == 0) {
-                const bool fixed = fix && bh_bloom_sep_is_quad(sp.ext, W, H);
+                const bool fixed = fix && bh_bloom_sep_fix_ok(sp.ext, W, H, epi);
+                const uint32_t* rl = epi == 1u ? residual : residual2;
+                const uint32_t rc = epi == 1u ? same.nrc : same.nrc2, rr = epi == 1u ? same.nrr : same.nrr2;
                 R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
-                                              plan, fixed ? residual : list, fixed ? same.nrc : same.nc,
-                                              fixed ? same.nrr : same.nr, dst, W, H, fixed ? (int32_t)same.org : -1, s);
+                                              plan, fixed ? rl : list, fixed ? rc : same.nc, fixed ? rr : same.nr, dst, W, H,
+                                              fixed ? (int32_t)same.org : -1, s);
                 return;
             }
             R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);

@@ -134,6 +134,24 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
 BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
 
 
+@pytest.mark.parametrize("env", [{"BH_BLOOM_FIX2": "1"}, {"BH_BLOOM_NO_FIX": "1"}, {"BH_BLOOM_ORG_KEEP": "1"}],
+                         ids=["fix2", "no_fix", "org_keep"])
+def test_bloom_switches_stay_bitexact(torch_cuda, env):
+    """The chain's A/B switches, which the library reads once per process, in a child process each: the final
+    epilogue's in-block fix (off by default), no in-block fix, and grid origins that keep the block count
+    (1920: a residual column) -- display sizes with opaque and with any alpha, a residual list (1366)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    e = dict(os.environ, **env)
+    e["PYTHONPATH"] = str(root) + os.pathsep + e.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, str(root / "tests" / "_bloom_env_check.py"), "1080x1920", "1080x1920:any",
+                        "720x1280:any", "768x1366", "768x1366:any"], env=e, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
 @pytest.mark.parametrize("path", BLOOM_GOLDEN, ids=[p.stem for p in BLOOM_GOLDEN])
 def test_bloom_matches_golden(torch_cuda, sky_small, path, schedule):

@@ -45,7 +45,7 @@ FUSED_WORK = {  # bh_bloom_check form of the fused chain -> the reference passes
     "final48": ("up", "remix", "remix"), "final0": ("up", "remix", "remix"), "final": ("up", "remix", "remix"),
     "up2_12": ("up",), "up2_3": ("up",), "up2_0": ("up",), "pass_up": ("up",), "pass_up_tap": ("up",),
     "pass_down": ("down",), "pass_copy": ("copy",), "pass_remix": ("remix",), "remix_plan": ("remix",),
-    "remix2_plan": ("remix", "remix"), "fixup/1": (), "fixup/1r": (), "fixup/2": (),
+    "remix2_plan": ("remix", "remix"), "fixup/1": (), "fixup/1r": (), "fixup/2": (), "fixup/2r": (),
 }
 
 
