@@ -76,8 +76,25 @@ __device__ __forceinline__ uint2 xcd_block() {
 #ifndef BH_BLOOM_ETAB
 #define BH_BLOOM_ETAB 0
 #endif
+// BH_BLOOM_ALUT_CONST (A/B): the alpha decode k/255 from a constant-memory table instead of LDS (1 KiB less
+// LDS per block; only blocks with a non-opaque texel read it)
+#ifndef BH_BLOOM_ALUT_CONST
+#define BH_BLOOM_ALUT_CONST 0
+#endif
+#if BH_BLOOM_ALUT_CONST
+struct AlphaTable {
+    float v[256];
+    constexpr AlphaTable() : v() {
+        for (int k = 0; k < 256; ++k) v[k] = (float)k / 255.0f;  // IEEE division, folded at compile time
+    }
+};
+__constant__ AlphaTable c_alut{};
+#endif
 struct Lds {
-    float lut[256], alut[256];
+    float lut[256];
+#if !BH_BLOOM_ALUT_CONST
+    float alut[256];
+#endif
 #if BH_BLOOM_ETAB
     uint32_t E[SRGB_CODES];
 #else
@@ -93,7 +110,9 @@ struct Tables {
 };
 __device__ __forceinline__ void load_tables(Tables tb, Lds& L) {
     L.lut[threadIdx.x] = tb.lut[threadIdx.x];
+#if !BH_BLOOM_ALUT_CONST
     L.alut[threadIdx.x] = (float)threadIdx.x / 255.0f;
+#endif
 #if BH_BLOOM_ETAB
     for (uint32_t i = threadIdx.x; i < (uint32_t)SRGB_CODES; i += 256) L.E[i] = tb.code[i];
 #else
@@ -123,7 +142,11 @@ __device__ __forceinline__ bool barrier_and(bool p) {
 }
 template <bool A1 = false>
 __device__ __forceinline__ F4 dec(const Lds& L, uint32_t t) {
+#if BH_BLOOM_ALUT_CONST
+    return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : c_alut.v[t >> 24]};
+#else
     return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : L.alut[t >> 24]};
+#endif
 }
 // lo <= hi: one v_med3_i32
 __device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return min(max(v, lo), hi); }
