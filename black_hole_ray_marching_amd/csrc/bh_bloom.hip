@@ -2593,6 +2593,19 @@ static SepForm sep_form(int ext, uint32_t ow, uint32_t oh) {
     return f;
 }
 
+// A/B: BH_BLOOM_CAP_<PLAIN|Y|FINAL>=n caps the quad pass of that epilogue at n blocks per CU (dynamic LDS
+// padding): a launch of 1.33 rounds of resident waves may finish sooner as 2 full rounds of less contended ones
+static size_t sepq_cap_pad(const void* fn, uint32_t epi) {
+    static const int cap[3] = {(int)env_u32("BH_BLOOM_CAP_PLAIN"), (int)env_u32("BH_BLOOM_CAP_Y"),
+                               (int)env_u32("BH_BLOOM_CAP_FINAL")};
+    const int n = epi < 3u ? cap[epi] : 0;
+    if (n <= 0) return 0;
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, fn) != hipSuccess) return 0;
+    const long want = 163840L / (n + 1) + 1 - (long)at.sharedSizeBytes;  // n + 1 blocks no longer fit
+    return want > 0 ? (size_t)want : 0;
+}
+
 // whether bh_launch_bloom_sep runs a plan of these extents with epilogue epi in the in-block fix form: the
 // quad kernel, and for the final epilogue a tile large enough for its words (sepq_fix2_fits)
 static bool sep_fix_form(const SepForm& f, uint32_t epi) {
@@ -2742,8 +2755,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
 #define BH_SEPQ(FP, E, RAW, FS, FX)                                                                                  \
     do {                                                                                                             \
         BH_BP_SLOT();                                                                                                \
-        hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS, FX>), gq, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X, \
-                           org);                                                                                     \
+        hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS, FX>), gq, dim3(256),                                      \
+                           sepq_cap_pad(reinterpret_cast<const void*>(&up_sepq_kernel<FP, E, RAW, FS, FX>), E), s, tb, A, \
+                           rx, ry, P, O, O0, O1, S, X, org);                                                         \
     } while (0)
 #define BH_EPI(LAUNCH, ...)                                                    \
     do {                                                                       \
