@@ -437,6 +437,12 @@ struct XOps {
         const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
         qm = fminf(qy, qx);
     }
+    // the disc and marker terms of sdf_from one by one (the per-term root-free step)
+    __device__ __forceinline__ float disc_from(v3 p, float rs, float rho2) {
+        const float rho = sqrt(rho2);
+        return fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
+    }
+    __device__ __forceinline__ float mark_from(float qm) { return sqrt(qm) - 0.5f; }
     __device__ __forceinline__ float sdf_from(v3 p, float rs, uint32_t flags, float rho2, float, float qm) {
         const float rho = sqrt(rho2);
         const float disc = fmaxf(fmaxf(rho - 6.0f * rs, -(rho - 3.0f * rs)), fabsf(p.y - 0.0f) - 0.02f);
@@ -482,6 +488,9 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 #ifndef BH_SKIP_STICKY
 #define BH_SKIP_STICKY 0
 #endif
+#ifndef BH_SDF_TERMS
+#define BH_SDF_TERMS 1  // the root-free test term by term on the wave-steps that fail it as a whole
+#endif
 #ifdef BH_DIAG_SLOW
 __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wave_steps;
 // one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
@@ -522,8 +531,14 @@ __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wa
 // In the exact build's core pass a wrong r (r2 outside the root core's domain) also raises the k1
 // division guard, so that step re-runs in IEEE ops, where the proof holds as written.
 // tests/test_skip.py checks the implication on adversarial samples of the step's float32 arithmetic.
-__device__ __forceinline__ float sdf_skip_slack(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
-                                                float qm, float qps) {
+// The same test term by term (BH_SDF_TERMS): each term's slack >= 0 alone proves that term's distance
+// >= T (1 - 2^-17.6) by the argument above, so a term whose slack holds can be left out of dist (taken as
+// +inf): if it was the minimum, every other term is at least as large and still gives RN(0.9 dist) >= dtr;
+// its surface test could not fire; and fminf drops a NaN term exactly as it drops +inf.
+// tests/test_skip.py::test_per_term_skip_keeps_dt_and_surface checks every subset of cleared terms.
+struct SdfSlack { float disc, mark, ps; };
+__device__ __forceinline__ SdfSlack sdf_term_slacks(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
+                                                   float qm, float qps) {
     const float T = __builtin_fmaf(dtr, 1.125f, 0.002f);
     const float u6 = T + 6.0f * a.rs, uy = T + 0.02f, um = T + 0.5f, up = T + 0.075f;
     // v - u^2 rounded once (fma): its sign is the sign of the exact v - u*u
@@ -531,8 +546,9 @@ __device__ __forceinline__ float sdf_skip_slack(const MarchArgs& a, uint32_t fla
     float mark = __builtin_fmaf(-um, um, qm);
     if (!(flags & BH_SCENE_DISC)) disc = __builtin_inff();
     if (!(flags & BH_SCENE_MARKERS)) mark = __builtin_inff();
-    return fminf(fminf(disc, mark), __builtin_fmaf(-up, up, qps));
+    return {disc, mark, __builtin_fmaf(-up, up, qps)};
 }
+__device__ __forceinline__ float sdf_skip_slack(const SdfSlack& t) { return fminf(fminf(t.disc, t.mark), t.ps); }
 #endif
 
 // UNI: every active lane of the wave is at loop iteration `it` (n_rk == it: the ping-pong loop), so the
@@ -610,8 +626,10 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         // the test (after a slow step only ~24 % of the next are fast: tools/skip_sim.py), then tests again
         const bool test = !BH_SKIP_STICKY || !sk || *sk == 0u;
         bool fast = false;
+        SdfSlack terms{0.0f, 0.0f, 0.0f};
         if (test) {
-            const float slack = blackout ? __builtin_inff() : sdf_skip_slack(a, scene_flags, dtr, rho2, yy, qm, qps);
+            terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps);
+            const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
             fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
         }
         if (BH_SKIP_STICKY && sk) *sk = (test && !fast) ? 1u : 0u;
@@ -622,6 +640,36 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
                 return true;
             }
             dt = dtr;
+        } else if (BH_SDF_TERMS && test && a.skip_sdf != 0u) {
+            // per term: a root only where some lane that stays needs it (sdf_term_slacks); where the disc
+            // and markers both clear, the photon sphere alone keeps the wave here (about 98 % of these
+            // wave-steps clear it, and 80 % one of the other two: tools/skip_sim.py)
+            const bool stay = !blackout;
+            const bool nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
+            const bool nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
+            const bool np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
+            float dv = __builtin_inff(), mv = __builtin_inff();
+            if (nd) {
+                dv = X.disc_from(ro, a.rs, rho2);
+                X.sq_arg(rho2);
+            }
+            if (nm) {
+                mv = X.mark_from(qm);
+                X.sq_arg(qm);
+            }
+            const float ds = fminf((scene_flags & BH_SCENE_DISC) ? dv : __builtin_inff(),
+                                   (scene_flags & BH_SCENE_MARKERS) ? mv : __builtin_inff());  // :285
+            if (blackout | (ds < MIN_DIST)) {                            // :286-288
+                fate = blackout ? (uint32_t)BH_FATE_BLACKOUT : (uint32_t)BH_FATE_SURFACE;
+                return true;
+            }
+            float dps = __builtin_inff();
+            if (np) {
+                dps = X.sqrt(qps) - 0.075f;
+                X.sq_arg(qps);
+            }
+            const float dist = fminf(ds, dps);                           // :299
+            dt = fminf(dist * 0.9f, dtr);                                // :307-310
         } else {
             const float ds = X.sdf_from(ro, a.rs, scene_flags, rho2, yy, qm);  // :285
             if constexpr (SFS == SF_DYN || SFS == BH_SCENE_DEFAULT) X.sq_args(rho2, qm);

@@ -79,6 +79,55 @@ def test_skip_implies_dt_equals_dtm_r(flags, rs, dtm):
     assert passed > 50_000  # the samples do exercise the skip
 
 
+def term_slacks(flags, dtr, rho2, yy, qm, qps, rs):
+    """sdf_term_slacks: the disc, marker and photon-sphere terms of the test, each on its own"""
+    T = fma32(dtr, 1.125, f32(0.002))
+    u6 = T + f32(6.0) * rs
+    uy, um, up = T + f32(0.02), T + f32(0.5), T + f32(0.075)
+    inf = np.full_like(dtr, np.inf)
+    disc = np.fmax(fms(u6, rho2), fms(uy, yy)) if flags & DISC else inf
+    mark = fms(um, qm) if flags & MARKERS else inf
+    return disc, mark, fms(up, qps)
+
+
+def step_without(flags, dtr, rho2, y, qm, qps, rs, skip_d, skip_m, skip_p):
+    """the per-term step (bh_march.hpp, BH_SDF_TERMS): a left-out term enters dist as +inf"""
+    rho = np.sqrt(rho2)
+    inf = f32(np.inf)
+    disc = np.where(skip_d, inf, np.fmax(np.fmax(rho - f32(6.0) * rs, -(rho - f32(3.0) * rs)), np.abs(y) - f32(0.02)))
+    m = np.where(skip_m, inf, np.sqrt(qm) - f32(0.5))
+    ds = np.fmin(disc if flags & DISC else inf, m if flags & MARKERS else inf)
+    dps = np.where(skip_p, inf, np.sqrt(qps) - f32(0.075))
+    dt = np.fmin(np.fmin(ds, dps) * f32(0.9), dtr)
+    return dt, ds < f32(0.001)
+
+
+@pytest.mark.parametrize("flags", [DISC | MARKERS, DISC, MARKERS])
+@pytest.mark.parametrize("rs,dtm", [(1.0, 0.5), (8.0, 0.5), (0.25, 0.01), (1.0, 3.0)])
+def test_per_term_skip_keeps_dt_and_surface(flags, rs, dtm):
+    """Any subset of the terms whose own slack holds may be left out of dist: the step's dt and surface
+    test are those of the full step, bit for bit (the wave leaves out a term only where every lane that
+    stays clears it, so a lane's left-out terms are always a subset of its cleared ones)."""
+    rng = np.random.default_rng(hash((flags, rs, dtm, "terms")) & 0xFFFFFFFF)
+    rs = f32(rs)
+    cleared = 0
+    for _ in range(1):
+        dtr, rho2, y, qm, qps = samples(rng, 150_000, rs, dtm)
+        yy = (y * y).astype(f32)
+        sd, sm, sp = term_slacks(flags, dtr, rho2, yy, qm, qps, rs)
+        cd, cm, cp = sd >= 0, sm >= 0, sp >= 0
+        dt, surface = full_step(flags, dtr, rho2, y, qm, qps, rs)
+        for mask in range(1, 8):
+            skip_d = cd & bool(mask & 1)
+            skip_m = cm & bool(mask & 2)
+            skip_p = cp & bool(mask & 4)
+            dt2, surface2 = step_without(flags, dtr, rho2, y, qm, qps, rs, skip_d, skip_m, skip_p)
+            bad = (dt2.view(np.int32) != dt.view(np.int32)) | (surface2 != surface)
+            assert not bad.any(), (mask, dtr[bad][:4], rho2[bad][:4], y[bad][:4], qm[bad][:4], qps[bad][:4])
+        cleared += int((cd | cm | cp).sum())
+    assert cleared > 50_000
+
+
 def test_skip_rejects_nan_and_infinite_thresholds():
     rs = f32(1.0)
     dtr = np.array([0.5, np.nan, 0.5, 0.5, np.inf, np.inf], f32)

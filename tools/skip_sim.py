@@ -60,6 +60,7 @@ def accel(p):
 
 
 wave_steps = skip_steps = exact_steps = 0
+term_combo = {}  # wave-steps that fail the all-terms test: which terms every live lane clears
 cond_hits = np.zeros(4)
 var_hits = {}
 tr_counts = [0, 0]
@@ -107,6 +108,15 @@ for it in range(a.cap):
                 "tight out, m; loose p": t_out & t_m & (qps - f32(0.01126) >= B)}
     for Rf in (40.0, 45.0, 50.0):
         variants[f"far r >= {Rf}"] = r2 >= f32(Rf * Rf)
+    # per-term clearance at wave level (tight forms) on the wave-steps the all-terms test sends to the roots
+    okw = lambda v: ((v | blackout) | ~live).reshape(-1, 64).all(1)  # noqa: E731
+    D, M, P = okw(t_y | t_out | t_in), okw(t_m), okw(t_p)
+    slow = act & ~(D & M & P)
+    for key, sel_ in (("disc+markers clear, photon not", D & M & ~P), ("photon clear, disc or markers not", P & ~(D & M)),
+                      ("disc clear only", D & ~M & ~P), ("markers clear only", M & ~D & ~P), ("none clear", ~D & ~M & ~P),
+                      ("disc+photon clear, markers not", D & P & ~M), ("markers+photon clear, disc not", M & P & ~D)):
+        term_combo[key] = term_combo.get(key, 0) + int((slow & sel_).sum())
+    term_combo["slow"] = term_combo.get("slow", 0) + int(slow.sum())
     # transitions of the wave-level decision (tight out|y, m, p): after a slow step, how often fast?
     dec = (((variants["tight out|y, m, p"] | blackout) | ~live).reshape(-1, 64).all(1))
     if it > 0:
@@ -147,3 +157,8 @@ print("live lane-steps %d: disc test fails %.3f, marker/photon test fails %.3f, 
 for kv, vv in var_hits.items():
     print(f"  {kv}: {vv / wave_steps:.3f}")
 print(f"after a slow wave-step: {tr_counts[0]} steps, of them fast {tr_counts[1] / max(tr_counts[0], 1):.3f}")
+sl = max(term_combo.get("slow", 0), 1)
+print(f"wave-steps taking the roots (tight all-terms test fails): {sl / wave_steps:.3f} of all; of them, per term:")
+for kv, vv in term_combo.items():
+    if kv != "slow":
+        print(f"  {kv}: {vv / sl:.3f}")
