@@ -421,6 +421,18 @@ struct XOps {
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
     // sdf_args: the arguments of its two roots (rho^2, the markers' qm) and y*y; sdf_from: the rest
+    // sdf_args in two parts: the disc's (rho^2, y*y) and the markers' (qm), the same operations
+    __device__ __forceinline__ void sdf_args_disc(v3 p, float& rho2, float& yy) {
+        rho2 = p.x * p.x + p.z * p.z;
+        yy = p.y * p.y;
+    }
+    __device__ __forceinline__ void sdf_args_mark(v3 p, float yy, float& qm) {
+        const float xx = p.x * p.x;
+        const float dz = -10.0f - p.z, zz = dz * dz;
+        const float ty = 10.0f - fabsf(p.y), tx = 10.0f - fabsf(p.x);
+        const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
+        qm = fminf(qy, qx);
+    }
     __device__ __forceinline__ void sdf_args(v3 p, float& rho2, float& yy, float& qm) {
         rho2 = p.x * p.x + p.z * p.z;
         // The four sphere arguments are q1,2 = (xx + (+-10 - y)^2) + zz and q3,4 = ((+-10 - x)^2 + yy)
@@ -491,6 +503,11 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 #ifndef BH_SDF_TERMS
 #define BH_SDF_TERMS 1  // the root-free test term by term on the wave-steps that fail it as a whole
 #endif
+#ifndef BH_SDF_RADII
+// terms cleared by the lane's radius alone, their arguments not formed (A/B, off: both radii 0.5217 ->
+// 0.5261 ms, the photon sphere's alone 0.5217 -> 0.5217; profiles/r05/sdf_radii/)
+#define BH_SDF_RADII 0
+#endif
 #ifdef BH_DIAG_SLOW
 __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wave_steps;
 // one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
@@ -537,16 +554,25 @@ __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wa
 // its surface test could not fire; and fminf drops a NaN term exactly as it drops +inf.
 // tests/test_skip.py::test_per_term_skip_keeps_dt_and_surface checks every subset of cleared terms.
 struct SdfSlack { float disc, mark, ps; };
+// m_on / ps_on false: that term already cleared by the lane radii (BH_SDF_RADII), its argument not formed
 __device__ __forceinline__ SdfSlack sdf_term_slacks(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
-                                                   float qm, float qps) {
+                                                   float qm, float qps, bool m_on = true, bool ps_on = true) {
     const float T = __builtin_fmaf(dtr, 1.125f, 0.002f);
-    const float u6 = T + 6.0f * a.rs, uy = T + 0.02f, um = T + 0.5f, up = T + 0.075f;
+    const float u6 = T + 6.0f * a.rs, uy = T + 0.02f;
     // v - u^2 rounded once (fma): its sign is the sign of the exact v - u*u
     float disc = fmaxf(__builtin_fmaf(-u6, u6, rho2), __builtin_fmaf(-uy, uy, yy));
-    float mark = __builtin_fmaf(-um, um, qm);
+    float mark = __builtin_inff(), ps = __builtin_inff();
+    if (m_on) {
+        const float um = T + 0.5f;
+        mark = __builtin_fmaf(-um, um, qm);
+    }
+    if (ps_on) {
+        const float up = T + 0.075f;
+        ps = __builtin_fmaf(-up, up, qps);
+    }
     if (!(flags & BH_SCENE_DISC)) disc = __builtin_inff();
     if (!(flags & BH_SCENE_MARKERS)) mark = __builtin_inff();
-    return {disc, mark, __builtin_fmaf(-up, up, qps)};
+    return {disc, mark, ps};
 }
 __device__ __forceinline__ float sdf_skip_slack(const SdfSlack& t) { return fminf(fminf(t.disc, t.mark), t.ps); }
 #endif
@@ -608,7 +634,25 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     } else
 #endif
     {
+#if !BH_FAST && BH_SDF_SKIP && BH_SDF_RADII
+    // Per-term radii (sdf_term_radii, bh_host.cpp): when every lane that stays lies beyond the photon sphere's
+    // radius, or outside the markers' band, that term clears without its argument (the wave forms no qps,
+    // no qm).  96 % of the headline's non-far wave-steps clear the photon sphere so, 20 % the markers
+    // (tools/skip_sim.py).
+    bool ps_on = true, m_on = true;
+    if constexpr (BRANCHY) {
+        const bool fin = r2 <= 0x1.fffffep127f;
+        ps_on = __builtin_amdgcn_ballot_w64(!((r2 >= a.ps_r2) & fin) & !blackout) != 0ull;
+        if (BH_SDF_RADII != 2)  // 2 (A/B): the photon sphere's radius only
+            m_on = __builtin_amdgcn_ballot_w64(!(((r2 >= a.mo_r2) | (r2 <= a.mi_r2)) & fin) & !blackout) != 0ull;
+    }
+    X.sdf_args_disc(ro, rho2, yy);
+    qm = 0.0f;
+    if (m_on) X.sdf_args_mark(ro, yy, qm);
+#else
     X.sdf_args(ro, rho2, yy, qm);                                      // the SDF roots' arguments
+    constexpr bool ps_on = true, m_on = true;
+#endif
 #if !BH_FAST && BH_SDF_SKIP
     // Root-free step (BRANCHY): dt = min(0.9 dist, dtm r) needs dist only where it could fall below
     // dtm r / 0.9, and the surface test only below MIN_DIST.  sdf_skip decides "dt == dtm r, no surface"
@@ -616,8 +660,11 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // the wave skips the three roots, their guards and the distance arithmetic.  Same bits: see sdf_skip.
     // The photon-sphere argument (:294) is formed before the exits for the test.
     if constexpr (BRANCHY) {
-        const v3 dc = sub(f.cps, ro);
-        const float qps = dot(dc, dc);
+        float qps = 0.0f;
+        if (ps_on) {
+            const v3 dc = sub(f.cps, ro);
+            qps = dot(dc, dc);
+        }
         // lanes that need the roots: slack < 0 or NaN, except those that leave by the blackout exit.  (The
         // blackout select becomes a branch around the test.  Taking the lane mask straight from the compare,
         // llvm.amdgcn.fcmp, and masking the blackout lanes as integers is 4 VALU fewer and measured 0.9 %
@@ -628,7 +675,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         bool fast = false;
         SdfSlack terms{0.0f, 0.0f, 0.0f};
         if (test) {
-            terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps);
+            terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps, m_on, ps_on);
             const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
             fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
         }
