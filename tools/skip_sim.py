@@ -61,6 +61,7 @@ def accel(p):
 
 wave_steps = skip_steps = exact_steps = 0
 term_combo = {}  # wave-steps that fail the all-terms test: which terms every live lane clears
+radius = {"steps": 0, "photon by radius": 0, "markers by radius": 0, "both": 0}  # non-far wave-steps
 cond_hits = np.zeros(4)
 var_hits = {}
 tr_counts = [0, 0]
@@ -108,6 +109,20 @@ for it in range(a.cap):
                 "tight out, m; loose p": t_out & t_m & (qps - f32(0.01126) >= B)}
     for Rf in (40.0, 45.0, 50.0):
         variants[f"far r >= {Rf}"] = r2 >= f32(Rf * Rf)
+    # per-term radii (bh_host.cpp sdf_term_radii): a wave whose staying lanes all lie beyond the photon sphere's
+    # radius, or outside the markers' band, clears that term without forming its argument
+    k = 1.1251 * 0.5
+    r_ps = 1.01 * (1.5 * 1.0001 + 0.078) / (1 - k)
+    r_mo = 1.01 * (10 * np.sqrt(2) + 0.5 + 0.003) / (1 - k)
+    r_mi = 0.99 * (10 * np.sqrt(2) - 0.5 - 0.003) / (1 + k)
+    far_w = (((r2 >= f32(41.5 ** 2 * 1.0201)) | blackout) | ~live).reshape(-1, 64).all(1)
+    nf = act & ~far_w
+    ps_w = (((r2 >= f32(r_ps ** 2)) | blackout) | ~live).reshape(-1, 64).all(1)
+    m_w = ((((r2 >= f32(r_mo ** 2)) | (r2 <= f32(r_mi ** 2))) | blackout) | ~live).reshape(-1, 64).all(1)
+    radius["steps"] += int(nf.sum())
+    radius["photon by radius"] += int((nf & ps_w).sum())
+    radius["markers by radius"] += int((nf & m_w).sum())
+    radius["both"] += int((nf & ps_w & m_w).sum())
     # per-term clearance at wave level (tight forms) on the wave-steps the all-terms test sends to the roots
     okw = lambda v: ((v | blackout) | ~live).reshape(-1, 64).all(1)  # noqa: E731
     D, M, P = okw(t_y | t_out | t_in), okw(t_m), okw(t_p)
@@ -157,6 +172,8 @@ print("live lane-steps %d: disc test fails %.3f, marker/photon test fails %.3f, 
 for kv, vv in var_hits.items():
     print(f"  {kv}: {vv / wave_steps:.3f}")
 print(f"after a slow wave-step: {tr_counts[0]} steps, of them fast {tr_counts[1] / max(tr_counts[0], 1):.3f}")
+print(f"non-far wave-steps {radius['steps'] / wave_steps:.3f} of all; of them " +
+      ", ".join(f"{k} {v / max(radius['steps'], 1):.3f}" for k, v in radius.items() if k != "steps"))
 sl = max(term_combo.get("slow", 0), 1)
 print(f"wave-steps taking the roots (tight all-terms test fails): {sl / wave_steps:.3f} of all; of them, per term:")
 for kv, vv in term_combo.items():
