@@ -1367,30 +1367,81 @@ __device__ __forceinline__ F4 finish_same(const Lds& L, const SameWords& s) {
 // same-size sample's texels are its pixel's own and one neighbour (t is within an ulp-sized offset of
 // the pixel's index), so F's plan entries are among the three preloaded per axis; `pick` reads the plan
 // for any other index.
+// rec (the host's records of the list, fixup_records): per entry two uint4, the column (row) and the plan
+// entries of it and of its two neighbours (clamped), so the pixel's column and row entries and F's
+// neighbours arrive with the list entry -- one dependent round trip fewer than list, then plan.
 template <uint32_t EPI>
 __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CTex B, CTex C,
                                                            const uint2* __restrict__ plan,
                                                            const uint32_t* __restrict__ list, uint32_t n_cols,
-                                                           uint32_t n_rows, Tex out) {
+                                                           uint32_t n_rows, Tex out, const uint4* __restrict__ rec) {
     __shared__ Lds L;
     const uint32_t W = out.w, H = out.h;
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x, nc = (uint64_t)n_cols * H;
     uint32_t x = 0u, y = 0u;
     bool live = true;
-    if (i < nc) {
-        x = list[i / H];
-        y = (uint32_t)(i % H);
+    uint2 cx, cy, PX[3], PY[3];
+    if (rec) {
+        uint32_t k = 0u;
+        bool col = true;
+        if (i < nc) {
+            k = (uint32_t)(i / H);
+            y = (uint32_t)(i % H);
+        } else {
+            const uint64_t j = i - nc;
+            live = j < (uint64_t)n_rows * W;
+            col = false;
+            if (live) {
+                k = n_cols + (uint32_t)(j / W);
+                x = (uint32_t)(j % W);
+            }
+        }
+        const uint4 r0 = rec[2u * k], r1 = rec[2u * k + 1u];
+        const uint2 e0 = make_uint2(r0.y, r0.z), e1 = make_uint2(r0.w, r1.x), e2 = make_uint2(r1.y, r1.z);
+        if (col) {
+            x = r0.x;
+            PX[0] = e0; PX[1] = e1; PX[2] = e2;
+            const uint32_t yc = min(y, H - 1u);
+            PY[1] = plan[W + yc];
+            if constexpr (EPI == EPI_FINAL) {
+                PY[0] = plan[W + (yc ? yc - 1u : 0u)];
+                PY[2] = plan[W + min(yc + 1u, H - 1u)];
+            }
+        } else {
+            y = r0.x;
+            PY[0] = e0; PY[1] = e1; PY[2] = e2;
+            const uint32_t xc = min(x, W - 1u);
+            PX[1] = plan[xc];
+            if constexpr (EPI == EPI_FINAL) {
+                PX[0] = plan[xc ? xc - 1u : 0u];
+                PX[2] = plan[min(xc + 1u, W - 1u)];
+            }
+        }
+        live = live && x < W && y < H;  // defensive: a list entry outside the frame
+        cx = PX[1];
+        cy = PY[1];
+        if (!live) { x = y = 0u; cx = plan[0]; cy = plan[W]; PX[0] = PX[2] = cx; PY[0] = PY[2] = cy; }
     } else {
-        const uint64_t j = i - nc;
-        live = j < (uint64_t)n_rows * W;
-        if (live) {
-            y = list[n_cols + j / W];
-            x = (uint32_t)(j % W);
+        if (i < nc) {
+            x = list[i / H];
+            y = (uint32_t)(i % H);
+        } else {
+            const uint64_t j = i - nc;
+            live = j < (uint64_t)n_rows * W;
+            if (live) {
+                y = list[n_cols + j / W];
+                x = (uint32_t)(j % W);
+            }
+        }
+        live = live && x < W && y < H;  // defensive: a list entry outside the frame
+        if (!live) x = y = 0u;
+        cx = plan[x];
+        cy = plan[W + y];
+        if constexpr (EPI == EPI_FINAL) {
+            PX[0] = plan[x ? x - 1u : 0u]; PX[1] = cx; PX[2] = plan[min(x + 1u, W - 1u)];
+            PY[0] = plan[W + (y ? y - 1u : 0u)]; PY[1] = cy; PY[2] = plan[W + min(y + 1u, H - 1u)];
         }
     }
-    live = live && x < W && y < H;  // defensive: a list entry outside the frame
-    if (!live) x = y = 0u;
-    const uint2 cx = plan[x], cy = plan[W + y];
     if (i >= nc && cx.y != 0u) live = false;  // an inexact column: its pixels are the first part's
     const SameWords a = gather_same(A, cx, cy);
     if constexpr (EPI == EPI_Y) {
@@ -1399,8 +1450,6 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         if (!live) return;
         out.px[y * W + x] = enc(L, remix(finish_same(L, a), finish_same(L, b)));
     } else {
-        const uint2 PX[3] = {plan[x ? x - 1u : 0u], cx, plan[min(x + 1u, W - 1u)]};
-        const uint2 PY[3] = {plan[W + (y ? y - 1u : 0u)], cy, plan[W + min(y + 1u, H - 1u)]};
         auto pick = [&](uint32_t u, uint32_t c, const uint2(&P)[3], uint32_t base) -> uint2 {
             if (u == c) return P[1];
             if (u + 1u == c) return P[0];
@@ -2512,7 +2561,41 @@ bool residual_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* l
     }
     return true;
 }
+// The fix-up records of a list (bh_bloom_fixup_records): entry k's column (row) and the plan entries of it and
+// of its clamped neighbours, exactly as the kernel would read them from the plan.
+bool records_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, uint32_t nr,
+                const uint32_t* rec) {
+    for (uint32_t k = 0; k < nc + nr; ++k) {
+        const uint32_t n = k < nc ? w : h, base = k < nc ? 0u : w, u = list[k];
+        const uint32_t* r = rec + 8u * k;
+        if (!chk(r[0] == u && u < n, "fix-up record %u names %u, its list %u", k, r[0], u)) return false;
+        const uint32_t nb[3] = {u ? u - 1u : 0u, u, std::min(u + 1u, n - 1u)};
+        for (int t = 0; t < 3; ++t)
+            if (!chk(r[1 + 2 * t] == plan[2u * (base + nb[t])] && r[2 + 2 * t] == plan[2u * (base + nb[t]) + 1u],
+                     "fix-up record %u: plan entry %u differs", k, nb[t]))
+                return false;
+    }
+    return true;
+}
 }  // namespace
+
+// The fix-up records of a list of n_cols columns then n_rows rows into out (8 words per entry, see
+// fixup_gather_kernel).
+extern "C" __attribute__((visibility("hidden"))) void bh_bloom_fixup_records(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                           const uint32_t* list, uint32_t nc, uint32_t nr,
+                                                                           uint32_t* out) {
+    for (uint32_t k = 0; k < nc + nr; ++k) {
+        const uint32_t n = k < nc ? w : h, base = k < nc ? 0u : w, u = std::min(list[k], n - 1u);
+        const uint32_t nb[3] = {u ? u - 1u : 0u, u, std::min(u + 1u, n - 1u)};
+        uint32_t* r = out + 8u * k;
+        r[0] = list[k];
+        for (int t = 0; t < 3; ++t) {
+            r[1 + 2 * t] = plan[2u * (base + nb[t])];
+            r[2 + 2 * t] = plan[2u * (base + nb[t]) + 1u];
+        }
+        r[7] = 0u;
+    }
+}
 
 // The quad grid's origin for the in-block fix of a same-size plan (bh_bloom_same_plan): per axis the even
 // offset in [0, 32) with the fewest inexact columns (rows) whose sample crosses a block edge (ties: the
@@ -2797,7 +2880,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* c, const uint32_t* same,
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
-                                                                          uint32_t h, int32_t residual_org, hipStream_t s) {
+                                                                          uint32_t h, int32_t residual_org, const uint32_t* recs,
+                                                                          hipStream_t s) {
     if (n_cols > w || n_rows > h || !list || !same) return (int)hipErrorInvalidValue;  // the list of this frame's plan
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
     if (g_dry) {
@@ -2810,19 +2894,21 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                   chk(list == same + 2u * ((size_t)w + h), "fix-up list is not its plan's")
                             : same_ok(w, h, same, nullptr, 0u, 0u, false) &&
                                   residual_ok(w, h, same, list, n_cols, n_rows, (uint32_t)residual_org, epi == EPI_FINAL);
-        return ok ? 0 : (int)hipErrorInvalidValue;
+        return ok && (!recs || records_ok(w, h, same, list, n_cols, n_rows, recs)) ? 0 : (int)hipErrorInvalidValue;
     }
     if (n == 0) return 0;
     const Tables tb{lut, enc, buckets, codes};
     const dim3 g((uint32_t)((n + 255u) / 256u));
     const uint2* S = reinterpret_cast<const uint2*>(same);
     static const bool per_sample = !BH_BLOOM_FIXUP_GATHER || std::getenv("BH_BLOOM_FIXUP_SAMPLE") != nullptr;  // A/B
+    static const bool no_rec = std::getenv("BH_BLOOM_FIXUP_NOREC") != nullptr;  // A/B: list, then plan
+    const uint4* R = no_rec ? nullptr : reinterpret_cast<const uint4*>(recs);
     if (!per_sample && epi == EPI_Y)
         hipLaunchKernelGGL(fixup_gather_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
-                           CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h});
+                           CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R);
     else if (!per_sample)
         hipLaunchKernelGGL(fixup_gather_kernel<EPI_FINAL>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
-                           CTex{c, w, h}, S, list, n_cols, n_rows, Tex{out, w, h});
+                           CTex{c, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R);
     else if (epi == EPI_Y)
         hipLaunchKernelGGL(fixup_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{b, w, h}, S, list,
                            n_cols, n_rows, Tex{out, w, h});

@@ -40,6 +40,9 @@ struct MarchArgs {
     uint32_t blackout_eh;
     uint32_t skip_sdf;         // the root-free step may run (bh_march.hpp, sdf_skip: dtm > 0, 0 < rs <= 8)
     float far_r2;              // r^2 beyond which a step needs no SDF argument (bh_host.cpp sdf_far_r2; +inf: off)
+    // per-term radii (bh_host.cpp sdf_term_radii): the photon-sphere term clears for r^2 >= ps_r2, the markers'
+    // for r^2 >= mo_r2 or r^2 <= mi_r2 (+inf / -1: off)
+    float ps_r2, mo_r2, mi_r2;
     // frame
     uint32_t width, height, max_iters, scene_flags;
     uint32_t format, layout;
@@ -261,7 +264,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* c, const uint32_t* same,
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
-                                                                          uint32_t h, int32_t residual_org, hipStream_t s);
+                                                                          uint32_t h, int32_t residual_org, const uint32_t* recs,
+                                                                          hipStream_t s);
+// the fix-up kernel's records of a list (8 words per entry: the index and the plan entries of it and its neighbours)
+extern "C" __attribute__((visibility("hidden"))) void bh_bloom_fixup_records(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                           const uint32_t* list, uint32_t nc, uint32_t nr,
+                                                                           uint32_t* out);
 // two downsamples a -> mw x mh -> out in one pass (the intermediate level not stored)
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_down2(const float* lut, const float* enc,
                                                                           const uint8_t* buckets, const uint32_t* codes,

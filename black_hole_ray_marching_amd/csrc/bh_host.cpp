@@ -83,6 +83,7 @@ struct bh_ctx {
         // same-size plan: the quad grid origin of the in-block fix and its residual (crossing) columns / rows,
         // listed after the full list
         uint32_t org = 0, nrc = 0, nrr = 0, nrc2 = 0, nrr2 = 0;  // residual lists of the Y / final epilogue
+        size_t rec = 0;  // word offset of the lists' fix-up records (full, residual 1, residual 2; 8 words each)
         std::shared_ptr<std::vector<uint32_t>> host;
     };
     struct BloomScratch {
@@ -740,6 +741,18 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
                 P.nrc2 = (uint32_t)rc2.size();
                 P.nrr2 = (uint32_t)rr2.size();
                 for (const auto* v : {&rc, &rr, &rc2, &rr2}) h->insert(h->end(), v->begin(), v->end());
+                // the three lists' records, 16-byte aligned (the kernel reads them as uint4)
+                const size_t lists = 2u * ((size_t)ow + oh), n_all = P.nc + P.nr + P.nrc + P.nrr + P.nrc2 + P.nrr2;
+                h->resize((h->size() + 3u) & ~(size_t)3u, 0u);
+                P.rec = h->size();
+                h->resize(P.rec + 8u * n_all, 0u);
+                uint32_t* R = h->data() + P.rec;
+                const uint32_t* L = h->data() + lists;
+                bh_bloom_fixup_records(ow, oh, h->data(), L, P.nc, P.nr, R);
+                L += P.nc + P.nr; R += 8u * (P.nc + P.nr);
+                bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc, P.nrr, R);
+                L += P.nrc + P.nrr; R += 8u * (P.nrc + P.nrr);
+                bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc2, P.nrr2, R);
             }
         }
     }
@@ -884,9 +897,12 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
                 const bool fixed = fix && bh_bloom_sep_fix_ok(sp.ext, W, H, epi);
                 const uint32_t* rl = epi == 1u ? residual : residual2;
                 const uint32_t rc = epi == 1u ? same.nrc : same.nrc2, rr = epi == 1u ? same.nrr : same.nrr2;
+                // the list's records: full, residual 1, residual 2 in that order after same.rec
+                const size_t rk = !fixed ? 0u : epi == 1u ? same.nc + same.nr : same.nc + same.nr + same.nrc + same.nrr;
+                const uint32_t* recs = same.rec ? plan + same.rec + 8u * rk : nullptr;
                 R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
                                               plan, fixed ? rl : list, fixed ? rc : same.nc, fixed ? rr : same.nr, dst, W, H,
-                                              fixed ? (int32_t)same.org : -1, s);
+                                              fixed ? (int32_t)same.org : -1, recs, s);
                 return;
             }
             R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);
@@ -1251,6 +1267,26 @@ static float sdf_far_r2(float rs, float dtm) {
     return std::nextafter((float)(R * R), INFINITY);
 }
 
+// The same bound term by term (bh_march.hpp, BH_SDF_RADII): a lane at distance R from the origin is at least
+// R - 1.5 rs - 0.075 from the photon sphere's surface and at least R - 10 sqrt2 - 0.5 (outside the markers'
+// centre circle) or 10 sqrt2 - R - 0.5 (inside it) from the markers'.  Beyond 1.01 R0 (outer radii, R0 where
+// the term meets 1.1251 dtm R + 0.003) or within 0.99 R0 (the inner radius, R0 where 10 sqrt2 - R - 0.503
+// meets 1.1251 dtm R) that term exceeds the root-free test's threshold by >= 0.01 R0 (1 -+ 1.1251 dtm) > 0.001,
+// so it clears (the per-term lemma, sdf_term_slacks) without its argument being formed; r^2 is compared as
+// computed, as for sdf_far_r2.  Off: +inf (outer), -1 (inner).
+static void sdf_term_radii(float rs, float dtm, float* ps_r2, float* mo_r2, float* mi_r2) {
+    *ps_r2 = INFINITY; *mo_r2 = INFINITY; *mi_r2 = -1.0f;
+    if (!(rs > 0.0f) || !(dtm > 0.0f)) return;
+    const double k = 1.1251 * (double)dtm, out = 1.0 - k, m = 10.0 * std::sqrt(2.0);
+    if (out > 0.01) {
+        const double Rp = 1.01 * (1.5 * rs + 0.075 + 0.003) / out, Rm = 1.01 * (m + 0.5 + 0.003) / out;
+        *ps_r2 = std::nextafter((float)(Rp * Rp), INFINITY);
+        *mo_r2 = std::nextafter((float)(Rm * Rm), INFINITY);
+    }
+    const double Ri = 0.99 * (m - 0.5 - 0.003) / (1.0 + k);
+    *mi_r2 = std::nextafter((float)(Ri * Ri), 0.0f);
+}
+
 // A/B switch (diagnostics): BH_NO_SDF_SKIP set => every step evaluates its SDF roots (bh_march.hpp, sdf_skip)
 static bool sdf_skip_disabled() {
     static const bool off = std::getenv("BH_NO_SDF_SKIP") != nullptr;
@@ -1297,6 +1333,8 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     a.blackout_eh = U->blackout_eh;
     a.skip_sdf = (U->delta_time_mult > 0.0f && U->rs > 0.0f && U->rs <= 8.0f && !sdf_skip_disabled()) ? 1u : 0u;
     a.far_r2 = a.skip_sdf ? sdf_far_r2(U->rs, U->delta_time_mult) : INFINITY;
+    a.ps_r2 = INFINITY; a.mo_r2 = INFINITY; a.mi_r2 = -1.0f;
+    if (a.skip_sdf) sdf_term_radii(U->rs, U->delta_time_mult, &a.ps_r2, &a.mo_r2, &a.mi_r2);
     a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
     a.format = d->format; a.layout = d->layout;
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;
