@@ -2,7 +2,7 @@
 # round 5: validation of the current build -- the whole GPU suite, smoke, the driver's bench command, the
 # bloom sizes, 2- and 3-rank rehearsals
 set -u -o pipefail
-source tools/gpu/outdir.sh r05 n
+source tools/gpu/outdir.sh r05 ${TAG:-n}
 timeout -k 10 900 python -u -m pytest -q -m gpu --timeout 300 --timeout-method thread tests > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -1 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 1
