@@ -503,6 +503,11 @@ __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= B
 #ifndef BH_SDF_TERMS
 #define BH_SDF_TERMS 1  // the root-free test term by term on the wave-steps that fail it as a whole
 #endif
+#ifndef BH_SDF_TERMS3
+// A/B: the per-term ballots also decide the all-terms test (no min over the slacks): measured equal,
+// 0.5189 vs 0.5193 ms (profiles/r05/sdf_terms3/), so off
+#define BH_SDF_TERMS3 0
+#endif
 #ifndef BH_SDF_RADII
 // terms cleared by the lane's radius alone, their arguments not formed (A/B, off: both radii 0.5217 ->
 // 0.5261 ms, the photon sphere's alone 0.5217 -> 0.5217; profiles/r05/sdf_radii/)
@@ -674,10 +679,20 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         const bool test = !BH_SKIP_STICKY || !sk || *sk == 0u;
         bool fast = false;
         SdfSlack terms{0.0f, 0.0f, 0.0f};
+        bool nd = true, nm = true, np = true;  // BH_SDF_TERMS3: which roots some staying lane needs
         if (test) {
             terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps, m_on, ps_on);
-            const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
-            fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
+            if (BH_SDF_TERMS3 && BH_SDF_TERMS) {
+                // the three per-term ballots decide both: fast when no term is needed
+                const bool stay = !blackout;
+                nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
+                nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
+                np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
+                fast = a.skip_sdf != 0u && !(nd | nm | np);
+            } else {
+                const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
+                fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
+            }
         }
         if (BH_SKIP_STICKY && sk) *sk = (test && !fast) ? 1u : 0u;
         if (fast) {
@@ -691,10 +706,12 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
             // per term: a root only where some lane that stays needs it (sdf_term_slacks); where the disc
             // and markers both clear, the photon sphere alone keeps the wave here (about 98 % of these
             // wave-steps clear it, and 80 % one of the other two: tools/skip_sim.py)
-            const bool stay = !blackout;
-            const bool nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
-            const bool nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
-            const bool np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
+            if (!BH_SDF_TERMS3) {
+                const bool stay = !blackout;
+                nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
+                nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
+                np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
+            }
             float dv = __builtin_inff(), mv = __builtin_inff();
             if (nd) {
                 dv = X.disc_from(ro, a.rs, rho2);
