@@ -784,6 +784,20 @@ __device__ uint32_t g_bp_slot;
 __device__ uint32_t g_bp_rec[BP_SLOTS][BP_MAXW][8];
 __device__ uint32_t g_bp_hdr[BP_SLOTS][4];  // FP, EPI, grid blocks, output width
 #define BP_T(i) (bp[i] = (uint32_t)__builtin_amdgcn_s_memtime())
+// one wave's record (lanes 0..7) and, from wave 0, the launch's header; fp 0 marks a fix-up launch
+__device__ __forceinline__ void bp_record(const uint32_t (&bp)[5], uint32_t real0, uint32_t wave, uint32_t fp, uint32_t epi,
+                                          uint32_t blocks, uint32_t ow) {
+    const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
+    const uint32_t real_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    const uint32_t lane = threadIdx.x & 63u, slot = g_bp_slot % BP_SLOTS;
+    if (lane < 8u && wave < BP_MAXW) {
+        uint32_t v = fp;
+        v = lane == 0u ? real0 : lane == 1u ? real_end : lane == 6u ? t_end - bp[0] : v;
+        for (int i = 0; i < 4; ++i) v = lane == 2u + i ? bp[i + 1] - bp[i] : v;
+        g_bp_rec[slot][wave][lane] = v;
+    }
+    if (wave == 0u && lane < 4u) g_bp_hdr[slot][lane] = lane == 0u ? fp : lane == 1u ? epi : lane == 2u ? blocks : ow;
+}
 #else
 #define BP_T(i) do {} while (0)
 #endif
@@ -805,7 +819,9 @@ constexpr bool sepq_fix2_fits() {
 template <int FP, uint32_t EPI, bool RAW, int FS = sepq_stride<FP, RAW>(), bool FIX = false>
 __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry,
                                                       const SepEntry* __restrict__ sep, Tex out, CTex own0, CTex own1,
-                                                      const uint2* __restrict__ same, Tex aux, uint32_t org) {
+                                                      const uint2* __restrict__ same, Tex aux, uint32_t org,
+                                                      const uint32_t* __restrict__ stc, uint32_t* __restrict__ strips,
+                                                      uint32_t strip_w) {
     // FIX2: the final epilogue's fix (an instantiation whose tile cannot hold its words never takes it; the
     // host does not request it there, bh_bloom_sep_fix_ok)
     constexpr bool FIX1 = FIX && EPI == EPI_Y, FIX2 = FIX && EPI == EPI_FINAL && sepq_fix2_fits<FP, RAW, FS>();
@@ -1079,6 +1095,16 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             __builtin_amdgcn_sched_barrier(0);
         }
         BP_T(3);
+        // STRIPS (final epilogue, stc != null): the column strips of the fix-up pass -- each column within 2 of
+        // an inexact column (stc: 1 + its strip column, bh_bloom_strip_table) also stores its col, Y and U
+        // words column-major, (image * strip_w + strip column) * oh + row
+        uint32_t st[2] = {0u, 0u};
+        if constexpr (EPI == EPI_FINAL && !FIX2) {
+            if (stc) {
+                st[0] = stc[min(x0, ow - 1u)];
+                st[1] = stc[min(x0 + 1u, ow - 1u)];
+            }
+        }
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -1091,6 +1117,15 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 } else {
                     const uint32_t ue = enc(L, u);
                     aux.px[pix] = ue;
+                    if constexpr (EPI == EPI_FINAL && !FIX2) {
+                        if (st[c] != 0u) {
+                            const size_t img = (size_t)strip_w * oh;
+                            uint32_t* const p = strips + (size_t)(st[c] - 1u) * oh + (y0 + b);
+                            p[0] = o0[b][c];
+                            p[img] = o1[b][c];
+                            p[2u * img] = ue;
+                        }
+                    }
                     if constexpr (FIX1) ublk[2u * qy + b][2u * qx + c] = ue;
                     if constexpr (FIX2) bw[b][c] = ue;
                     if (exact[b][c]) {
@@ -1227,20 +1262,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
 #if BH_BLOOM_PHASES
 phases:
     BP_T(4);
-    {
-        const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
-        const uint32_t real_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
-        const uint32_t lane = threadIdx.x & 63u, slot = g_bp_slot % BP_SLOTS;
-        const uint32_t wave = (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (threadIdx.x >> 6);
-        if (lane < 8u && wave < BP_MAXW) {
-            uint32_t v = FP;
-            v = lane == 0u ? bp_real0 : lane == 1u ? real_end : lane == 6u ? t_end - bp[0] : v;
-            for (int i = 0; i < 4; ++i) v = lane == 2u + i ? bp[i + 1] - bp[i] : v;
-            g_bp_rec[slot][wave][lane] = v;
-        }
-        if (wave == 0u && lane < 4u)
-            g_bp_hdr[slot][lane] = lane == 0u ? FP : lane == 1u ? EPI : lane == 2u ? gridDim.x * gridDim.y : ow;
-    }
+    bp_record(bp, bp_real0, (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (threadIdx.x >> 6), FP, EPI, gridDim.x * gridDim.y, ow);
 #endif
 }
 
@@ -1355,6 +1377,22 @@ __device__ __forceinline__ SameWords gather_same(CTex t, uint2 cx, uint2 cy) {
     s.t[3] = ex && ey ? t.px[r1 + x1] : 0u;
     return s;
 }
+// The same gather from a texture (rs = row stride, cs = 1, xb = 0) or from a column strip of the fix-up
+// (rs = 1, cs = H, xb = the strip's first column; xm caps the column offset: 4 in a strip)
+struct SrcImg { const uint32_t* px; uint32_t rs, cs, xm; int32_t xb; };
+__device__ __forceinline__ SameWords gather_img(SrcImg t, uint2 cx, uint2 cy) {
+    auto at = [&](uint32_t x, uint32_t r) { return min((uint32_t)((int32_t)x - t.xb), t.xm) * t.cs + r * t.rs; };
+    const uint32_t x0 = cx.x & 0xFFFFu, x1 = cx.x >> 16, r0 = cy.x & 0xFFFFu, r1 = cy.x >> 16;
+    SameWords s;
+    s.fa = __uint_as_float(cx.y);
+    s.fb = __uint_as_float(cy.y);
+    const bool ex = s.fa != 0.0f, ey = s.fb != 0.0f;
+    s.t[0] = t.px[at(x0, r0)];
+    s.t[1] = ex ? t.px[at(x1, r0)] : 0u;
+    s.t[2] = ey ? t.px[at(x0, r1)] : 0u;
+    s.t[3] = ex && ey ? t.px[at(x1, r1)] : 0u;
+    return s;
+}
 __device__ __forceinline__ F4 finish_same(const Lds& L, const SameWords& s) {
     if (s.fa == 0.0f && s.fb == 0.0f) return dec(L, s.t[0]);
     const F4 a = dec(L, s.t[0]), b = dec(L, s.t[1]), c = dec(L, s.t[2]), d = dec(L, s.t[3]);
@@ -1370,15 +1408,28 @@ __device__ __forceinline__ F4 finish_same(const Lds& L, const SameWords& s) {
 // rec (the host's records of the list, fixup_records): per entry two uint4, the column (row) and the plan
 // entries of it and of its two neighbours (clamped), so the pixel's column and row entries and F's
 // neighbours arrive with the list entry -- one dependent round trip fewer than list, then plan.
+// strips (EPI_FINAL, the full list with records): a column lane (one row of an inexact column x) reads its
+// texels -- all in x's strip at their offset from x (strip_ok) -- from the strips the final up pass's epilogue
+// wrote, column-major (a wave's 64 rows: 256 contiguous bytes per strip column), instead of the three
+// row-major textures, where each lane's word is a cache line of its own.  The record's word 7 is 1 + x's strip
+// column.
 template <uint32_t EPI>
 __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CTex B, CTex C,
                                                            const uint2* __restrict__ plan,
                                                            const uint32_t* __restrict__ list, uint32_t n_cols,
-                                                           uint32_t n_rows, Tex out, const uint4* __restrict__ rec) {
+                                                           uint32_t n_rows, Tex out, const uint4* __restrict__ rec,
+                                                           const uint32_t* __restrict__ strips, uint32_t strip_w) {
     __shared__ Lds L;
+#if BH_BLOOM_PHASES
+    // phases: the list entry and plan entries used, the tables staged, the pixel computed and stored
+    uint32_t bp[5] = {};
+    const uint32_t bp_real0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+    const uint32_t bp_wave = blockIdx.x * 4u + (threadIdx.x >> 6);
+#endif
+    BP_T(0);
     const uint32_t W = out.w, H = out.h;
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x, nc = (uint64_t)n_cols * H;
-    uint32_t x = 0u, y = 0u;
+    uint32_t x = 0u, y = 0u, qx = 0u;  // qx: a column lane's strip column (strips)
     bool live = true;
     uint2 cx, cy, PX[3], PY[3];
     if (rec) {
@@ -1400,6 +1451,7 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         const uint2 e0 = make_uint2(r0.y, r0.z), e1 = make_uint2(r0.w, r1.x), e2 = make_uint2(r1.y, r1.z);
         if (col) {
             x = r0.x;
+            qx = r1.w - 1u;
             PX[0] = e0; PX[1] = e1; PX[2] = e2;
             const uint32_t yc = min(y, H - 1u);
             PY[1] = plan[W + yc];
@@ -1443,12 +1495,22 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         }
     }
     if (i >= nc && cx.y != 0u) live = false;  // an inexact column: its pixels are the first part's
-    const SameWords a = gather_same(A, cx, cy);
+#if BH_BLOOM_PHASES
+    asm volatile("" ::"v"(cx.x), "v"(cy.x));
+#endif
+    BP_T(1);
+    const bool sl = EPI == EPI_FINAL && strips != nullptr && rec != nullptr && i < nc;  // a column lane on strips
+    auto img = [&](CTex T, uint32_t im) -> SrcImg {
+        if (sl) return {strips + (size_t)im * strip_w * H, 1u, H, strip_w - 1u, (int32_t)x - (int32_t)qx};
+        return {T.px, W, 1u, 0xFFFFFFFFu, 0};
+    };
+    const SameWords a = EPI == EPI_FINAL ? gather_img(img(A, 0u), cx, cy) : gather_same(A, cx, cy);
     if constexpr (EPI == EPI_Y) {
         const SameWords b = gather_same(B, cx, cy);
         load_tables(tb, L);
-        if (!live) return;
-        out.px[y * W + x] = enc(L, remix(finish_same(L, a), finish_same(L, b)));
+        BP_T(2);
+        BP_T(3);
+        if (live) out.px[y * W + x] = enc(L, remix(finish_same(L, a), finish_same(L, b)));
     } else {
         auto pick = [&](uint32_t u, uint32_t c, const uint2(&P)[3], uint32_t base) -> uint2 {
             if (u == c) return P[1];
@@ -1462,29 +1524,41 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         const uint2 py0 = pick(cy.x & 0xFFFFu, y, PY, W), py1 = pick(cy.x >> 16, y, PY, W);
         // F at the (up to 4) texels of final_in1 the lerp weighs (remix2_plan_kernel)
         SameWords fbw[4] = {}, fcw[4] = {};
-        fbw[0] = gather_same(B, px0, py0);
-        fcw[0] = gather_same(C, px0, py0);
+        const SrcImg IB = img(B, 1u), IC = img(C, 2u);
+        fbw[0] = gather_img(IB, px0, py0);
+        fcw[0] = gather_img(IC, px0, py0);
         if (ex) {
-            fbw[1] = gather_same(B, px1, py0);
-            fcw[1] = gather_same(C, px1, py0);
+            fbw[1] = gather_img(IB, px1, py0);
+            fcw[1] = gather_img(IC, px1, py0);
         }
         if (ey) {
-            fbw[2] = gather_same(B, px0, py1);
-            fcw[2] = gather_same(C, px0, py1);
+            fbw[2] = gather_img(IB, px0, py1);
+            fcw[2] = gather_img(IC, px0, py1);
         }
         if (ex && ey) {
-            fbw[3] = gather_same(B, px1, py1);
-            fcw[3] = gather_same(C, px1, py1);
+            fbw[3] = gather_img(IB, px1, py1);
+            fcw[3] = gather_img(IC, px1, py1);
         }
         load_tables(tb, L);
-        if (!live) return;
-        auto F = [&](int k) { return quant(L, remix(finish_same(L, fbw[k]), finish_same(L, fcw[k]))); };
-        const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
-        const F4 f0 = F(0), f1 = ex ? F(1) : z, f2 = ey ? F(2) : z, f3 = ex && ey ? F(3) : z;
-        const F4 f = lerp_plan(make_float4(f0.r, f0.g, f0.b, f0.a), make_float4(f1.r, f1.g, f1.b, f1.a),
-                               make_float4(f2.r, f2.g, f2.b, f2.a), make_float4(f3.r, f3.g, f3.b, f3.a), fa, fb);
-        out.px[y * W + x] = enc(L, remix(finish_same(L, a), f));
+        BP_T(2);
+        if (live) {
+#if BH_BLOOM_PHASES
+            // the texel words arrived (their first use)
+            asm volatile("" ::"v"(a.t[0]), "v"(fbw[0].t[0]), "v"(fcw[0].t[0]));
+#endif
+            BP_T(3);
+            auto F = [&](int k) { return quant(L, remix(finish_same(L, fbw[k]), finish_same(L, fcw[k]))); };
+            const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
+            const F4 f0 = F(0), f1 = ex ? F(1) : z, f2 = ey ? F(2) : z, f3 = ex && ey ? F(3) : z;
+            const F4 f = lerp_plan(make_float4(f0.r, f0.g, f0.b, f0.a), make_float4(f1.r, f1.g, f1.b, f1.a),
+                                   make_float4(f2.r, f2.g, f2.b, f2.a), make_float4(f3.r, f3.g, f3.b, f3.a), fa, fb);
+            out.px[y * W + x] = enc(L, remix(finish_same(L, a), f));
+        }
     }
+#if BH_BLOOM_PHASES
+    BP_T(4);
+    bp_record(bp, bp_real0, bp_wave, 0u, EPI, gridDim.x, W);
+#endif
 }
 
 template <uint32_t EPI>
@@ -2577,7 +2651,65 @@ bool records_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* li
     }
     return true;
 }
+// The inexact columns of a same-size plan (its list's column count)
+uint32_t n_inexact(uint32_t w, const uint32_t* plan) {
+    uint32_t n = 0;
+    for (uint32_t x = 0; x < w; ++x) n += plan[2u * x + 1u] != 0u;
+    return n;
+}
+// The column records' word 7: 1 + the column's strip column (fixup_gather_kernel's qx)
+bool strip_records_ok(const uint32_t* list, uint32_t nc, const uint32_t* stc, const uint32_t* rec) {
+    for (uint32_t k = 0; k < nc; ++k)
+        if (!chk(rec[8u * k + 7u] == stc[list[k]], "fix-up record %u: strip column %u, table %u", k, rec[8u * k + 7u], stc[list[k]]))
+            return false;
+    return true;
+}
+// The fix-up's column strips (bh_bloom_strip_table, up_sepq_kernel's STRIPS epilogue, fixup_gather_kernel):
+// stc[c] is 0 or 1 + column c's strip column, distinct and below tw, so each strip word has one writer; and
+// every texel a column lane of inexact column x reads (its own sample and F's at the sample's texels) lies in
+// x's strip at the same offset: stc[c] - stc[x] == c - x.
+bool strip_ok(uint32_t w, uint32_t h, const uint32_t* plan, const uint32_t* list, uint32_t nc, const uint32_t* stc,
+              uint32_t tw) {
+    if (!chk(tw > 0u && tw <= w && nc <= w, "strips: %u strip columns, %u inexact columns of %u", tw, nc, w)) return false;
+    std::vector<uint8_t> seen(tw, 0u);
+    for (uint32_t c = 0; c < w; ++c) {
+        if (stc[c] == 0u) continue;
+        const uint32_t q = stc[c] - 1u;
+        if (!chk(q < tw && !seen[q], "strip table: column %u -> strip column %u of %u", c, q, tw)) return false;
+        seen[q] = 1u;
+    }
+    for (uint32_t k = 0; k < nc; ++k) {
+        const uint32_t x = list[k];
+        if (!chk(x < w && stc[x] != 0u, "strips: inexact column %u outside every strip", x)) return false;
+        auto same_strip = [&](uint32_t c) { return c < w && stc[c] != 0u && (int64_t)stc[c] - stc[x] == (int64_t)c - x; };
+        const uint32_t e = plan[2u * x], ex = plan[2u * x + 1u];
+        const uint32_t px[2] = {e & 0xFFFFu, e >> 16};
+        for (int t = 0; t < (ex != 0u ? 2 : 1); ++t) {
+            const uint32_t ep = plan[2u * px[t]], wp = plan[2u * px[t] + 1u];
+            if (!chk(same_strip(px[t]) && same_strip(ep & 0xFFFFu) && (wp == 0u || same_strip(ep >> 16)),
+                     "strips: column %u reads texel %u (samples %u, %u) outside its strip", x, px[t], ep & 0xFFFFu, ep >> 16))
+                return false;
+        }
+    }
+    (void)h;
+    return true;
+}
 }  // namespace
+
+// The strip table of a same-size plan's nc inexact columns (list, ascending): the columns within 2 of an
+// inexact column, merged into contiguous runs (inexact columns cluster), numbered left to right: stc[c] = 1 +
+// c's strip column, 0 outside.  Returns the number of strip columns (0: no inexact column).
+extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_strip_table(uint32_t w, const uint32_t* list, uint32_t nc,
+                                                                             uint32_t* stc) {
+    std::fill(stc, stc + w, 0u);
+    uint32_t tw = 0;
+    for (uint32_t k = 0; k < nc; ++k) {
+        const int64_t lo = std::max<int64_t>((int64_t)list[k] - 2, 0), hi = std::min<int64_t>((int64_t)list[k] + 2, (int64_t)w - 1);
+        for (int64_t c = lo; c <= hi; ++c)
+            if (stc[c] == 0u) stc[c] = ++tw;
+    }
+    return tw;
+}
 
 // The fix-up records of a list of n_cols columns then n_rows rows into out (8 words per entry, see
 // fixup_gather_kernel).
@@ -2807,21 +2939,31 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
                                                                         uint32_t ow, uint32_t oh, uint32_t org, bool fix,
+                                                                        const uint32_t* stc, uint32_t* strips,
+                                                                        uint32_t strip_w, bool* strips_written,
                                                                         hipStream_t s) {
+    if (strips_written) *strips_written = false;
     const SepForm f = sep_form(ext, ow, oh);
     if (f.FP == 0 || !sep) return (int)hipErrorInvalidValue;
     // the grid origin and the in-block fix are the quad kernel's (the fix with the Y or final epilogue)
     if (!f.quad) org = 0u;
     fix = fix && sep_fix_form(f, epi);
+    // the fix-up's column strips: the quad kernel's final epilogue without its in-block fix
+    const bool st = stc && f.quad && epi == EPI_FINAL && !fix && same;
     if (g_dry) {  // the plan is a host copy: check the form's every read instead of launching
         char form[32];
         std::snprintf(form, sizeof form, "%s%d%s/%u%s", f.quad ? "sepq" : "sep", f.FP, f.raw ? "r" : "", epi, fix ? "f" : "");
         note_launch(form, ow, oh, aw, ah, rx, ry);
+        if (st && !strip_ok(ow, oh, same, same + 2u * ((size_t)ow + oh), n_inexact(ow, same), stc, strip_w))
+            return (int)hipErrorInvalidValue;
+        if (strips_written) *strips_written = st;
         return bh_bloom_sep_verify(ow, oh, aw, ah, rx, ry, sep, ext, org, fix, nullptr) &&
                        (epi == EPI_PLAIN || chk(same != nullptr, "separable epilogue without a same-size plan"))
                    ? 0
                    : (int)hipErrorInvalidValue;
     }
+    if (st && !strips) return (int)hipErrorInvalidValue;
+    const uint32_t* const STC = st ? stc : nullptr;
     const Tables tb{lut, enc, buckets, codes};
     const CTex A{a, aw, ah}, O0{own0 ? own0 : a, ow, oh}, O1{own1 ? own1 : a, ow, oh};
     const SepEntry* P = reinterpret_cast<const SepEntry*>(sep);
@@ -2840,7 +2982,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
         BH_BP_SLOT();                                                                                                \
         hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS, FX>), gq, dim3(256),                                      \
                            sepq_cap_pad(reinterpret_cast<const void*>(&up_sepq_kernel<FP, E, RAW, FS, FX>), E), s, tb, A, \
-                           rx, ry, P, O, O0, O1, S, X, org);                                                         \
+                           rx, ry, P, O, O0, O1, S, X, org, STC, strips, strip_w);                                   \
     } while (0)
 #define BH_EPI(LAUNCH, ...)                                                    \
     do {                                                                       \
@@ -2870,7 +3012,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
 #undef BH_EPI
 #undef BH_SEPQ
 #undef BH_SEP
-    return (int)hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (strips_written) *strips_written = st && e == hipSuccess;
+    return (int)e;
 }
 
 // The fix-up pass of a fused epilogue (fixup_kernel): `list` = n_cols columns then n_rows rows
@@ -2881,8 +3025,12 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
                                                                           uint32_t h, int32_t residual_org, const uint32_t* recs,
-                                                                          hipStream_t s) {
+                                                                          const uint32_t* stc, const uint32_t* strips,
+                                                                          uint32_t strip_w, hipStream_t s) {
     if (n_cols > w || n_rows > h || !list || !same) return (int)hipErrorInvalidValue;  // the list of this frame's plan
+    // the column strips (the full list of the final epilogue, with its records; stc: the table they were written by)
+    static const bool no_rec = std::getenv("BH_BLOOM_FIXUP_NOREC") != nullptr;  // A/B: list, then plan
+    const bool st = stc && recs && !no_rec && epi == EPI_FINAL && residual_org < 0;
     const uint64_t n = (uint64_t)n_cols * h + (uint64_t)n_rows * w;
     if (g_dry) {
         // residual_org < 0: the list of every inexact column and row, right after the plan; else the residual
@@ -2894,21 +3042,37 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                   chk(list == same + 2u * ((size_t)w + h), "fix-up list is not its plan's")
                             : same_ok(w, h, same, nullptr, 0u, 0u, false) &&
                                   residual_ok(w, h, same, list, n_cols, n_rows, (uint32_t)residual_org, epi == EPI_FINAL);
-        return ok && (!recs || records_ok(w, h, same, list, n_cols, n_rows, recs)) ? 0 : (int)hipErrorInvalidValue;
+        return ok && (!recs || records_ok(w, h, same, list, n_cols, n_rows, recs)) &&
+                       (!st || (strip_ok(w, h, same, list, n_cols, stc, strip_w) && strip_records_ok(list, n_cols, stc, recs)))
+                   ? 0
+                   : (int)hipErrorInvalidValue;
     }
+    if (st && !strips) return (int)hipErrorInvalidValue;
+    const uint32_t* const SP = st ? strips : nullptr;
     if (n == 0) return 0;
     const Tables tb{lut, enc, buckets, codes};
-    const dim3 g((uint32_t)((n + 255u) / 256u));
+    const dim3 g0((uint32_t)((n + 255u) / 256u));
     const uint2* S = reinterpret_cast<const uint2*>(same);
     static const bool per_sample = !BH_BLOOM_FIXUP_GATHER || std::getenv("BH_BLOOM_FIXUP_SAMPLE") != nullptr;  // A/B
-    static const bool no_rec = std::getenv("BH_BLOOM_FIXUP_NOREC") != nullptr;  // A/B: list, then plan
     const uint4* R = no_rec ? nullptr : reinterpret_cast<const uint4*>(recs);
+#if BH_BLOOM_PHASES
+    if (!per_sample) bp_next_slot(s);
+    // timing only (wrong pixels): the fix-up's row part alone, or its column part alone
+    static const int part = std::getenv("BH_BLOOM_PHASES_FIXUP_PART") ? std::atoi(std::getenv("BH_BLOOM_PHASES_FIXUP_PART")) : 0;
+    if (part == 1) n_cols = 0u;
+    if (part == 2) n_rows = 0u;
+    const dim3 gp((uint32_t)(((uint64_t)n_cols * h + (uint64_t)n_rows * w + 255u) / 256u));
+    if (part != 0 && gp.x == 0u) return 0;
+    const dim3 g = part ? gp : g0;
+#else
+    const dim3 g = g0;
+#endif
     if (!per_sample && epi == EPI_Y)
         hipLaunchKernelGGL(fixup_gather_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
-                           CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R);
+                           CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R, nullptr, 0u);
     else if (!per_sample)
         hipLaunchKernelGGL(fixup_gather_kernel<EPI_FINAL>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
-                           CTex{c, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R);
+                           CTex{c, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R, SP, strip_w);
     else if (epi == EPI_Y)
         hipLaunchKernelGGL(fixup_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h}, CTex{b, w, h}, S, list,
                            n_cols, n_rows, Tex{out, w, h});
@@ -3042,7 +3206,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     }
     if (shader == SH_UP && !P.valid && sep && sep_form(sep_ext, ow, oh).FP != 0 && !g_no_sep) {
         return bh_launch_bloom_sep(lut, enc, buckets, codes, a, aw, ah, rx, ry, sep, sep_ext, EPI_PLAIN, nullptr, nullptr,
-                                   nullptr, out, nullptr, ow, oh, 0u, false, s);
+                                   nullptr, out, nullptr, ow, oh, 0u, false, nullptr, nullptr, 0u, nullptr, s);
     }
     if (g_dry) {  // pass_kernel: an up pass stages through with_source<FP_UP>; the others read clamped indices
         note_launch(shader == SH_UP ? (P.valid ? "pass_up_tap" : "pass_up") : shader == SH_COPY ? "pass_copy"

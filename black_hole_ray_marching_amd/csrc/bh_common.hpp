@@ -257,7 +257,10 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
                                                                         const uint32_t* own0, const uint32_t* own1,
                                                                         const uint32_t* same, uint32_t* out, uint32_t* aux,
                                                                         uint32_t ow, uint32_t oh, uint32_t org, bool fix,
+                                                                        const uint32_t* stc, uint32_t* strips,
+                                                                        uint32_t strip_w, bool* strips_written,
                                                                         hipStream_t s);
+// the fix-up pass of a fused epilogue; stc / strips: the final epilogue's column strips (the up pass wrote them)
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const float* lut, const float* enc,
                                                                           const uint8_t* buckets, const uint32_t* codes,
                                                                           uint32_t epi, const uint32_t* a, const uint32_t* b,
@@ -265,7 +268,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
                                                                           const uint32_t* list, uint32_t n_cols,
                                                                           uint32_t n_rows, uint32_t* out, uint32_t w,
                                                                           uint32_t h, int32_t residual_org, const uint32_t* recs,
-                                                                          hipStream_t s);
+                                                                          const uint32_t* stc, const uint32_t* strips,
+                                                                          uint32_t strip_w, hipStream_t s);
+// the column strips' table of a same-size plan's inexact columns; returns the number of strip columns
+extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_strip_table(uint32_t w, const uint32_t* list, uint32_t nc,
+                                                                         uint32_t* stc);
 // the fix-up kernel's records of a list (8 words per entry: the index and the plan entries of it and its neighbours)
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_fixup_records(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                            const uint32_t* list, uint32_t nc, uint32_t nr,

@@ -84,6 +84,11 @@ struct bh_ctx {
         // listed after the full list
         uint32_t org = 0, nrc = 0, nrr = 0, nrc2 = 0, nrr2 = 0;  // residual lists of the Y / final epilogue
         size_t rec = 0;  // word offset of the lists' fix-up records (full, residual 1, residual 2; 8 words each)
+        // the final epilogue's column strips (bh_bloom_strip_table): word offset of the table (0: none), its
+        // strip columns and the strip storage (3 images x stw columns x oh rows; not allocated in dry mode)
+        size_t stc = 0;
+        uint32_t stw = 0;
+        uint32_t* strips = nullptr;
         std::shared_ptr<std::vector<uint32_t>> host;
     };
     struct BloomScratch {
@@ -116,7 +121,10 @@ static void free_frame_table(bh_ctx::FrameTable& t);
 static void free_bloom_scratch(bh_ctx::BloomScratch& b) {
     for (uint32_t* t : b.tex) (void)hipFree(t);
     for (auto& p : b.sep_plans)
-        if (!p.host) (void)hipFree(p.dev);
+        if (!p.host) {
+            (void)hipFree(p.dev);
+            (void)hipFree(p.strips);
+        }
     b.tex.clear();
     b.sep_plans.clear();
 }
@@ -699,6 +707,8 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 // kernel -- with `dry_fail` (bh_bloom_check) a failed check is reported there instead.  In dry mode the
 // plan stays on the host (dev points into `host`).  A capturing call never builds one (bh_bloom refuses a
 // set not prepared outside capture).
+// The column strips' storage limit per plan (3 words per strip column and row: 1.3 MB at 1920 x 1080)
+constexpr size_t BH_STRIPS_BUDGET = (size_t)64 << 20;
 // Returned by value: the cache is a vector that later plans reallocate.  (Round 4's memory-access fault:
 // a pointer into it, held across the next call, read a freed record's fix-up counts)
 bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* dry_fail, uint32_t ow, uint32_t oh,
@@ -753,6 +763,21 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
                 bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc, P.nrr, R);
                 L += P.nrc + P.nrr; R += 8u * (P.nrc + P.nrr);
                 bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc2, P.nrr2, R);
+                // the column strips of the final fix-up (BH_BLOOM_NO_STRIPS: off, A/B), within a storage budget
+                static const bool no_strips = std::getenv("BH_BLOOM_NO_STRIPS") != nullptr;
+                if (!no_strips && P.nc > 0u) {
+                    const size_t at = h->size();
+                    h->resize(at + ow, 0u);
+                    const uint32_t stw = bh_bloom_strip_table(ow, h->data() + lists, P.nc, h->data() + at);
+                    if (stw > 0u && 3u * (size_t)stw * oh * 4u <= BH_STRIPS_BUDGET) {
+                        P.stc = at;
+                        P.stw = stw;
+                        // word 7 of each column record: 1 + the column's strip column
+                        for (uint32_t k = 0; k < P.nc; ++k) (*h)[P.rec + 8u * k + 7u] = (*h)[at + (*h)[lists + k]];
+                    } else {
+                        h->resize(at);
+                    }
+                }
             }
         }
     }
@@ -771,8 +796,10 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
     } else {
         hipError_t e = hipMalloc(&P.dev, h->size() * sizeof(uint32_t));
         if (e == hipSuccess) e = hipMemcpy(P.dev, h->data(), h->size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        if (e == hipSuccess && P.stc) e = hipMalloc(&P.strips, 3u * (size_t)P.stw * oh * 4u);
         if (e != hipSuccess) {
             if (P.dev) (void)hipFree(P.dev);
+            if (P.strips) (void)hipFree(P.strips);
             *err = (int)e;
             bh_ctx::SepPlan none;
             none.key = key;
@@ -892,8 +919,12 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
             if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
                 sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err, org, fix);
             if (R.err != 0) return;
+            // the final epilogue writes the column strips its fix-up reads (bh_bloom.hip STRIPS)
+            const uint32_t* stc = epi == 2u && same.stc ? plan + same.stc : nullptr;
+            bool strips = false;
             if (sp.dev && bh_launch_bloom_sep(c->lut, c->enc, c->enc_b, c->enc_e, src, sw, sh, res[0], res[1], sp.dev,
-                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, org, fix, s) == 0) {
+                                              sp.ext, epi, own0, own1, plan, dst, aux, W, H, org, fix, stc, same.strips,
+                                              same.stw, &strips, s) == 0) {
                 const bool fixed = fix && bh_bloom_sep_fix_ok(sp.ext, W, H, epi);
                 const uint32_t* rl = epi == 1u ? residual : residual2;
                 const uint32_t rc = epi == 1u ? same.nrc : same.nrc2, rr = epi == 1u ? same.nrr : same.nrr2;
@@ -902,7 +933,8 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
                 const uint32_t* recs = same.rec ? plan + same.rec + 8u * rk : nullptr;
                 R.err = bh_launch_bloom_fixup(c->lut, c->enc, c->enc_b, c->enc_e, epi, own0, epi == 1u ? aux : own1, aux,
                                               plan, fixed ? rl : list, fixed ? rc : same.nc, fixed ? rr : same.nr, dst, W, H,
-                                              fixed ? (int32_t)same.org : -1, recs, s);
+                                              fixed ? (int32_t)same.org : -1, recs, strips && !fixed ? stc : nullptr,
+                                              same.strips, same.stw, s);
                 return;
             }
             R.pass(bh_bloom_shader_up, src, sw, sh, nullptr, res, aux, W, H);

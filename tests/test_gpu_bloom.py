@@ -134,12 +134,15 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
 BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
 
 
-@pytest.mark.parametrize("env", [{"BH_BLOOM_FIX2": "1"}, {"BH_BLOOM_NO_FIX": "1"}, {"BH_BLOOM_ORG_KEEP": "1"}],
-                         ids=["fix2", "no_fix", "org_keep"])
+@pytest.mark.parametrize("env", [{"BH_BLOOM_FIX2": "1"}, {"BH_BLOOM_NO_FIX": "1"}, {"BH_BLOOM_ORG_KEEP": "1"},
+                                 {"BH_BLOOM_NO_STRIPS": "1"}, {"BH_BLOOM_FIXUP_NOREC": "1"}],
+                         ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec"])
 def test_bloom_switches_stay_bitexact(torch_cuda, env):
     """The chain's A/B switches, which the library reads once per process, in a child process each: the final
-    epilogue's in-block fix (off by default), no in-block fix, and grid origins that keep the block count
-    (1920: a residual column) -- display sizes with opaque and with any alpha, a residual list (1366)."""
+    epilogue's in-block fix (off by default), no in-block fix, grid origins that keep the block count (1920: a
+    residual column), the final fix-up from the row-major textures instead of its column strips, and the fix-up
+    without its records (which also drops the strips) -- display sizes with opaque and with any alpha, a
+    residual list (1366)."""
     import os
     import subprocess
     import sys
