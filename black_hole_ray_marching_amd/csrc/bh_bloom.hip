@@ -812,6 +812,13 @@ __device__ __forceinline__ void bp_record(const uint32_t (&bp)[5], uint32_t real
 // -- B from the block's words, Y and col from the block's own words, all through LDS.  Its three barriers
 // come after the taps, so the dead tile holds the B, Y and F words and the dead plan entries the col words.
 constexpr uint32_t FIX_WORDS = 32u * 33u;  // one padded 32 x 32 array of words
+// BH_BLOOM_OWN_LATE: the epilogue's own texels are loaded after the tile is staged, so that the launch's first
+// waves load only their footprints (its opening burst is HBM-bound) and the own texels arrive during the taps;
+// the block's opaque test then covers the footprint only, and the epilogue decodes the own texels' alpha unless
+// its wave's own texels are all opaque too (A/B: 0 loads them with the footprint)
+#ifndef BH_BLOOM_OWN_LATE
+#define BH_BLOOM_OWN_LATE 1
+#endif
 template <int FP, bool RAW, int FS>
 constexpr bool sepq_fix2_fits() {
     return sizeof(std::conditional_t<RAW, uint32_t, float4>) * (FP * FS + FP / 2) >= 3u * FIX_WORDS * 4u;
@@ -825,6 +832,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     // FIX2: the final epilogue's fix (an instantiation whose tile cannot hold its words never takes it; the
     // host does not request it there, bh_bloom_sep_fix_ok)
     constexpr bool FIX1 = FIX && EPI == EPI_Y, FIX2 = FIX && EPI == EPI_FINAL && sepq_fix2_fits<FP, RAW, FS>();
+    constexpr bool LATE = BH_BLOOM_OWN_LATE && EPI != EPI_PLAIN && !FIX2;
     using TileT = std::conditional_t<RAW, uint32_t, float4>;
     __shared__ Lds L;
     __shared__ __attribute__((aligned(16))) unsigned char tile_mem[sizeof(TileT) * (FP * FS + FP / 2)];
@@ -887,7 +895,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         if (threadIdx.x < 32u) sce[threadIdx.x] = same[clampi((int32_t)(bx + threadIdx.x), 0, (int32_t)ow - 1)];
         else if (threadIdx.x < 64u) sre[threadIdx.x - 32u] = same[ow + clampi((int32_t)(by + threadIdx.x - 32u), 0, (int32_t)oh - 1)];
     }
-    // own texels of the epilogue (four pixels), loaded before the tables, used last
+    // own texels of the epilogue (four pixels), loaded before the tables (LATE: after the staging), used last
     uint32_t o0[2][2], o1[2][2];
     bool in[2][2], exact[2][2];
     uint2 scx[2] = {}, scy[2] = {};  // same-size plan entries of the quad's columns and rows (FIX1)
@@ -902,8 +910,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             o0[b][c] = o1[b][c] = 0xFF000000u;
             exact[b][c] = false;
             if constexpr (EPI != EPI_PLAIN) {
-                o0[b][c] = own0.px[pix];
-                if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
+                if constexpr (!LATE) {
+                    o0[b][c] = own0.px[pix];
+                    if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
+                }
                 if constexpr (FIX2) {
                     // exact[] after the staging barrier, from sce / sre
                 } else if constexpr (FIX1) {
@@ -937,6 +947,17 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         for (int b = 0; b < 2; ++b)
 #pragma unroll
             for (int c = 0; c < 2; ++c) exact[b][c] = in[b][c] && sce[2u * qx + c].y == 0u && sre[2u * qy + b].y == 0u;
+    }
+    if constexpr (LATE) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t pix = (in[b][c] ? y0 + b : 0u) * ow + (in[b][c] ? x0 + c : 0u);
+                o0[b][c] = own0.px[pix];
+                if constexpr (EPI == EPI_FINAL) o1[b][c] = own1.px[pix];
+            }
+        __builtin_amdgcn_sched_barrier(0);  // issued here, awaited in the epilogue
     }
     BP_T(2);
 #if BH_BLOOM_PHASES
@@ -1105,6 +1126,18 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 st[1] = stc[min(x0 + 1u, ow - 1u)];
             }
         }
+        // LATE: the own texels were not in the block's opaque test; AO: the wave's are opaque as well
+        bool own_op = true;
+        if constexpr (LATE && A1) {
+            uint32_t mo = 0xFFFFFFFFu;
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) mo = min(mo, min(o0[b][c], o1[b][c]));
+            own_op = __builtin_amdgcn_ballot_w64(mo < 0xFF000000u) == 0ull;
+        }
+        auto epilogue = [&](auto AOc) {
+        constexpr bool AO = decltype(AOc)::value;
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -1129,18 +1162,21 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                     if constexpr (FIX1) ublk[2u * qy + b][2u * qx + c] = ue;
                     if constexpr (FIX2) bw[b][c] = ue;
                     if (exact[b][c]) {
-                        const F4 uq = dec<A1>(L, ue);
+                        const F4 uq = dec<AO>(L, ue);
                         if constexpr (EPI == EPI_Y) {
-                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), uq));
+                            out.px[pix] = enc(L, remix(dec<AO>(L, o0[b][c]), uq));
                         } else {
                             // z = q(Y + 0.5 B): F at this exact pixel, kept as its word for FIX2
-                            const uint32_t zq = enc(L, remix(dec<A1>(L, o1[b][c]), uq));
+                            const uint32_t zq = enc(L, remix(dec<AO>(L, o1[b][c]), uq));
                             if constexpr (FIX2) fw[b][c] = zq;
-                            out.px[pix] = enc(L, remix(dec<A1>(L, o0[b][c]), dec<A1>(L, zq)));
+                            out.px[pix] = enc(L, remix(dec<AO>(L, o0[b][c]), dec<AO>(L, zq)));
                         }
                     }
                 }
             }
+        };
+        if (A1 && own_op) epilogue(std::bool_constant<A1>{});
+        else epilogue(std::false_type{});
         }  // live
         if constexpr (FIX2) {
             // the taps of every wave are done: the tile and the plan entries are dead
