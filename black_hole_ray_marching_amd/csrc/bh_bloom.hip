@@ -1924,9 +1924,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
     const uint32_t x = xcd_block().x * 16u + (threadIdx.x & 15u), y = xcd_block().y * 16u + (threadIdx.x >> 4);
     const crm::Rcp Rw = crm::rcp_refined((float)out.w), Rh = crm::rcp_refined((float)out.h);
     const Taps k(rx, ry);
-    // the pixel's own Y and col texels: loaded before the footprint and the tables, used last
     const bool in = x < out.w && y < out.h;
     const uint32_t i = (uint32_t)y * out.w + x;
+#if BH_BLOOM_OWN_LATE
+    // the pixel's own Y and col texels: loaded after the footprint is staged (see up_sepq_kernel's LATE), in
+    // flight during the taps; the block's opaque test covers the footprint, the wave's own texels pick the
+    // last stage's form
+    with_source<FP_FINAL, true, STD>(
+        tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P,
+        [&](const auto& src) {
+            constexpr bool A1 = std::decay_t<decltype(src)>::kA1;
+            const uint32_t yv = in ? Y.px[i] : 0xFF000000u, cv = in ? col.px[i] : 0xFF000000u;
+            __builtin_amdgcn_sched_barrier(0);
+            if (!in) return;
+            const F4 b3 = quant<A1>(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
+            bool own_op = true;
+            if constexpr (A1) own_op = __builtin_amdgcn_ballot_w64(min(yv, cv) < 0xFF000000u) == 0ull;
+            auto fin = [&](auto AOc) {
+                constexpr bool AO = decltype(AOc)::value;
+                const F4 z = quant<AO>(L, remix(dec<AO>(L, yv), b3));
+                out.px[i] = enc(L, remix(dec<AO>(L, cv), z));
+            };
+            if (A1 && own_op) fin(std::bool_constant<A1>{});
+            else fin(std::false_type{});
+        },
+        true);
+#else
+    // the pixel's own Y and col texels: loaded before the footprint and the tables, used last
     const uint32_t yv = in ? Y.px[i] : 0u, cv = in ? col.px[i] : 0u;
     with_source<FP_FINAL, true, STD>(
         tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P,
@@ -1938,6 +1962,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
             out.px[i] = enc(L, remix(dec<A1>(L, cv), z));
         },
         !in || (min(yv, cv) >= 0xFF000000u));
+#endif
 }
 
 // ---- persistent blocks (standard plans) ------------------------------------------------------------
