@@ -1,10 +1,10 @@
 """Post-processing chain (bh_bloom) on one GPU: time per frame of the Kawase
 bloom + remix over a 4096x2048 BGRA8 frame (the march kernel's own two targets), HIP events on the
 stream, fused (AUTO) and literal schedules.  `roofline` (tools/bloom_roofline.py): the chain's
-reference arithmetic in flop-equivalents against the FP32 VALU peak, its algorithmic bytes (read col +
-blackout, write the surface: 12 B/pixel) against HBM, and -- when a committed rocprofv3 PMC summary of this
-frame size exists (profiles/r05/bloom_roof/roofline<W>.json) -- the hardware's VALU-issue, LDS and HBM busy
-fractions, time-weighted over the fused chain's kernels.
+algorithmic bytes (read col + blackout, write the surface: 12 B/pixel) against HBM, the reference's arithmetic
+in flop-equivalents as a rate against the FP32 VALU peak (an op count, not executed instructions), and -- when
+a committed rocprofv3 PMC summary of this frame size exists (profiles/r05/bloom_roof/roofline<W>.json) -- the
+hardware's executed VALU-issue, LDS and HBM busy fractions, time-weighted over the fused chain's kernels.
     python tools/bench_bloom.py [--width 4096 --height 2048 --levels 3 --steps 100]"""
 import argparse
 import json
