@@ -819,6 +819,13 @@ constexpr uint32_t FIX_WORDS = 32u * 33u;  // one padded 32 x 32 array of words
 #ifndef BH_BLOOM_OWN_LATE
 #define BH_BLOOM_OWN_LATE 1
 #endif
+// BH_BLOOM_ROWLOAD: the footprint staged row by row -- wave w loads tile rows w, w + 4, ... (two rows per
+// wave-instruction when FP <= 32), lane = column -- so each load's address is one 24-bit multiply-add off a
+// per-lane column and a per-round row, and an out-of-footprint lane stores into a spare tile slot instead of
+// branching; the linear form (A/B: 0) divides its element index by the footprint width for every load
+#ifndef BH_BLOOM_ROWLOAD
+#define BH_BLOOM_ROWLOAD 1
+#endif
 template <int FP, bool RAW, int FS>
 constexpr bool sepq_fix2_fits() {
     return sizeof(std::conditional_t<RAW, uint32_t, float4>) * (FP * FS + FP / 2) >= 3u * FIX_WORDS * 4u;
@@ -835,7 +842,8 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     constexpr bool LATE = BH_BLOOM_OWN_LATE && EPI != EPI_PLAIN && !FIX2;
     using TileT = std::conditional_t<RAW, uint32_t, float4>;
     __shared__ Lds L;
-    __shared__ __attribute__((aligned(16))) unsigned char tile_mem[sizeof(TileT) * (FP * FS + FP / 2)];
+    // + 1: the spare slot of BH_BLOOM_ROWLOAD's out-of-footprint lanes
+    __shared__ __attribute__((aligned(16))) unsigned char tile_mem[sizeof(TileT) * (FP * FS + FP / 2 + 1)];
     TileT* const tile = reinterpret_cast<TileT*>(tile_mem);
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
     // the lanes instead of every second one (2-way bank conflicts)
@@ -869,15 +877,29 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     const int32_t lo_y = (int32_t)floorf(sample_coord(texcoord(byf, Rh) + k.dv_min(), a.h));
     const int32_t hi_y = (int32_t)floorf(sample_coord(texcoord(yl, Rh) + k.dv_max(), a.h));
     const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // the host sizes FP: no cut
+    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
+#if BH_BLOOM_ROWLOAD
+    constexpr int RPI = FP > 32 ? 1 : 2, R = (FP + 4 * RPI - 1) / (4 * RPI);  // rows per wave-instruction, rounds
+    const int32_t ln = (int32_t)(threadIdx.x & 63u);
+    const int32_t rlx = RPI == 1 ? ln : (ln & 31), rly0 = (int32_t)(threadIdx.x >> 6) * RPI + (RPI == 1 ? 0 : ln >> 5);
+    const uint32_t rcol = (uint32_t)clampi(lo_x + rlx, 0, wm);
+    const bool rcol_in = rlx < cx;
+    uint32_t raw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t ly = rly0 + 4 * RPI * r;
+        raw[r] = a.px[__umul24((uint32_t)clampi(lo_y + ly, 0, hm), a.w) + rcol];  // clamped: always inside
+    }
+#else
     constexpr int R = (FP * FP + 255) / 256;
     uint32_t raw[R];
-    const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
         raw[r] = 0xFF000000u;
         if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
     }
+#endif
     // plan entries as tile offsets: entry e < 256 column (e >> 5, e & 31), else row
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -928,6 +950,21 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         }
     load_tables(tb, L);
     BP_T(1);
+#if BH_BLOOM_ROWLOAD
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int32_t ly = rly0 + 4 * RPI * r;
+        const bool v = rcol_in && ly < cy;
+        const int32_t o = v ? ly * FS + rlx + (ly >> 1) : FP * FS + FP / 2;  // else the spare slot
+        if constexpr (RAW) {
+            tile[o] = raw[r];
+        } else {
+            const F4 d = dec(L, raw[r]);
+            tile[o] = make_float4(d.r, d.g, d.b, d.a);
+        }
+        m = min(m, v ? raw[r] : 0xFF000000u);
+    }
+#else
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
@@ -941,6 +978,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         }
         m = min(m, raw[r]);
     }
+#endif
     const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
     if constexpr (FIX2) {
 #pragma unroll
