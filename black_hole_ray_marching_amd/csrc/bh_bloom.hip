@@ -822,7 +822,8 @@ constexpr uint32_t FIX_WORDS = 32u * 33u;  // one padded 32 x 32 array of words
 // BH_BLOOM_ROWLOAD: the footprint staged row by row -- wave w loads tile rows w, w + 4, ... (two rows per
 // wave-instruction when FP <= 32), lane = column -- so each load's address is one 24-bit multiply-add off a
 // per-lane column and a per-round row, and an out-of-footprint lane stores into a spare tile slot instead of
-// branching; the linear form (A/B: 0) divides its element index by the footprint width for every load
+// branching; where rows of FP lanes take fewer rounds (FP = 40: 7 instead of 10) the element index is split
+// by the constant FP instead.  The linear form (A/B: 0) divides its element index by the footprint width.
 #ifndef BH_BLOOM_ROWLOAD
 #define BH_BLOOM_ROWLOAD 1
 #endif
@@ -879,16 +880,32 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // the host sizes FP: no cut
     const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
 #if BH_BLOOM_ROWLOAD
-    constexpr int RPI = FP > 32 ? 1 : 2, R = (FP + 4 * RPI - 1) / (4 * RPI);  // rows per wave-instruction, rounds
+    // rows per wave-instruction and rounds; LIN: rows of FP elements (constant split) when that takes fewer rounds
+    constexpr int RPI = FP > 32 ? 1 : 2, RR = (FP + 4 * RPI - 1) / (4 * RPI), RL = (FP * FP + 255) / 256;
+    constexpr bool LIN = RL < RR;
+    constexpr int R = LIN ? RL : RR;
     const int32_t ln = (int32_t)(threadIdx.x & 63u);
     const int32_t rlx = RPI == 1 ? ln : (ln & 31), rly0 = (int32_t)(threadIdx.x >> 6) * RPI + (RPI == 1 ? 0 : ln >> 5);
     const uint32_t rcol = (uint32_t)clampi(lo_x + rlx, 0, wm);
     const bool rcol_in = rlx < cx;
+    // element (ly, lx) of round r
+    auto rl_at = [&](int r, int32_t& ly, int32_t& lx) {
+        if constexpr (LIN) {
+            const uint32_t i = threadIdx.x + 256u * (uint32_t)r;
+            ly = (int32_t)(i / (uint32_t)FP);
+            lx = (int32_t)i - ly * FP;
+        } else {
+            ly = rly0 + 4 * RPI * r;
+            lx = rlx;
+        }
+    };
     uint32_t raw[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int32_t ly = rly0 + 4 * RPI * r;
-        raw[r] = a.px[__umul24((uint32_t)clampi(lo_y + ly, 0, hm), a.w) + rcol];  // clamped: always inside
+        int32_t ly, lx;
+        rl_at(r, ly, lx);
+        const uint32_t col = LIN ? (uint32_t)clampi(lo_x + lx, 0, wm) : rcol;
+        raw[r] = a.px[__umul24((uint32_t)clampi(lo_y + ly, 0, hm), a.w) + col];  // clamped: always inside
     }
 #else
     constexpr int R = (FP * FP + 255) / 256;
@@ -953,9 +970,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
 #if BH_BLOOM_ROWLOAD
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int32_t ly = rly0 + 4 * RPI * r;
-        const bool v = rcol_in && ly < cy;
-        const int32_t o = v ? ly * FS + rlx + (ly >> 1) : FP * FS + FP / 2;  // else the spare slot
+        int32_t ly, lx;
+        rl_at(r, ly, lx);
+        const bool v = (LIN ? lx < cx : rcol_in) && ly < cy;
+        const int32_t o = v ? ly * FS + lx + (ly >> 1) : FP * FS + FP / 2;  // else the spare slot
         if constexpr (RAW) {
             tile[o] = raw[r];
         } else {
@@ -1875,6 +1893,25 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
         const int32_t wm = (int32_t)X.w - 1, hm = (int32_t)X.h - 1;
         constexpr int R = (FP_YQ * FP_YQ + 255) / 256;
         uint32_t raw[R];
+#if BH_BLOOM_ROWLOAD
+        // rows of FP_YQ elements (a constant split, see up_sepq_kernel's BH_BLOOM_ROWLOAD); the elements past the
+        // footprint load clamped texels and store into the spare slot
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = threadIdx.x + 256u * (uint32_t)r;
+            const int32_t ly = (int32_t)(i / (uint32_t)FP_YQ), lx = (int32_t)i - ly * FP_YQ;
+            raw[r] = X.px[__umul24((uint32_t)clampi(y0 + ly, 0, hm), X.w) + (uint32_t)clampi(x0 + lx, 0, wm)];
+        }
+        load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t i = threadIdx.x + 256u * (uint32_t)r;
+            const int32_t ly = (int32_t)(i / (uint32_t)FP_YQ), lx = (int32_t)i - ly * FP_YQ;
+            const bool v = lx < nx && ly < ny;
+            const F4 d = dec(L, raw[r]);
+            tile[v ? ly * FS_YQ + lx + ((ly + p) >> 1) : FP_YQ * FS_YQ + FP_YQ / 2] = make_float4(d.r, d.g, d.b, d.a);
+        }
+#else
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
@@ -1889,6 +1926,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
                 tile[ly * FS_YQ + lx + ((ly + p) >> 1)] = make_float4(d.r, d.g, d.b, d.a);
             }
         }
+#endif
     }
     __syncthreads();
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner

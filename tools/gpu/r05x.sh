@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 $O/pytest_bloom.log
 for rep in 1 2 3; do
   for v in main rowlin; do
-    for s in "1920 1080" "1280 720"; do
+    for s in "1920 1080" "1280 720" "4096 2048"; do
       set -- $s
       L=black_hole_ray_marching_amd/libbh_render.so; if [ $v != main ]; then L=tools/variants/$v.so; fi
       BH_LIB=$L timeout -k 10 120 python tools/bench_bloom.py --width $1 --height $2 --schedule auto --steps 200 2>>$O/ab.err | sed "s/^/$v /" >> $O/ab.log || exit 1
