@@ -32,7 +32,7 @@ BH_SCHED_FLAG_LATENCY = 0x400       # exact math: force the machine-scheduled bu
 BH_FATE_CAP, BH_FATE_ESCAPE, BH_FATE_SURFACE, BH_FATE_BLACKOUT = 0, 1, 2, 3
 BH_TILE = 8
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 BYTES_PER_PIXEL = {BH_OUT_RGBA32F: 16, BH_OUT_RGBA16F: 8, BH_OUT_BGRA8_SRGB: 4}
 
@@ -115,6 +115,7 @@ SIGNATURES = {
                            C.c_void_p, C.c_void_p]),
     "bh_bloom_check": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.c_char_p,
                                  C.c_size_t]),
+    "bh_bloom_plan_failures": (C.c_int64, [C.c_char_p, C.c_size_t]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
     "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "bh_graph_release": (C.c_int, [C.c_void_p]),

@@ -2999,6 +2999,20 @@ extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint3
     g_why = prev;
     return ok;
 }
+// The fix-up records of a list (records_ok) and, when stc != nullptr, the column strips of the plan's full list
+// with the column records' word 7 (strip_ok, strip_records_ok): what bh_bloom_check's dry run checks at each
+// launch, run by sep_plan on every real plan before it is uploaded.
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_records_verify(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                            const uint32_t* list, uint32_t nc, uint32_t nr,
+                                                                            const uint32_t* rec, const uint32_t* stc,
+                                                                            uint32_t strip_w, std::string* why) {
+    std::string* prev = g_why;
+    g_why = why;
+    const bool ok = records_ok(w, h, plan, list, nc, nr, rec) &&
+                    (!stc || (strip_ok(w, h, plan, list, nc, stc, strip_w) && strip_records_ok(list, nc, stc, rec)));
+    g_why = prev;
+    return ok;
+}
 // Dry mode (bh_bloom_check): while it is on, the launchers below check their launch's form on the host and
 // return without launching; the plan pointers they receive are host copies.
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void) {

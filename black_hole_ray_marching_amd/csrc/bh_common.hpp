@@ -314,6 +314,10 @@ extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint
                                                                           std::vector<uint32_t>* rows2);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                          uint32_t nc, uint32_t nr, std::string* why);
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_records_verify(uint32_t w, uint32_t h, const uint32_t* plan,
+                                                                            const uint32_t* list, uint32_t nc, uint32_t nr,
+                                                                            const uint32_t* rec, const uint32_t* stc,
+                                                                            uint32_t strip_w, std::string* why);
 extern "C" __attribute__((visibility("hidden"))) void bh_bloom_dry_begin(void);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_dry_end(uint64_t* launches, uint64_t* checks,
                                                                      std::string* fail, std::string* plan);

@@ -709,6 +709,27 @@ BloomPlan bloom_plan(uint32_t W, uint32_t H, uint32_t levels) {
 // set not prepared outside capture).
 // The column strips' storage limit per plan (3 words per strip column and row: 1.3 MB at 1920 x 1080)
 constexpr size_t BH_STRIPS_BUDGET = (size_t)64 << 20;
+// A plan the host check refused: in dry mode the check's failure; in a real bh_bloom a process-wide count and
+// last message (bh_bloom_plan_failures) and one line on stderr, so that a regression in plan generation --
+// bit-exact, but the slower general kernel -- does not pass silently.
+std::atomic<uint64_t> g_plan_failures{0};
+std::string g_plan_last;  // guarded by g_plan_mu
+std::atomic_flag g_plan_mu = ATOMIC_FLAG_INIT;
+void plan_failure(std::string* dry_fail, uint32_t ow, uint32_t oh, uint32_t tw, uint32_t th, uint32_t rx, uint32_t ry,
+                  const std::string& why) {
+    const std::string msg = "plan " + std::to_string(ow) + "x" + std::to_string(oh) + " <- " + std::to_string(tw) + "x" +
+                            std::to_string(th) + " res " + std::to_string(rx) + "x" + std::to_string(ry) + ": " + why;
+    if (dry_fail) {
+        if (dry_fail->empty()) *dry_fail = msg;
+        return;
+    }
+    while (g_plan_mu.test_and_set(std::memory_order_acquire)) std::this_thread::yield();
+    g_plan_last = msg;
+    g_plan_mu.clear(std::memory_order_release);
+    if (g_plan_failures.fetch_add(1) == 0)
+        std::fprintf(stderr, "bh_bloom: a host check refused a plan; its pass runs the general kernel (same bytes, "
+                             "slower): %s\n", msg.c_str());
+}
 // Returned by value: the cache is a vector that later plans reallocate.  (Round 4's memory-access fault:
 // a pointer into it, held across the next call, read a freed record's fix-up counts)
 bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* dry_fail, uint32_t ow, uint32_t oh,
@@ -763,17 +784,38 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
                 bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc, P.nrr, R);
                 L += P.nrc + P.nrr; R += 8u * (P.nrc + P.nrr);
                 bh_bloom_fixup_records(ow, oh, h->data(), L, P.nrc2, P.nrr2, R);
+                // every list's records as the fix-up kernels read them (a failure drops the plan)
+                {
+                    const uint32_t* Lc = h->data() + lists;
+                    const uint32_t* Rc = h->data() + P.rec;
+                    const uint32_t nlist[3][2] = {{P.nc, P.nr}, {P.nrc, P.nrr}, {P.nrc2, P.nrr2}};
+                    for (int li = 0; ok && li < 3; ++li) {
+                        ok = bh_bloom_records_verify(ow, oh, h->data(), Lc, nlist[li][0], nlist[li][1], Rc, nullptr, 0u, &why);
+                        Lc += nlist[li][0] + nlist[li][1];
+                        Rc += 8u * (nlist[li][0] + nlist[li][1]);
+                    }
+                }
                 // the column strips of the final fix-up (BH_BLOOM_NO_STRIPS: off, A/B), within a storage budget
                 static const bool no_strips = std::getenv("BH_BLOOM_NO_STRIPS") != nullptr;
-                if (!no_strips && P.nc > 0u) {
+                if (ok && !no_strips && P.nc > 0u) {
                     const size_t at = h->size();
                     h->resize(at + ow, 0u);
                     const uint32_t stw = bh_bloom_strip_table(ow, h->data() + lists, P.nc, h->data() + at);
                     if (stw > 0u && 3u * (size_t)stw * oh * 4u <= BH_STRIPS_BUDGET) {
-                        P.stc = at;
-                        P.stw = stw;
                         // word 7 of each column record: 1 + the column's strip column
                         for (uint32_t k = 0; k < P.nc; ++k) (*h)[P.rec + 8u * k + 7u] = (*h)[at + (*h)[lists + k]];
+                        // checked before upload: the gather kernel clamps its strip column, so a wrong table would
+                        // give wrong pixels, not a fault; a failing table drops the strips (the plain fix-up runs)
+                        std::string swhy;
+                        if (bh_bloom_records_verify(ow, oh, h->data(), h->data() + lists, P.nc, 0u, h->data() + P.rec,
+                                                    h->data() + at, stw, &swhy)) {
+                            P.stc = at;
+                            P.stw = stw;
+                        } else {
+                            for (uint32_t k = 0; k < P.nc; ++k) (*h)[P.rec + 8u * k + 7u] = 0u;
+                            h->resize(at);
+                            plan_failure(dry_fail, ow, oh, tw, th, rx, ry, "strips dropped: " + swhy);
+                        }
                     } else {
                         h->resize(at);
                     }
@@ -782,9 +824,7 @@ bh_ctx::SepPlan sep_plan(bh_ctx::BloomScratch* b, bool capturing, std::string* d
         }
     }
     if (!ok) {
-        if (dry_fail && !why.empty() && dry_fail->empty())
-            *dry_fail = "plan " + std::to_string(ow) + "x" + std::to_string(oh) + " <- " + std::to_string(tw) + "x" +
-                        std::to_string(th) + " res " + std::to_string(rx) + "x" + std::to_string(ry) + ": " + why;
+        if (!why.empty()) plan_failure(dry_fail, ow, oh, tw, th, rx, ry, why);
         bh_ctx::SepPlan none;
         none.key = key;
         b->sep_plans.push_back(none);
@@ -1083,6 +1123,17 @@ int bh_bloom_check(uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, u
         return BH_ERR_INTERNAL;
     }
     return BH_OK;
+}
+
+int64_t bh_bloom_plan_failures(char* out_last, size_t len) {
+    if (out_last && len) {
+        while (g_plan_mu.test_and_set(std::memory_order_acquire)) std::this_thread::yield();
+        const size_t n = std::min(g_plan_last.size(), len - 1);
+        std::memcpy(out_last, g_plan_last.data(), n);
+        out_last[n] = '\0';
+        g_plan_mu.clear(std::memory_order_release);
+    }
+    return (int64_t)g_plan_failures.load();
 }
 
 int bh_graph_release(bh_ctx* c) {

@@ -201,6 +201,14 @@ def bloom_check(width: int, height: int, levels: int = 3, schedule: int = 0) -> 
     return out
 
 
+def bloom_plan_failures() -> tuple[int, str]:
+    """bh_bloom_plan_failures: (plans real bh_bloom calls built whose host check refused them -- each such pass
+    ran its general kernel, same bytes, slower -- process-wide, the last refusal's message)."""
+    buf = C.create_string_buffer(512)
+    n = load().bh_bloom_plan_failures(buf, len(buf))
+    return int(n), buf.value.decode()
+
+
 def _ptr(t) -> int | None:
     if t is None:
         return None
@@ -558,6 +566,6 @@ def tiles_unpack_rgbm_partition(packed, out_col, out_blackout, partition: "Parti
 __all__ = ["Camera", "Partition", "partition_map", "tiles_unpack_rgbm_partition", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
            "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM", "BH_LAYOUT_TILES_RGBM14",
            "BH_UNPACK_RGBM14",
-           "srgb_encode_table", "load_sky", "BH_OUT_BGRA8_SRGB",
+           "srgb_encode_table", "load_sky", "bloom_plan_failures", "BH_OUT_BGRA8_SRGB",
            "BhError", "MAX_ITERATIONS", "BH_OUT_RGBA32F", "BH_OUT_RGBA16F", "BH_MATH_EXACT", "BH_MATH_FAST",
            "BH_LAYOUT_ROWMAJOR", "BH_LAYOUT_TILES", "BH_LAYOUT_TILES_RGB", "BH_SCENE_DEFAULT", "BYTES_PER_PIXEL"]

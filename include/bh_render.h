@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define BH_ABI_VERSION 7
+#define BH_ABI_VERSION 8
 
 /* Temporal-order states (frame geometry x shard x stream) one ctx keeps (see above). */
 #define BH_ORDER_STATES 32
@@ -300,6 +300,12 @@ int bh_bloom(bh_ctx* ctx, const void* col_bgra8, const void* blackout_bgra8, uin
  * its output and input sizes and resolution uniform; tools/bloom_roofline.py reads it). */
 int bh_bloom_check(uint32_t width, uint32_t height, uint32_t levels, uint32_t schedule, uint64_t* out_launches,
                    char* out_plan, size_t plan_len);
+
+/* Process-wide count of the plans real bh_bloom calls built and whose host check (the checks of
+ * bh_bloom_check) refused: such a pass runs its general kernel -- the same bytes, slower -- and the first
+ * refusal is also reported on stderr.  out_last (optional, len bytes, NUL-terminated, truncated) = the last
+ * refusal's message.  0 for every frame size the tests name. */
+int64_t bh_bloom_plan_failures(char* out_last, size_t len);
 
 /* Graph contract (see the top of this file): unpin every order state and bloom scratch set that a
  * capture marked, so that LRU eviction may free them again.  Call it only after destroying every HIP

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     lib = bh.load()
-    assert lib.bh_abi_version() == _abi.ABI_VERSION == 7
+    assert lib.bh_abi_version() == _abi.ABI_VERSION == 8
     # the Python mirror's constants are the header's
     text = HEADER.read_text()
     for name, value in (("BH_ABI_VERSION", _abi.ABI_VERSION), ("BH_MAX_FRAMES", _abi.BH_MAX_FRAMES),

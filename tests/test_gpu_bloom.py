@@ -53,6 +53,9 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # every grid origin some inexact columns cross a block edge; 3 at the
                                         # best) and nonzero grid origins (1920: 8, 720 rows: 14)
                                         (768, 1366, 3),
+                                        # common display widths the CPU sweep (1..2100) does not reach:
+                                        # their strip tables and records
+                                        (1440, 2560, 3), (2160, 3840, 3),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
                                         (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
@@ -115,6 +118,21 @@ def test_render_then_bloom_matches_oracle_chain(torch_cuda, sky_small):
     oc, ob = bgra(o[0]), bgra(o[1])
     assert np.array_equal(col.cpu().numpy(), oc) and np.array_equal(bo.cpu().numpy(), ob)
     assert np.array_equal(out.cpu().numpy(), oracle.bloom(oc, ob, 3))
+    scene.close()
+
+
+def test_no_plan_was_refused(torch_cuda, sky_small):
+    """Every plan a real bh_bloom builds is checked on the host before upload (records, strips); a refused plan
+    would run the general kernel -- the same bytes, slower -- so the tests' display sizes must refuse none
+    (bh_bloom_plan_failures counts them process-wide)."""
+    torch = torch_cuda
+    scene = bh.Scene(16, 16, sky=sky_small)
+    for H, W in ((1080, 1920), (720, 1280), (1440, 2560), (2160, 3840), (768, 1366), (2048, 4096)):
+        t = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        scene.bloom(t, t, torch.empty_like(t), width=W, height=H)
+    torch.cuda.synchronize()
+    n, last = bh.bloom_plan_failures()
+    assert n == 0, last
     scene.close()
 
 
