@@ -54,53 +54,24 @@ struct F4 { float r, g, b, a; };
 // texture -- run on different XCDs, and every XCD fetches its blocks' footprints through its own L2.
 // Remapped, XCD k processes the k-th eighth of the grid in row-major order (the remainder, fewer than
 // 8 blocks, keeps the raw order): adjacent blocks share an L2.  A bijection of the grid; results never
-// depend on it.  (BH_BLOOM_XCD=0 builds the raw order, for A/B.)
-#ifndef BH_BLOOM_XCD
-#define BH_BLOOM_XCD 1
-#endif
+// depend on it.
 __device__ __forceinline__ uint2 xcd_block() {
-#if BH_BLOOM_XCD
     const uint32_t gx = gridDim.x, n = gx * gridDim.y;
     const uint32_t b = blockIdx.y * gx + blockIdx.x, per = n >> 3;
     const uint32_t t = b < (per << 3) ? (b & 7u) * per + (b >> 3) : b;
     const uint32_t ty = t / gx;
     return make_uint2(t - ty * gx, ty);
-#else
-    return make_uint2(blockIdx.x, blockIdx.y);
-#endif
 }
 
 // LDS tables of a block: sRGB decode (256), alpha decode k/255 (256) and the encoder: its thresholds
-// (257) and base codes (table form), or (BH_BLOOM_ETAB) its code table (one read per channel instead of
-// two dependent ones; bh_srgb.hpp)
-#ifndef BH_BLOOM_ETAB
-#define BH_BLOOM_ETAB 0
-#endif
-// BH_BLOOM_ALUT_CONST (A/B): the alpha decode k/255 from a constant-memory table instead of LDS (1 KiB less
-// LDS per block; only blocks with a non-opaque texel read it)
-#ifndef BH_BLOOM_ALUT_CONST
-#define BH_BLOOM_ALUT_CONST 0
-#endif
-#if BH_BLOOM_ALUT_CONST
-struct AlphaTable {
-    float v[256];
-    constexpr AlphaTable() : v() {
-        for (int k = 0; k < 256; ++k) v[k] = (float)k / 255.0f;  // IEEE division, folded at compile time
-    }
-};
-__constant__ AlphaTable c_alut{};
-#endif
+// (257) and base codes (table form, bh_srgb.hpp).  (Measured and not kept, DESIGN.md §7b: the encoder's
+// code table -- one read per channel instead of two dependent ones -- and the alpha decode from constant
+// memory instead of LDS.)
 struct Lds {
     float lut[256];
-#if !BH_BLOOM_ALUT_CONST
     float alut[256];
-#endif
-#if BH_BLOOM_ETAB
-    uint32_t E[SRGB_CODES];
-#else
     float T[SRGB_TABLE];
     uint32_t B32[SRGB_BUCKETS / 4];
-#endif
 };
 struct Tables {
     const float* lut;      // 256
@@ -110,26 +81,17 @@ struct Tables {
 };
 __device__ __forceinline__ void load_tables(Tables tb, Lds& L) {
     L.lut[threadIdx.x] = tb.lut[threadIdx.x];
-#if !BH_BLOOM_ALUT_CONST
     L.alut[threadIdx.x] = (float)threadIdx.x / 255.0f;
-#endif
-#if BH_BLOOM_ETAB
-    for (uint32_t i = threadIdx.x; i < (uint32_t)SRGB_CODES; i += 256) L.E[i] = tb.code[i];
-#else
     L.T[threadIdx.x] = tb.enc[threadIdx.x];
     if (threadIdx.x == 0) L.T[256] = tb.enc[256];
     const uint32_t* b = reinterpret_cast<const uint32_t*>(tb.bkt);
     for (uint32_t i = threadIdx.x; i < SRGB_BUCKETS / 4; i += 256) L.B32[i] = b[i];
-#endif
     __syncthreads();
 }
 
 // A1: the caller knows the texel's alpha byte is 255 (a block whose inputs are all opaque, see
 // with_source): alpha decodes to 1.0 without a table read, and the compiler folds the alpha channel's
 // whole arithmetic (sums, x/12, the encoder) to constants
-#ifndef BH_BLOOM_OPAQUE
-#define BH_BLOOM_OPAQUE 1  // 0 (A/B): never take the opaque-block forms
-#endif
 // Block-wide AND of a predicate at a barrier the caller needs anyway: one ballot per wave, its lane 0's
 // word in LDS, the barrier, then every thread reads the 4 words (__syncthreads_and costs an LDS atomic
 // per thread on one address).
@@ -142,11 +104,7 @@ __device__ __forceinline__ bool barrier_and(bool p) {
 }
 template <bool A1 = false>
 __device__ __forceinline__ F4 dec(const Lds& L, uint32_t t) {
-#if BH_BLOOM_ALUT_CONST
-    return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : c_alut.v[t >> 24]};
-#else
     return {L.lut[(t >> 16) & 0xffu], L.lut[(t >> 8) & 0xffu], L.lut[t & 0xffu], A1 ? 1.0f : L.alut[t >> 24]};
-#endif
 }
 // lo <= hi: one v_med3_i32
 __device__ __forceinline__ int32_t clampi(int32_t v, int32_t lo, int32_t hi) { return min(max(v, lo), hi); }
@@ -158,14 +116,9 @@ __device__ __forceinline__ uint32_t unorm8(float a) {
 }
 // the Bgra8UnormSrgb store of a pass's result
 __device__ __forceinline__ uint32_t enc(const Lds& L, F4 c) {
-#if BH_BLOOM_ETAB
-    return srgb_encode_code(c.b, L.E) | (srgb_encode_code(c.g, L.E) << 8) | (srgb_encode_code(c.r, L.E) << 16) |
-           (unorm8(c.a) << 24);
-#else
     const uint8_t* B = reinterpret_cast<const uint8_t*>(L.B32);
     return srgb_encode_lut(c.b, B, L.T) | (srgb_encode_lut(c.g, B, L.T) << 8) | (srgb_encode_lut(c.r, B, L.T) << 16) |
            (unorm8(c.a) << 24);
-#endif
 }
 template <bool A1 = false>
 __device__ __forceinline__ F4 quant(const Lds& L, F4 c) { return dec<A1>(L, enc(L, c)); }
@@ -465,7 +418,7 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
         for (int a = 0; a < R; ++a)
 #pragma unroll
             for (int b = 0; b < R; ++b) m = min(m, raw[a][b]);
-        const bool a1 = barrier_and(opaque && m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+        const bool a1 = barrier_and(opaque && m >= 0xFF000000u);
         const int32_t px = (int32_t)bx + tx, py = (int32_t)by + ty;
         if (a1) body(PlanSrc<FP, RAW, STD, true>{t, tile, x0, y0, &P, &L, px, py});
         else body(PlanSrc<FP, RAW, STD, false>{t, tile, x0, y0, &P, &L, px, py});
@@ -504,11 +457,8 @@ __device__ __forceinline__ void with_source(Tables tb, CTex t, Lds& L, float4* t
     }
 }
 
-#ifndef BH_BLOOM_WPE
-#define BH_BLOOM_WPE 1
-#endif
 // occupancy floor for the 8-tap kernels: the unrolled taps otherwise take 160 VGPRs (3 waves/SIMD)
-#define BLOOM_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_WPE)))
+#define BLOOM_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
 constexpr int FP_UP = 24;     // staged footprint of a generic up pass (taps within a few texels)
 constexpr int FP_Y = 24;      // blur1 at full size: taps within +-3 texels (22 x 22)
 constexpr int FP_FINAL = 44;  // the last up pass at res / 4: taps within +-12 texels (42 x 42)
@@ -548,9 +498,6 @@ __device__ __forceinline__ F4 lerp_plan(const float4& t00, const float4& t10, co
     return q;
 }
 
-#ifndef BH_BLOOM_SEP_PIPE
-#define BH_BLOOM_SEP_PIPE 1
-#endif
 // FP: the staged footprint's side.  RAW: the tile holds the BGRA8 words (4 B per texel instead of 16, for
 // the wide footprint of the final pass: 44 x 48 words = 8.4 KiB instead of 33 KiB), decoded when a tap
 // reads them.  FS: the tile's row stride, a multiple of 16 float4 for the decoded tile (ds_read_b128 lane
@@ -628,21 +575,12 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
         m = min(m, raw[r]);
     }
     // every staged texel (and every own texel) opaque: alpha 1.0 throughout, its arithmetic folds away
-    const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+    const bool a1 = barrier_and(m >= 0xFF000000u);
     if (!in) return;
     auto run = [&](auto A1c) {
         constexpr bool A1 = decltype(A1c)::value;
-        auto texel = [&](int32_t o) {
-            if constexpr (RAW) {
-                const F4 d = dec<A1>(L, tile[o]);
-                return make_float4(d.r, d.g, d.b, d.a);
-            } else {
-                return tile[o];
-            }
-        };
         F4 s{0.0f, 0.0f, 0.0f, 0.0f};
         SepEntry c = colp[0][tx], r = rowp[0][ty];
-#if BH_BLOOM_SEP_PIPE
         // software-pipelined: tap i + 1's four tile reads are issued before tap i computes (the LDS
         // latency of one tap hides behind the other's lerps); RAW tiles pipeline the words, decoded at use
         using W = std::conditional_t<RAW, uint32_t, float4>;
@@ -652,7 +590,6 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
             const int32_t o = c.f + r.f;
             w00 = word(o); w10 = word(o + 1); w01 = word(o + FS); w11 = word(o + FS + 1);
         }
-#endif
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             // the next tap's plan entries are read while this tap computes; one tap at a time otherwise
@@ -663,7 +600,6 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 cn = colp[i + 1][tx];
                 rn = rowp[i + 1][ty];
             }
-#if BH_BLOOM_SEP_PIPE
             const W v00 = w00, v10 = w10, v01 = w01, v11 = w11;
             if (i < 7) {
                 const int32_t on = cn.f + rn.f;
@@ -678,10 +614,6 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
                 }
             };
             const float4 t00 = unpack(v00), t10 = unpack(v10), t01 = unpack(v01), t11 = unpack(v11);
-#else
-            const int32_t o = c.f + r.f;
-            const float4 t00 = texel(o), t10 = texel(o + 1), t01 = texel(o + FS), t11 = texel(o + FS + 1);
-#endif
             const float ia = c.ia, fa = c.fa, ib = r.ia, fb = r.fa;  // sample()'s operations in its order
             F4 q;
             q.r = (t00.x * ia + t10.x * fa) * ib + (t01.x * ia + t11.x * fa) * fb;
@@ -729,78 +661,20 @@ __global__ void BLOOM_BOUNDS up_sep_kernel(Tables tb, CTex a, uint32_t rx, uint3
 // two apart (a same-size pass's consecutive quad rows) are 2 FS + 1 entries apart and the next quad row
 // reads the other bank parity (the yq tile's row-pair shift, see FS_YQ).  A row entry of the plan holds
 // that row offset and (pad) the row ly itself: the row below is FS + (ly & 1) further.
-#ifndef BH_BLOOM_SEPQ_STREAM
-#define BH_BLOOM_SEPQ_STREAM 1
-#endif
-// BH_BLOOM_SEPQ_E8: the block's plan entries in 8 bytes (floor offset and row as int16, fa; ia = 1 - fa
-// recomputed, the host plan's own operation) -- 4 KiB less LDS per block.  BH_BLOOM_SEPQ_WPE: a waves per
-// EU bound for the quad kernel (0: none).  Both A/B switches.
-#ifndef BH_BLOOM_SEPQ_E8
-#define BH_BLOOM_SEPQ_E8 1
-#endif
-#ifndef BH_BLOOM_SEPQ_WPE
-#define BH_BLOOM_SEPQ_WPE 6
-#endif
-#if BH_BLOOM_SEPQ_E8
+// The block's plan entries in 8 bytes (floor offset and row as int16, fa; ia = 1 - fa recomputed, the host
+// plan's own operation) -- 4 KiB less LDS per block than the 16-byte SepEntry.
 struct QEntry { int16_t f, pad; float fa; };
 __device__ __forceinline__ float q_ia(const QEntry& e) { return 1.0f - e.fa; }
 __device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry& e) {
     return {(int16_t)f, (int16_t)pad, e.fa};
 }
-#else
-using QEntry = SepEntry;
-__device__ __forceinline__ float q_ia(const QEntry& e) { return e.ia; }
-__device__ __forceinline__ QEntry q_entry(int32_t f, int32_t pad, const SepEntry& e) { return {f, e.fa, e.ia, pad}; }
-#endif
-// The raw 60-word tile's row stride (A/B; any stride keeps the quad rows' bank parity: the next quad row
-// is 2 FS + 1 words further, an odd number).  64 instead of 80: 15 KiB of tile instead of 19
-// BH_BLOOM_SEPQ_AXIS: a tap whose floor steps are wave-uniform along one axis only shares that axis's texels
-// (xgen / ygen below) instead of reading each pixel's four (A/B switch)
-#ifndef BH_BLOOM_SEPQ_AXIS
-#define BH_BLOOM_SEPQ_AXIS 0  // measured slower (1920x1080 chain 0.1239 -> 0.1261 ms, profiles/r05/bloom_fix/)
-#endif
-#ifndef BH_BLOOM_SEPQ_FS60
-#define BH_BLOOM_SEPQ_FS60 64
-#endif
-#if BH_BLOOM_SEPQ_WPE
-#define SEPQ_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BH_BLOOM_SEPQ_WPE)))
-#else
-#define SEPQ_BOUNDS __launch_bounds__(256)
-#endif
+// The raw 60-word tile's row stride (any stride keeps the quad rows' bank parity: the next quad row is
+// 2 FS + 1 words further, an odd number).  64 instead of 80: 15 KiB of tile instead of 19
+constexpr int SEPQ_FS60 = 64;
+// an occupancy floor of 6 waves per EU for the quad kernel
+#define SEPQ_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6)))
 template <int FP, bool RAW>
 constexpr int sepq_stride() { return RAW ? (FP + 16) / 32 * 32 + 16 : (FP + 15) / 16 * 16; }
-// Diagnostic build (-DBH_BLOOM_PHASES=1, tools/probe_bloom_phases.py): every wave of up_sepq_kernel writes
-// one record (plain stores, no atomics: a shared counter's contention would stretch what it measures) into
-// the launch's slot of g_bp_rec -- slot g_bp_slot, which the launcher sets in stream order before each
-// quad launch: [0] global start and [1] end (s_memrealtime, 100 MHz, low 32 bits), [2..5] shader cycles of
-// start -> footprint, own-texel and table loads issued + tables staged, -> tile written + barrier, -> the 8
-// taps, -> epilogue stored; [6] cycles start -> end; [7] FP.  Wave 0 of block 0 also writes the slot's header.
-#ifndef BH_BLOOM_PHASES
-#define BH_BLOOM_PHASES 0
-#endif
-#if BH_BLOOM_PHASES
-constexpr uint32_t BP_SLOTS = 8, BP_MAXW = 40960;
-__device__ uint32_t g_bp_slot;
-__device__ uint32_t g_bp_rec[BP_SLOTS][BP_MAXW][8];
-__device__ uint32_t g_bp_hdr[BP_SLOTS][4];  // FP, EPI, grid blocks, output width
-#define BP_T(i) (bp[i] = (uint32_t)__builtin_amdgcn_s_memtime())
-// one wave's record (lanes 0..7) and, from wave 0, the launch's header; fp 0 marks a fix-up launch
-__device__ __forceinline__ void bp_record(const uint32_t (&bp)[5], uint32_t real0, uint32_t wave, uint32_t fp, uint32_t epi,
-                                          uint32_t blocks, uint32_t ow) {
-    const uint32_t t_end = (uint32_t)__builtin_amdgcn_s_memtime();
-    const uint32_t real_end = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    const uint32_t lane = threadIdx.x & 63u, slot = g_bp_slot % BP_SLOTS;
-    if (lane < 8u && wave < BP_MAXW) {
-        uint32_t v = fp;
-        v = lane == 0u ? real0 : lane == 1u ? real_end : lane == 6u ? t_end - bp[0] : v;
-        for (int i = 0; i < 4; ++i) v = lane == 2u + i ? bp[i + 1] - bp[i] : v;
-        g_bp_rec[slot][wave][lane] = v;
-    }
-    if (wave == 0u && lane < 4u) g_bp_hdr[slot][lane] = lane == 0u ? fp : lane == 1u ? epi : lane == 2u ? blocks : ow;
-}
-#else
-#define BP_T(i) do {} while (0)
-#endif
 // FIX (EPI_Y only): the block also recomputes its inexact pixels whose same-size sample stays inside the
 // block -- S(X) from the staged tile, S(U1) from the block's own U words exchanged through LDS after a
 // barrier -- so the fix-up pass keeps only the columns and rows whose sample crosses a block edge (none for
@@ -812,21 +686,15 @@ __device__ __forceinline__ void bp_record(const uint32_t (&bp)[5], uint32_t real
 // -- B from the block's words, Y and col from the block's own words, all through LDS.  Its three barriers
 // come after the taps, so the dead tile holds the B, Y and F words and the dead plan entries the col words.
 constexpr uint32_t FIX_WORDS = 32u * 33u;  // one padded 32 x 32 array of words
-// BH_BLOOM_OWN_LATE: the epilogue's own texels are loaded after the tile is staged, so that the launch's first
-// waves load only their footprints (its opening burst is HBM-bound) and the own texels arrive during the taps;
-// the block's opaque test then covers the footprint only, and the epilogue decodes the own texels' alpha unless
-// its wave's own texels are all opaque too (A/B: 0 loads them with the footprint)
-#ifndef BH_BLOOM_OWN_LATE
-#define BH_BLOOM_OWN_LATE 1
-#endif
-// BH_BLOOM_ROWLOAD: the footprint staged row by row -- wave w loads tile rows w, w + 4, ... (two rows per
-// wave-instruction when FP <= 32), lane = column -- so each load's address is one 24-bit multiply-add off a
-// per-lane column and a per-round row, and an out-of-footprint lane stores into a spare tile slot instead of
-// branching; where rows of FP lanes take fewer rounds (FP = 40: 7 instead of 10) the element index is split
-// by the constant FP instead.  The linear form (A/B: 0) divides its element index by the footprint width.
-#ifndef BH_BLOOM_ROWLOAD
-#define BH_BLOOM_ROWLOAD 1
-#endif
+// The epilogue's own texels are loaded after the tile is staged ("late"), so that the launch's first waves
+// load only their footprints (its opening burst is HBM-bound) and the own texels arrive during the taps; the
+// block's opaque test then covers the footprint only, and the epilogue decodes the own texels' alpha unless
+// its wave's own texels are all opaque too.
+// The footprint is staged row by row -- wave w loads tile rows w, w + 4, ... (two rows per wave-instruction
+// when FP <= 32), lane = column -- so each load's address is one 24-bit multiply-add off a per-lane column and
+// a per-round row, and an out-of-footprint lane stores into a spare tile slot instead of branching; where rows
+// of FP lanes take fewer rounds (FP = 40: 7 instead of 10) the element index is split by the constant FP
+// instead.
 template <int FP, bool RAW, int FS>
 constexpr bool sepq_fix2_fits() {
     return sizeof(std::conditional_t<RAW, uint32_t, float4>) * (FP * FS + FP / 2) >= 3u * FIX_WORDS * 4u;
@@ -840,10 +708,10 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     // FIX2: the final epilogue's fix (an instantiation whose tile cannot hold its words never takes it; the
     // host does not request it there, bh_bloom_sep_fix_ok)
     constexpr bool FIX1 = FIX && EPI == EPI_Y, FIX2 = FIX && EPI == EPI_FINAL && sepq_fix2_fits<FP, RAW, FS>();
-    constexpr bool LATE = BH_BLOOM_OWN_LATE && EPI != EPI_PLAIN && !FIX2;
+    constexpr bool LATE = EPI != EPI_PLAIN && !FIX2;
     using TileT = std::conditional_t<RAW, uint32_t, float4>;
     __shared__ Lds L;
-    // + 1: the spare slot of BH_BLOOM_ROWLOAD's out-of-footprint lanes
+    // + 1: the spare slot of the row-wise staging's out-of-footprint lanes
     __shared__ __attribute__((aligned(16))) unsigned char tile_mem[sizeof(TileT) * (FP * FS + FP / 2 + 1)];
     TileT* const tile = reinterpret_cast<TileT*>(tile_mem);
     // plan entries by parity (even columns, then odd): a quad's two entries are consecutive 16-B slots across
@@ -857,11 +725,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     // FIX2: the same-size plan entries of the block's columns and rows, staged with the footprint (in registers
     // across the taps they pushed the final pass past its 80 VGPRs into scratch)
     __shared__ uint2 sce[FIX2 ? 32 : 1], sre[FIX2 ? 32 : 1];
-#if BH_BLOOM_PHASES
-    uint32_t bp[5];
-    const uint32_t bp_real0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-#endif
-    BP_T(0);
     // the block's first column / row (negative for the first block of a grid with an origin offset: wrapped,
     // so x < ow fails for the columns left of the frame) and the first ones inside the frame
     const uint32_t bx = xcd_block().x * 32u - (org & 0xFFFFu), by = xcd_block().y * 32u - (org >> 16);
@@ -879,7 +742,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     const int32_t hi_y = (int32_t)floorf(sample_coord(texcoord(yl, Rh) + k.dv_max(), a.h));
     const int32_t cx = min(hi_x - lo_x + 2, FP), cy = min(hi_y - lo_y + 2, FP);  // the host sizes FP: no cut
     const int32_t wm = (int32_t)a.w - 1, hm = (int32_t)a.h - 1;
-#if BH_BLOOM_ROWLOAD
     // rows per wave-instruction and rounds; LIN: rows of FP elements (constant split) when that takes fewer rounds
     constexpr int RPI = FP > 32 ? 1 : 2, RR = (FP + 4 * RPI - 1) / (4 * RPI), RL = (FP * FP + 255) / 256;
     constexpr bool LIN = RL < RR;
@@ -907,16 +769,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         const uint32_t col = LIN ? (uint32_t)clampi(lo_x + lx, 0, wm) : rcol;
         raw[r] = a.px[__umul24((uint32_t)clampi(lo_y + ly, 0, hm), a.w) + col];  // clamped: always inside
     }
-#else
-    constexpr int R = (FP * FP + 255) / 256;
-    uint32_t raw[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
-        raw[r] = 0xFF000000u;
-        if (ly < cy) raw[r] = a.px[(uint32_t)clampi(lo_y + ly, 0, hm) * a.w + clampi(lo_x + lx, 0, wm)];
-    }
-#endif
     // plan entries as tile offsets: entry e < 256 column (e >> 5, e & 31), else row
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -966,8 +818,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             m = min(m, min(o0[b][c], o1[b][c]));
         }
     load_tables(tb, L);
-    BP_T(1);
-#if BH_BLOOM_ROWLOAD
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int32_t ly, lx;
@@ -982,22 +832,7 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
         }
         m = min(m, v ? raw[r] : 0xFF000000u);
     }
-#else
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / cx, lx = i - ly * cx;
-        if (ly < cy) {
-            if constexpr (RAW) {
-                tile[ly * FS + lx + (ly >> 1)] = raw[r];
-            } else {
-                const F4 d = dec(L, raw[r]);
-                tile[ly * FS + lx + (ly >> 1)] = make_float4(d.r, d.g, d.b, d.a);
-            }
-        }
-        m = min(m, raw[r]);
-    }
-#endif
-    const bool a1 = barrier_and(m >= 0xFF000000u) && BH_BLOOM_OPAQUE;
+    const bool a1 = barrier_and(m >= 0xFF000000u);
     if constexpr (FIX2) {
 #pragma unroll
         for (int b = 0; b < 2; ++b)
@@ -1015,21 +850,11 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             }
         __builtin_amdgcn_sched_barrier(0);  // issued here, awaited in the epilogue
     }
-    BP_T(2);
-#if BH_BLOOM_PHASES
-    bp[3] = bp[2];
-#endif
     // a quad whose first pixel is outside is outside as a whole (even origin offsets); it has no taps, but
     // with FIX its lanes still meet the block's barriers
     const bool live = in[0][0];
     uint32_t bw[2][2] = {}, fw[2][2] = {};  // FIX2: the quad's B words and (exact pixels) F words
-    if (!FIX1 && !FIX2 && !live) {
-#if BH_BLOOM_PHASES
-        goto phases;
-#else
-        return;
-#endif
-    }
+    if (!FIX1 && !FIX2 && !live) return;
     {
     auto run = [&](auto A1c) {
         constexpr bool A1 = decltype(A1c)::value;
@@ -1067,7 +892,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             const int32_t d1 = FS + (rT.pad & 1), d2 = 2 * FS + 1;  // the window's rows 1 and 2
             auto window = [&](auto DXc, auto DYc) {
                 constexpr int DX = decltype(DXc)::value, DY = decltype(DYc)::value;
-#if BH_BLOOM_SEPQ_STREAM
                 // rows 0 and 1 for the top pixels, then row 2 replaces row 0 for the bottom ones: 2 (2 + DX)
                 // texels live at a time instead of 3 (2 + DX)
                 float4 t0[2 + DX], t1[2 + DX];
@@ -1094,69 +918,11 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
                         acc(s[1][c], lerp(t0[ca], t0[ca + 1], t1[ca], t1[ca + 1], c ? cR : cL, rB), i);
                     }
                 }
-#else
-                float4 t[2 + DY][2 + DX];
-#pragma unroll
-                for (int r = 0; r < 2 + DY; ++r)
-#pragma unroll
-                    for (int c = 0; c < 2 + DX; ++c) t[r][c] = texel(o + (r == 0 ? 0 : r == 1 ? d1 : d2) + c);
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int ca = c ? DX : 0, rb = b ? DY : 0;
-                        acc(s[b][c], lerp(t[rb][ca], t[rb][ca + 1], t[rb + 1][ca], t[rb + 1][ca + 1], c ? cR : cL, b ? rB : rT), i);
-                    }
-#endif
-            };
-            // one axis uniform: the other axis's two pixels read their own texel pairs (per-lane offsets), the
-            // uniform axis shares its rows (columns) as in the window -- 4 (2 + DY) or (2 + DX) 4 reads, not 16
-            auto xgen = [&](auto DYc) {  // rows uniform (step DY), columns per lane: cL.f, cR.f
-                constexpr int DY = decltype(DYc)::value;
-                const int32_t oR = cR.f + rT.f;
-                float4 t0[4], t1[4];
-                t0[0] = texel(o); t0[1] = texel(o + 1); t0[2] = texel(oR); t0[3] = texel(oR + 1);
-                t1[0] = texel(o + d1); t1[1] = texel(o + d1 + 1); t1[2] = texel(oR + d1); t1[3] = texel(oR + d1 + 1);
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-                    acc(s[0][c], lerp(t0[2 * c], t0[2 * c + 1], t1[2 * c], t1[2 * c + 1], c ? cR : cL, rT), i);
-                if constexpr (DY == 1) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    t0[0] = texel(o + d2); t0[1] = texel(o + d2 + 1); t0[2] = texel(oR + d2); t0[3] = texel(oR + d2 + 1);
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        acc(s[1][c], lerp(t1[2 * c], t1[2 * c + 1], t0[2 * c], t0[2 * c + 1], c ? cR : cL, rB), i);
-                } else {
-#pragma unroll
-                    for (int c = 0; c < 2; ++c)
-                        acc(s[1][c], lerp(t0[2 * c], t0[2 * c + 1], t1[2 * c], t1[2 * c + 1], c ? cR : cL, rB), i);
-                }
-            };
-            auto ygen = [&](auto DXc) {  // columns uniform (step DX), rows per lane: rT, rB
-                constexpr int DX = decltype(DXc)::value;
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const QEntry& re = b ? rB : rT;
-                    const int32_t ob = cL.f + re.f, dn = FS + (re.pad & 1);
-                    float4 t0[2 + DX], t1[2 + DX];
-#pragma unroll
-                    for (int c = 0; c < 2 + DX; ++c) { t0[c] = texel(ob + c); t1[c] = texel(ob + dn + c); }
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const int ca = c ? DX : 0;
-                        acc(s[b][c], lerp(t0[ca], t0[ca + 1], t1[ca], t1[ca + 1], c ? cR : cL, re), i);
-                    }
-                    if (b == 0) __builtin_amdgcn_sched_barrier(0);
-                }
             };
             if (uni && dx0 == 1 && dy0 == 1) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 0 && dy0 == 1) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 1>{});
             else if (uni && dx0 == 1 && dy0 == 0) window(std::integral_constant<int, 1>{}, std::integral_constant<int, 0>{});
             else if (uni && dx0 == 0 && dy0 == 0) window(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
-            else if (BH_BLOOM_SEPQ_AXIS && uy && dy0 == 1) xgen(std::integral_constant<int, 1>{});
-            else if (BH_BLOOM_SEPQ_AXIS && uy) xgen(std::integral_constant<int, 0>{});
-            else if (BH_BLOOM_SEPQ_AXIS && ux && dx0 == 1) ygen(std::integral_constant<int, 1>{});
-            else if (BH_BLOOM_SEPQ_AXIS && ux) ygen(std::integral_constant<int, 0>{});
             else {
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
@@ -1171,7 +937,6 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
             asm volatile("" ::"v"(s[0][0].r), "v"(s[0][1].r), "v"(s[1][0].r), "v"(s[1][1].r));
             __builtin_amdgcn_sched_barrier(0);
         }
-        BP_T(3);
         // STRIPS (final epilogue, stc != null): the column strips of the fix-up pass -- each column within 2 of
         // an inexact column (stc: 1 + its strip column, bh_bloom_strip_table) also stores its col, Y and U
         // words column-major, (image * strip_w + strip column) * oh + row
@@ -1351,33 +1116,8 @@ __global__ void SEPQ_BOUNDS up_sepq_kernel(Tables tb, CTex a, uint32_t rx, uint3
     if (a1) run(std::true_type{});
     else run(std::false_type{});
     }
-#if BH_BLOOM_PHASES
-phases:
-    BP_T(4);
-    bp_record(bp, bp_real0, (blockIdx.y * gridDim.x + blockIdx.x) * 4u + (threadIdx.x >> 6), FP, EPI, gridDim.x * gridDim.y, ow);
-#endif
 }
 
-#if BH_BLOOM_PHASES
-static uint32_t g_bp_next = 0;
-// the next quad launch's record slot, in stream order (a pageable source: staged before the call returns)
-static void bp_next_slot(hipStream_t s) {
-    const uint32_t v = g_bp_next++;
-    (void)hipMemcpyToSymbolAsync(HIP_SYMBOL(g_bp_slot), &v, 4, 0, hipMemcpyHostToDevice, s);
-}
-// records of the last `slots` quad launches: hdr [BP_SLOTS][4], rec [BP_SLOTS][BP_MAXW][8]; returns the number
-// of launches so far (resets the count when reset != 0)
-extern "C" int bh_bloom_phases_read(uint32_t* hdr, uint32_t* rec, int reset) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(hdr, HIP_SYMBOL(g_bp_hdr), sizeof(uint32_t) * BP_SLOTS * 4) != hipSuccess) return -1;
-    if (rec && hipMemcpyFromSymbol(rec, HIP_SYMBOL(g_bp_rec), sizeof(uint32_t) * BP_SLOTS * BP_MAXW * 8) != hipSuccess)
-        return -1;
-    const int n = (int)g_bp_next;
-    if (reset) g_bp_next = 0;
-    return n;
-}
-extern "C" uint32_t bh_bloom_phases_geometry(void) { return BP_SLOTS << 24 | BP_MAXW; }
-#endif
 
 // ---- remixes of the chain at any proven-identity size (general fused schedule) ----------------------
 // On frames whose same-size passes are identities on stored texels (the host's same_size_identity, e.g.
@@ -1450,9 +1190,6 @@ __global__ void __launch_bounds__(256) remix2_plan_kernel(Tables tb, CTex col, C
 // listed ones).  EPI_Y: out = remix(S(A), S(B)) (A = X, B = U1); EPI_FINAL: out = remix(S(A), S(F)),
 // F = q(remix(S(B), S(C))) (A = col, B = Y, C = B-texture) -- remix_plan_kernel's / remix2_plan_kernel's
 // per-pixel arithmetic.
-#ifndef BH_BLOOM_FIXUP_GATHER
-#define BH_BLOOM_FIXUP_GATHER 1  // 0 (A/B): the per-sample form below
-#endif
 // A same-size sample's texel words, gathered before the block stages its tables: (x0, y0), (x1, y0),
 // (x0, y1), (x1, y1).  A word whose weight is 0 is not read (0 instead): it enters sample_same's lerp as
 // t * 0 == +0 for any finite decoded t >= 0, so finish_same gives sample_same's bits.
@@ -1512,13 +1249,6 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
                                                            uint32_t n_rows, Tex out, const uint4* __restrict__ rec,
                                                            const uint32_t* __restrict__ strips, uint32_t strip_w) {
     __shared__ Lds L;
-#if BH_BLOOM_PHASES
-    // phases: the list entry and plan entries used, the tables staged, the pixel computed and stored
-    uint32_t bp[5] = {};
-    const uint32_t bp_real0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
-    const uint32_t bp_wave = blockIdx.x * 4u + (threadIdx.x >> 6);
-#endif
-    BP_T(0);
     const uint32_t W = out.w, H = out.h;
     const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x, nc = (uint64_t)n_cols * H;
     uint32_t x = 0u, y = 0u, qx = 0u;  // qx: a column lane's strip column (strips)
@@ -1587,10 +1317,6 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         }
     }
     if (i >= nc && cx.y != 0u) live = false;  // an inexact column: its pixels are the first part's
-#if BH_BLOOM_PHASES
-    asm volatile("" ::"v"(cx.x), "v"(cy.x));
-#endif
-    BP_T(1);
     const bool sl = EPI == EPI_FINAL && strips != nullptr && rec != nullptr && i < nc;  // a column lane on strips
     auto img = [&](CTex T, uint32_t im) -> SrcImg {
         if (sl) return {strips + (size_t)im * strip_w * H, 1u, H, strip_w - 1u, (int32_t)x - (int32_t)qx};
@@ -1600,8 +1326,6 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
     if constexpr (EPI == EPI_Y) {
         const SameWords b = gather_same(B, cx, cy);
         load_tables(tb, L);
-        BP_T(2);
-        BP_T(3);
         if (live) out.px[y * W + x] = enc(L, remix(finish_same(L, a), finish_same(L, b)));
     } else {
         auto pick = [&](uint32_t u, uint32_t c, const uint2(&P)[3], uint32_t base) -> uint2 {
@@ -1632,13 +1356,7 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
             fcw[3] = gather_img(IC, px1, py1);
         }
         load_tables(tb, L);
-        BP_T(2);
         if (live) {
-#if BH_BLOOM_PHASES
-            // the texel words arrived (their first use)
-            asm volatile("" ::"v"(a.t[0]), "v"(fbw[0].t[0]), "v"(fcw[0].t[0]));
-#endif
-            BP_T(3);
             auto F = [&](int k) { return quant(L, remix(finish_same(L, fbw[k]), finish_same(L, fcw[k]))); };
             const F4 z{0.0f, 0.0f, 0.0f, 0.0f};
             const F4 f0 = F(0), f1 = ex ? F(1) : z, f2 = ey ? F(2) : z, f3 = ex && ey ? F(3) : z;
@@ -1647,10 +1365,6 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
             out.px[y * W + x] = enc(L, remix(finish_same(L, a), f));
         }
     }
-#if BH_BLOOM_PHASES
-    BP_T(4);
-    bp_record(bp, bp_real0, bp_wave, 0u, EPI, gridDim.x, W);
-#endif
 }
 
 template <uint32_t EPI>
@@ -1852,10 +1566,7 @@ constexpr int FP_YQ = 40;  // 32 + the taps' reach (38 at 4096x2048)
 // SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE 0.34 at strides 40 and 41).  With it a quad row is 2 FS_YQ + 1
 // float4 further, odd: the next quad row reads the odd slots.  (p makes the quad's first texel row even in
 // the shifted index, so a tap's row offsets are launch constants: yq_rowoff(d) = d FS_YQ + floor(d / 2).)
-#ifndef BH_BLOOM_FS_YQ
-#define BH_BLOOM_FS_YQ 40
-#endif
-constexpr int FS_YQ = BH_BLOOM_FS_YQ;
+constexpr int FS_YQ = 40;
 __host__ __device__ constexpr int32_t yq_rowoff(int32_t d) { return d * FS_YQ + (d >= 0 ? d / 2 : -((1 - d) / 2)); }
 template <int HX, int HY>
 __device__ __forceinline__ void yquad_tap(const float4* T, int32_t d1, int i, F4 (&s)[2][2]) {
@@ -1893,8 +1604,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
         const int32_t wm = (int32_t)X.w - 1, hm = (int32_t)X.h - 1;
         constexpr int R = (FP_YQ * FP_YQ + 255) / 256;
         uint32_t raw[R];
-#if BH_BLOOM_ROWLOAD
-        // rows of FP_YQ elements (a constant split, see up_sepq_kernel's BH_BLOOM_ROWLOAD); the elements past the
+        // rows of FP_YQ elements (a constant split, see up_sepq_kernel's row-wise staging); the elements past the
         // footprint load clamped texels and store into the spare slot
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1911,22 +1621,6 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
             const F4 d = dec(L, raw[r]);
             tile[v ? ly * FS_YQ + lx + ((ly + p) >> 1) : FP_YQ * FS_YQ + FP_YQ / 2] = make_float4(d.r, d.g, d.b, d.a);
         }
-#else
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
-            if (ly < ny) raw[r] = X.px[(uint32_t)clampi(y0 + ly, 0, hm) * X.w + clampi(x0 + lx, 0, wm)];
-        }
-        load_tables(tb, L);  // after the footprint's loads are issued: both round trips overlap
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int32_t i = (int32_t)threadIdx.x + r * 256, ly = i / nx, lx = i - ly * nx;
-            if (ly < ny) {
-                const F4 d = dec(L, raw[r]);
-                tile[ly * FS_YQ + lx + ((ly + p) >> 1)] = make_float4(d.r, d.g, d.b, d.a);
-            }
-        }
-#endif
     }
     __syncthreads();
     const uint32_t x = bx + 2u * (threadIdx.x & 15u), y = by + 2u * (threadIdx.x >> 4);  // the quad's corner
@@ -2002,7 +1696,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
     const Taps k(rx, ry);
     const bool in = x < out.w && y < out.h;
     const uint32_t i = (uint32_t)y * out.w + x;
-#if BH_BLOOM_OWN_LATE
     // the pixel's own Y and col texels: loaded after the footprint is staged (see up_sepq_kernel's LATE), in
     // flight during the taps; the block's opaque test covers the footprint, the wave's own texels pick the
     // last stage's form
@@ -2025,20 +1718,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) b
             else fin(std::false_type{});
         },
         true);
-#else
-    // the pixel's own Y and col texels: loaded before the footprint and the tables, used last
-    const uint32_t yv = in ? Y.px[i] : 0u, cv = in ? col.px[i] : 0u;
-    with_source<FP_FINAL, true, STD>(
-        tb, U0, L, tile, k, out.w, out.h, Rw, Rh, P,
-        [&](const auto& src) {
-            constexpr bool A1 = std::decay_t<decltype(src)>::kA1;
-            if (!in) return;
-            const F4 b3 = quant<A1>(L, up8(src, k, texcoord(x, Rw), texcoord(y, Rh), point));
-            const F4 z = quant<A1>(L, remix(dec<A1>(L, yv), b3));
-            out.px[i] = enc(L, remix(dec<A1>(L, cv), z));
-        },
-        !in || (min(yv, cv) >= 0xFF000000u));
-#endif
 }
 
 // ---- persistent blocks (standard plans) ------------------------------------------------------------
@@ -2255,10 +1934,7 @@ constexpr int FP_UPQ = 28;  // footprint of 16 texels + the taps' reach (24 at 4
 // one texel per output quad), 16 consecutive slots per quad row, and the lane groups take two quad rows
 // (see FS_YQ): with 28 the second row overlapped the first's slots (bank conflicts 0.42 of LDS-active
 // cycles), with 32 it lands on the same slots of the next 64 banks (0.01)
-#ifndef BH_BLOOM_FS_UPQ
-#define BH_BLOOM_FS_UPQ 32
-#endif
-constexpr int FS_UPQ = BH_BLOOM_FS_UPQ;
+constexpr int FS_UPQ = 32;
 template <int STD>
 __global__ void BLOOM_BOUNDS up2_kernel(Tables tb, CTex a, uint32_t rx, uint32_t ry, uint32_t point, Up2Plan P,
                                         Tex out) {
@@ -2936,7 +2612,7 @@ static SepForm sep_form(int ext, uint32_t ow, uint32_t oh) {
         f.quad = true;
         f.FP = q;
         f.raw = q == 60 || (q == 28 && (raw_mask & 1u)) || (q == 40 && (raw_mask & 2u));
-        f.FS = f.raw ? (q == 60 ? BH_BLOOM_SEPQ_FS60 : 48) : (q == 28 ? 32 : 40);
+        f.FS = f.raw ? (q == 60 ? SEPQ_FS60 : 48) : (q == 28 ? 32 : 40);
     } else if (one != 0) {
         f.FP = one;
         f.raw = one == 44;
@@ -3123,14 +2799,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     const dim3 g = grid_for(ow, oh), gq((ow + (org & 0xFFFFu) + 31u) / 32u, (oh + (org >> 16) + 31u) / 32u);
 #define BH_SEP(FP, E, RAW) \
     hipLaunchKernelGGL((up_sep_kernel<FP, E, RAW>), g, dim3(256), 0, s, tb, A, rx, ry, P, O, O0, O1, S, X)
-#if BH_BLOOM_PHASES
-#define BH_BP_SLOT() bp_next_slot(s)
-#else
-#define BH_BP_SLOT() (void)0
-#endif
 #define BH_SEPQ(FP, E, RAW, FS, FX)                                                                                  \
     do {                                                                                                             \
-        BH_BP_SLOT();                                                                                                \
         hipLaunchKernelGGL((up_sepq_kernel<FP, E, RAW, FS, FX>), gq, dim3(256),                                      \
                            sepq_cap_pad(reinterpret_cast<const void*>(&up_sepq_kernel<FP, E, RAW, FS, FX>), E), s, tb, A, \
                            rx, ry, P, O, O0, O1, S, X, org, STC, strips, strip_w);                                   \
@@ -3152,7 +2822,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     else if (f.quad && f.FP == 40 && f.raw) BH_EPI(BH_Q, 40, true, 48);
     else if (f.quad && f.FP == 28) BH_EPI(BH_Q, 28, false, 32);
     else if (f.quad && f.FP == 40) BH_EPI(BH_Q, 40, false, 40);
-    else if (f.quad && f.FP == 60) BH_EPI(BH_Q, 60, true, BH_BLOOM_SEPQ_FS60);
+    else if (f.quad && f.FP == 60) BH_EPI(BH_Q, 60, true, SEPQ_FS60);
     else if (f.FP == 24) BH_EPI(BH_1, 24, false);
     else if (f.FP == 44) BH_EPI(BH_1, 44, true);
     else return (int)hipErrorInvalidValue;
@@ -3204,20 +2874,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_fixup(const
     const Tables tb{lut, enc, buckets, codes};
     const dim3 g0((uint32_t)((n + 255u) / 256u));
     const uint2* S = reinterpret_cast<const uint2*>(same);
-    static const bool per_sample = !BH_BLOOM_FIXUP_GATHER || std::getenv("BH_BLOOM_FIXUP_SAMPLE") != nullptr;  // A/B
+    static const bool per_sample = std::getenv("BH_BLOOM_FIXUP_SAMPLE") != nullptr;  // A/B: the per-sample form
     const uint4* R = no_rec ? nullptr : reinterpret_cast<const uint4*>(recs);
-#if BH_BLOOM_PHASES
-    if (!per_sample) bp_next_slot(s);
-    // timing only (wrong pixels): the fix-up's row part alone, or its column part alone
-    static const int part = std::getenv("BH_BLOOM_PHASES_FIXUP_PART") ? std::atoi(std::getenv("BH_BLOOM_PHASES_FIXUP_PART")) : 0;
-    if (part == 1) n_cols = 0u;
-    if (part == 2) n_rows = 0u;
-    const dim3 gp((uint32_t)(((uint64_t)n_cols * h + (uint64_t)n_rows * w + 255u) / 256u));
-    if (part != 0 && gp.x == 0u) return 0;
-    const dim3 g = part ? gp : g0;
-#else
     const dim3 g = g0;
-#endif
     if (!per_sample && epi == EPI_Y)
         hipLaunchKernelGGL(fixup_gather_kernel<EPI_Y>, g, dim3(256), 0, s, tb, CTex{a, w, h}, CTex{b, w, h},
                            CTex{b, w, h}, S, list, n_cols, n_rows, Tex{out, w, h}, R, nullptr, 0u);

@@ -40,9 +40,9 @@ struct MarchArgs {
     uint32_t blackout_eh;
     uint32_t skip_sdf;         // the root-free step may run (bh_march.hpp, sdf_skip: dtm > 0, 0 < rs <= 8)
     float far_r2;              // r^2 beyond which a step needs no SDF argument (bh_host.cpp sdf_far_r2; +inf: off)
-    // per-term radii (bh_host.cpp sdf_term_radii): the photon-sphere term clears for r^2 >= ps_r2, the markers'
-    // for r^2 >= mo_r2 or r^2 <= mi_r2 (+inf / -1: off)
-    float ps_r2, mo_r2, mi_r2;
+    // unused: the per-term radii of a root-free-step variant measured slower and removed;
+    // kept so that the kernel argument layout -- and the kernels' machine code -- stay those measured
+    float reserved_[3];
     // frame
     uint32_t width, height, max_iters, scene_flags;
     uint32_t format, layout;

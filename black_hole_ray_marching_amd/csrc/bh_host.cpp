@@ -1350,26 +1350,6 @@ static float sdf_far_r2(float rs, float dtm) {
     return std::nextafter((float)(R * R), INFINITY);
 }
 
-// The same bound term by term (bh_march.hpp, BH_SDF_RADII): a lane at distance R from the origin is at least
-// R - 1.5 rs - 0.075 from the photon sphere's surface and at least R - 10 sqrt2 - 0.5 (outside the markers'
-// centre circle) or 10 sqrt2 - R - 0.5 (inside it) from the markers'.  Beyond 1.01 R0 (outer radii, R0 where
-// the term meets 1.1251 dtm R + 0.003) or within 0.99 R0 (the inner radius, R0 where 10 sqrt2 - R - 0.503
-// meets 1.1251 dtm R) that term exceeds the root-free test's threshold by >= 0.01 R0 (1 -+ 1.1251 dtm) > 0.001,
-// so it clears (the per-term lemma, sdf_term_slacks) without its argument being formed; r^2 is compared as
-// computed, as for sdf_far_r2.  Off: +inf (outer), -1 (inner).
-static void sdf_term_radii(float rs, float dtm, float* ps_r2, float* mo_r2, float* mi_r2) {
-    *ps_r2 = INFINITY; *mo_r2 = INFINITY; *mi_r2 = -1.0f;
-    if (!(rs > 0.0f) || !(dtm > 0.0f)) return;
-    const double k = 1.1251 * (double)dtm, out = 1.0 - k, m = 10.0 * std::sqrt(2.0);
-    if (out > 0.01) {
-        const double Rp = 1.01 * (1.5 * rs + 0.075 + 0.003) / out, Rm = 1.01 * (m + 0.5 + 0.003) / out;
-        *ps_r2 = std::nextafter((float)(Rp * Rp), INFINITY);
-        *mo_r2 = std::nextafter((float)(Rm * Rm), INFINITY);
-    }
-    const double Ri = 0.99 * (m - 0.5 - 0.003) / (1.0 + k);
-    *mi_r2 = std::nextafter((float)(Ri * Ri), 0.0f);
-}
-
 // A/B switch (diagnostics): BH_NO_SDF_SKIP set => every step evaluates its SDF roots (bh_march.hpp, sdf_skip)
 static bool sdf_skip_disabled() {
     static const bool off = std::getenv("BH_NO_SDF_SKIP") != nullptr;
@@ -1416,8 +1396,6 @@ int bh_render_frames(bh_ctx* c, uint32_t n_frames, const bh_camera_uniform* cams
     a.blackout_eh = U->blackout_eh;
     a.skip_sdf = (U->delta_time_mult > 0.0f && U->rs > 0.0f && U->rs <= 8.0f && !sdf_skip_disabled()) ? 1u : 0u;
     a.far_r2 = a.skip_sdf ? sdf_far_r2(U->rs, U->delta_time_mult) : INFINITY;
-    a.ps_r2 = INFINITY; a.mo_r2 = INFINITY; a.mi_r2 = -1.0f;
-    if (a.skip_sdf) sdf_term_radii(U->rs, U->delta_time_mult, &a.ps_r2, &a.mo_r2, &a.mi_r2);
     a.width = d->width; a.height = d->height; a.max_iters = d->max_iters; a.scene_flags = d->scene_flags;
     a.format = d->format; a.layout = d->layout;
     a.shard_index = d->shard_index; a.shard_count = d->shard_count;
@@ -1608,17 +1586,10 @@ int bh_partition_map(uint32_t width, uint32_t height, uint32_t S, const uint32_t
     const std::vector<uint32_t> owner = partition_owners(S, weights);
     if (owner.empty()) return bad_arg(__func__, __LINE__);
     const uint32_t M = (uint32_t)owner.size(), tx_n = (width + 7u) / 8u, ty_n = (height + 7u) / 8u;
-    // A/B only (BH_PARTITION_SB=s, tools/probe_rank0.py): the interleave over s x s tile super-blocks instead of
-    // single tiles (a shard's consecutive tiles then neighbour each other in the frame)
-    static const uint32_t sb = [] {
-        const char* e = std::getenv("BH_PARTITION_SB");
-        const unsigned long v = e ? std::strtoul(e, nullptr, 10) : 1ul;
-        return (uint32_t)(v >= 1ul && v <= 64ul ? v : 1ul);
-    }();
     std::vector<uint32_t> next(S, 0);
     for (uint32_t ty = 0; ty < ty_n; ++ty)
         for (uint32_t tx = 0; tx < tx_n; ++tx) {
-            const uint32_t k = owner[(tx / sb + 3ull * (ty / sb)) % M];
+            const uint32_t k = owner[(tx + 3ull * ty) % M];
             const size_t t = (size_t)ty * tx_n + tx;
             if (owner_out) owner_out[t] = k;
             if (index_out) index_out[t] = next[k];

@@ -22,12 +22,9 @@
 #ifndef BH_FAST
 #error "define BH_FAST to 0 or 1"
 #endif
-// rd_derivative's reciprocal from the root's own v_rsq (crm::rcp_from_rsq) instead of a v_rcp of Q: four
+// (rd_derivative's reciprocal from the root's own v_rsq, crm::rcp_from_rsq, instead of a v_rcp of Q: four
 // fewer transcendentals per RK step, but NOT exact -- 60 (numerator, Q) pairs, at Q significands next to
-// 2 (e.g. n = 1, Q = 0x2cffffff), round the other way (selftest op 13) -- so it stays off (A/B only)
-#ifndef BH_RCP_SEED
-#define BH_RCP_SEED 0
-#endif
+// 2 (e.g. n = 1, Q = 0x2cffffff), round the other way (selftest op 13) -- so the march keeps rcp_refined.)
 
 namespace bh {
 namespace BH_NS {
@@ -394,8 +391,7 @@ struct XOps {
     // rd_derivative (:125-127): (s * p) / pow(dot(p,p), 2.5), pow(q, 2.5) := (q*q)*sqrt(q);
     // q and sqrt(q) passed in when already known (k1: q = r^2, sqrt(q) = r).
     // K = 1..4: the RK stage (k1's numerators may be zeros, see above)
-    // y: v_rsq(q) from the root of q (sqrt_y), the seed of RN(1/Q) (crm::rcp_from_rsq; BH_RCP_SEED 0:
-    // a v_rcp of Q instead)
+    // y: v_rsq(q) from the root of q (sqrt_y); unused (a v_rcp of Q seeds RN(1/Q), see the top of the file)
     template <int K>
     __device__ __forceinline__ v3 accel_qs(v3 p, float s, float q, float sq, float y) {
         const float Q = (q * q) * sq;
@@ -405,7 +401,7 @@ struct XOps {
             if constexpr (K == 1) kmin = crm::kmin3(crm::key(nx), crm::key(ny), crm::key(nz));
             else if constexpr (K == 2) amin = absmin3(nx, ny, nz);
             else amin = absmin3(amin, nx, ny, nz);
-            const crm::Rcp R = BH_RCP_SEED ? crm::rcp_from_rsq(Q, y) : crm::rcp_refined(Q);
+            const crm::Rcp R = crm::rcp_refined(Q);
             return mk(crm::div_core(nx, R), crm::div_core(ny, R), crm::div_core(nz, R));
         } else {
             return mk(nx / Q, ny / Q, nz / Q);
@@ -421,18 +417,6 @@ struct XOps {
     __device__ __forceinline__ float length(v3 p) { return sqrt(dot(p, p)); }
     // sdf (:119-123); markers: min(sqrt(qi) - 0.5) == sqrt(min qi) - 0.5 exactly (monotone ops)
     // sdf_args: the arguments of its two roots (rho^2, the markers' qm) and y*y; sdf_from: the rest
-    // sdf_args in two parts: the disc's (rho^2, y*y) and the markers' (qm), the same operations
-    __device__ __forceinline__ void sdf_args_disc(v3 p, float& rho2, float& yy) {
-        rho2 = p.x * p.x + p.z * p.z;
-        yy = p.y * p.y;
-    }
-    __device__ __forceinline__ void sdf_args_mark(v3 p, float yy, float& qm) {
-        const float xx = p.x * p.x;
-        const float dz = -10.0f - p.z, zz = dz * dz;
-        const float ty = 10.0f - fabsf(p.y), tx = 10.0f - fabsf(p.x);
-        const float qy = (xx + ty * ty) + zz, qx = (tx * tx + yy) + zz;
-        qm = fminf(qy, qx);
-    }
     __device__ __forceinline__ void sdf_args(v3 p, float& rho2, float& yy, float& qm) {
         rho2 = p.x * p.x + p.z * p.z;
         // The four sphere arguments are q1,2 = (xx + (+-10 - y)^2) + zz and q3,4 = ((+-10 - x)^2 + yy)
@@ -494,25 +478,9 @@ constexpr float R2_GT1 = 0x1.000002p0f;
 
 __device__ __forceinline__ bool fate_before_rk(uint32_t fate) { return fate >= BH_FATE_SURFACE; }
 
-#ifndef BH_SDF_SKIP
-#define BH_SDF_SKIP 1
-#endif
-#ifndef BH_SKIP_STICKY
-#define BH_SKIP_STICKY 0
-#endif
-#ifndef BH_SDF_TERMS
-#define BH_SDF_TERMS 1  // the root-free test term by term on the wave-steps that fail it as a whole
-#endif
-#ifndef BH_SDF_TERMS3
-// A/B: the per-term ballots also decide the all-terms test (no min over the slacks): measured equal,
-// 0.5189 vs 0.5193 ms (profiles/r05/sdf_terms3/), so off
-#define BH_SDF_TERMS3 0
-#endif
-#ifndef BH_SDF_RADII
-// terms cleared by the lane's radius alone, their arguments not formed (A/B, off: both radii 0.5217 ->
-// 0.5261 ms, the photon sphere's alone 0.5217 -> 0.5217; profiles/r05/sdf_radii/)
-#define BH_SDF_RADII 0
-#endif
+// (Measured and not kept, DESIGN.md §5: a "sticky" root-free test that skips the test after a step that took
+// the roots; per-term ballots deciding the all-terms test too, 0.5189 vs 0.5193 ms, profiles/r05/sdf_terms3/;
+// terms cleared by the lane's radius alone, 0.5217 -> 0.5261 ms, profiles/r05/sdf_radii/, §5 item 29.)
 #ifdef BH_DIAG_SLOW
 __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wave_steps;
 // one count per wave: the lowest active lane adds (a global atomic: a vector memory op)
@@ -553,28 +521,22 @@ __device__ uint32_t g_diag_skip_wave_steps, g_diag_all_wave_steps, g_diag_far_wa
 // In the exact build's core pass a wrong r (r2 outside the root core's domain) also raises the k1
 // division guard, so that step re-runs in IEEE ops, where the proof holds as written.
 // tests/test_skip.py checks the implication on adversarial samples of the step's float32 arithmetic.
-// The same test term by term (BH_SDF_TERMS): each term's slack >= 0 alone proves that term's distance
+// The same test term by term: each term's slack >= 0 alone proves that term's distance
 // >= T (1 - 2^-17.6) by the argument above, so a term whose slack holds can be left out of dist (taken as
 // +inf): if it was the minimum, every other term is at least as large and still gives RN(0.9 dist) >= dtr;
 // its surface test could not fire; and fminf drops a NaN term exactly as it drops +inf.
 // tests/test_skip.py::test_per_term_skip_keeps_dt_and_surface checks every subset of cleared terms.
 struct SdfSlack { float disc, mark, ps; };
-// m_on / ps_on false: that term already cleared by the lane radii (BH_SDF_RADII), its argument not formed
 __device__ __forceinline__ SdfSlack sdf_term_slacks(const MarchArgs& a, uint32_t flags, float dtr, float rho2, float yy,
-                                                   float qm, float qps, bool m_on = true, bool ps_on = true) {
+                                                   float qm, float qps) {
     const float T = __builtin_fmaf(dtr, 1.125f, 0.002f);
     const float u6 = T + 6.0f * a.rs, uy = T + 0.02f;
     // v - u^2 rounded once (fma): its sign is the sign of the exact v - u*u
     float disc = fmaxf(__builtin_fmaf(-u6, u6, rho2), __builtin_fmaf(-uy, uy, yy));
-    float mark = __builtin_inff(), ps = __builtin_inff();
-    if (m_on) {
-        const float um = T + 0.5f;
-        mark = __builtin_fmaf(-um, um, qm);
-    }
-    if (ps_on) {
-        const float up = T + 0.075f;
-        ps = __builtin_fmaf(-up, up, qps);
-    }
+    const float um = T + 0.5f;
+    float mark = __builtin_fmaf(-um, um, qm);
+    const float up = T + 0.075f;
+    float ps = __builtin_fmaf(-up, up, qps);
     if (!(flags & BH_SCENE_DISC)) disc = __builtin_inff();
     if (!(flags & BH_SCENE_MARKERS)) mark = __builtin_inff();
     return {disc, mark, ps};
@@ -586,7 +548,7 @@ __device__ __forceinline__ float sdf_skip_slack(const SdfSlack& t) { return fmin
 // cap test is a wave-uniform (scalar) compare.
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
-                                        uint32_t& fate, uint32_t it = 0u, uint32_t* sk = nullptr) {
+                                        uint32_t& fate, uint32_t it = 0u) {
     constexpr uint32_t SFS = sf_scene(SF);
     constexpr bool CO = sf_cam_out(SF);
     const uint32_t scene_flags = (SFS == SF_DYN) ? a.scene_flags : SFS;
@@ -622,7 +584,7 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     const float dtr = a.dtm * r;                                       // :307-310's second operand
     float dt;
     bool surface = false;
-#if !BH_FAST && BH_SDF_SKIP
+#if !BH_FAST
     // Far field: a lane with a.far_r2 <= r^2 <= FLT_MAX (the host's sdf_far_r2, +inf when off) is so far
     // from the disc, the markers and the photon sphere that every distance term exceeds the root-free
     // test's threshold by construction (proof at sdf_far_r2, bh_host.cpp): when every lane that stays is
@@ -630,7 +592,6 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // distance term may stay finite.)
     if (BRANCHY && __builtin_amdgcn_ballot_w64(!(r2 >= a.far_r2 && r2 <= 0x1.fffffep127f) & !blackout) == 0ull) {
         BH_DIAG_FAR_COUNT();
-        if (BH_SKIP_STICKY && sk) *sk = 0u;
         if (blackout) {
             fate = (uint32_t)BH_FATE_BLACKOUT;
             return true;
@@ -639,62 +600,23 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     } else
 #endif
     {
-#if !BH_FAST && BH_SDF_SKIP && BH_SDF_RADII
-    // Per-term radii (sdf_term_radii, bh_host.cpp): when every lane that stays lies beyond the photon sphere's
-    // radius, or outside the markers' band, that term clears without its argument (the wave forms no qps,
-    // no qm).  96 % of the headline's non-far wave-steps clear the photon sphere so, 20 % the markers
-    // (tools/skip_sim.py).
-    bool ps_on = true, m_on = true;
-    if constexpr (BRANCHY) {
-        const bool fin = r2 <= 0x1.fffffep127f;
-        ps_on = __builtin_amdgcn_ballot_w64(!((r2 >= a.ps_r2) & fin) & !blackout) != 0ull;
-        if (BH_SDF_RADII != 2)  // 2 (A/B): the photon sphere's radius only
-            m_on = __builtin_amdgcn_ballot_w64(!(((r2 >= a.mo_r2) | (r2 <= a.mi_r2)) & fin) & !blackout) != 0ull;
-    }
-    X.sdf_args_disc(ro, rho2, yy);
-    qm = 0.0f;
-    if (m_on) X.sdf_args_mark(ro, yy, qm);
-#else
     X.sdf_args(ro, rho2, yy, qm);                                      // the SDF roots' arguments
-    constexpr bool ps_on = true, m_on = true;
-#endif
-#if !BH_FAST && BH_SDF_SKIP
+#if !BH_FAST
     // Root-free step (BRANCHY): dt = min(0.9 dist, dtm r) needs dist only where it could fall below
     // dtm r / 0.9, and the surface test only below MIN_DIST.  sdf_skip decides "dt == dtm r, no surface"
     // from the squared arguments; when it holds on every live lane (blackout lanes leave either way)
     // the wave skips the three roots, their guards and the distance arithmetic.  Same bits: see sdf_skip.
     // The photon-sphere argument (:294) is formed before the exits for the test.
     if constexpr (BRANCHY) {
-        float qps = 0.0f;
-        if (ps_on) {
-            const v3 dc = sub(f.cps, ro);
-            qps = dot(dc, dc);
-        }
+        const v3 dc = sub(f.cps, ro);
+        const float qps = dot(dc, dc);
         // lanes that need the roots: slack < 0 or NaN, except those that leave by the blackout exit.  (The
         // blackout select becomes a branch around the test.  Taking the lane mask straight from the compare,
         // llvm.amdgcn.fcmp, and masking the blackout lanes as integers is 4 VALU fewer and measured 0.9 %
         // slower: profiles/r04/ab_skip_forms/.)
-        // BH_SKIP_STICKY (A/B): after a tested step that took the roots, the next step takes them without
-        // the test (after a slow step only ~24 % of the next are fast: tools/skip_sim.py), then tests again
-        const bool test = !BH_SKIP_STICKY || !sk || *sk == 0u;
-        bool fast = false;
-        SdfSlack terms{0.0f, 0.0f, 0.0f};
-        bool nd = true, nm = true, np = true;  // BH_SDF_TERMS3: which roots some staying lane needs
-        if (test) {
-            terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps, m_on, ps_on);
-            if (BH_SDF_TERMS3 && BH_SDF_TERMS) {
-                // the three per-term ballots decide both: fast when no term is needed
-                const bool stay = !blackout;
-                nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
-                nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
-                np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
-                fast = a.skip_sdf != 0u && !(nd | nm | np);
-            } else {
-                const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
-                fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
-            }
-        }
-        if (BH_SKIP_STICKY && sk) *sk = (test && !fast) ? 1u : 0u;
+        const SdfSlack terms = sdf_term_slacks(a, scene_flags, dtr, rho2, yy, qm, qps);
+        const float slack = blackout ? __builtin_inff() : sdf_skip_slack(terms);
+        const bool fast = a.skip_sdf != 0u && __builtin_amdgcn_ballot_w64(!(slack >= 0.0f)) == 0ull;
         if (fast) {
             BH_DIAG_SKIP_COUNT();
             if (blackout) {
@@ -702,16 +624,14 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
                 return true;
             }
             dt = dtr;
-        } else if (BH_SDF_TERMS && test && a.skip_sdf != 0u) {
+        } else if (a.skip_sdf != 0u) {
             // per term: a root only where some lane that stays needs it (sdf_term_slacks); where the disc
             // and markers both clear, the photon sphere alone keeps the wave here (about 98 % of these
             // wave-steps clear it, and 80 % one of the other two: tools/skip_sim.py)
-            if (!BH_SDF_TERMS3) {
-                const bool stay = !blackout;
-                nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
-                nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
-                np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
-            }
+            const bool stay = !blackout;
+            const bool nd = __builtin_amdgcn_ballot_w64(stay & !(terms.disc >= 0.0f)) != 0ull;
+            const bool nm = __builtin_amdgcn_ballot_w64(stay & !(terms.mark >= 0.0f)) != 0ull;
+            const bool np = __builtin_amdgcn_ballot_w64(stay & !(terms.ps >= 0.0f)) != 0ull;
             float dv = __builtin_inff(), mv = __builtin_inff();
             if (nd) {
                 dv = X.disc_from(ro, a.rs, rho2);
@@ -884,7 +804,7 @@ __device__ __forceinline__ p3 paccel_qs(p3 p, float s, float q, float sq, float 
     if constexpr (K == 1) G.kmin = crm::kmin3(crm::key(n.xy.x), crm::key(n.xy.y), crm::key(n.z));
     else if constexpr (K == 2) G.amin = XOps<true>::absmin3(n.xy.x, n.xy.y, n.z);
     else G.amin = XOps<true>::absmin3(G.amin, n.xy.x, n.xy.y, n.z);
-    return pdiv(n, BH_RCP_SEED ? crm::rcp_from_rsq(Q, y) : crm::rcp_refined(Q));
+    return pdiv(n, crm::rcp_refined(Q));
 }
 template <int K>
 __device__ __forceinline__ p3 paccel(p3 p, float s, PkGuard& G) {
@@ -980,10 +900,9 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
 // fates before the RK update), with the exact mode's guarded fast path and its rare IEEE re-run.
 template <uint32_t SF = SF_DYN, bool UNI = false>
 __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out,
-                                              uint32_t& fate, uint32_t it = 0u, uint32_t* sk = nullptr) {
+                                              uint32_t& fate, uint32_t it = 0u) {
 #if BH_FAST
     FOps X;
-    (void)sk;
     return step_bf<true, FOps, SF, UNI>(a, f, in, out, X, fate, it);
 #else
     XOps<true> X;
@@ -991,7 +910,7 @@ __device__ __forceinline__ bool march_step_io(const MarchArgs& a, const Frame& f
     if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
         atomicAdd(&g_diag_all_wave_steps, 1u);
 #endif
-    bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it, sk);
+    bool done = step_bf<true, XOps<true>, SF, UNI>(a, f, in, out, X, fate, it);
 #ifdef BH_DIAG_SLOW
     const uint64_t badm = __builtin_amdgcn_ballot_w64(X.bad);
     if (badm != 0ull && (threadIdx.x & 63u) == 0u) {
@@ -1334,15 +1253,7 @@ constexpr uint32_t PRIO_ITERS = 48;
 // slots on the CU; no workgroup barrier beyond the wave's own table load.  1 vs 4 waves (interleaved
 // A/B, profiles/r02d/ab_wg/): headline -0.6 %, 1920x1080 -0.8 %, cap 1000 -1.0 %, one frame per
 // launch -1.4 %, 256x256 cap 64 +0.6 % (noise level).  32 such workgroups per CU fill its 160 KiB.
-#ifndef BH_WG_WAVES
-#define BH_WG_WAVES 1u
-#endif
-#ifndef BH_SPW
-#define BH_SPW 1u
-#endif
-#ifndef BH_SPW_STRIDED
-#define BH_SPW_STRIDED 0
-#endif
+constexpr uint32_t WG_WAVES = 1u;
 
 // ---- schedule BH_SCHED_TILE: one wave64 = one 8x8 tile (default) ---------------------------------
 // Dispatch slot -> tile through `order` (previous frame's per-tile cost, expensive tiles first) or
@@ -1385,7 +1296,7 @@ __device__ __forceinline__ uint32_t state_hash(const RayState& st) {
 // The workgroup's history areas (4 KiB per wave: 8 waves per SIMD still fit, 5 KiB x 32).
 template <int>
 __device__ __forceinline__ HistLds* hist_lds() {
-    __shared__ HistLds hist[BH_WG_WAVES];
+    __shared__ HistLds hist[WG_WAVES];
     return hist;
 }
 
@@ -1394,10 +1305,7 @@ __device__ __forceinline__ HistLds* hist_lds() {
 // Cycles are looked for until iteration CYCLE_ITERS_END only: the ones found start by iteration ~50
 // (median 30); the rays still marching after that crawl or orbit without repeating, and
 // stopping the search never changes a result -- the loop then just runs to its normative end.
-#ifndef BH_CYCLE_ITERS_END
-#define BH_CYCLE_ITERS_END 192u
-#endif
-constexpr uint32_t CYCLE_ITERS_END = BH_CYCLE_ITERS_END;
+constexpr uint32_t CYCLE_ITERS_END = 192u;
 template <uint32_t SF>
 __device__ __forceinline__ uint32_t march_cycles(const MarchArgs& a, const Frame& f, RayState& st, uint32_t& steps,
                                                  HistLds& H, uint32_t lane) {
@@ -1466,7 +1374,6 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
     // 0.842 -> 0.837 ms headline, 0.99 -> 0.92 ms at cap 1000, A/B r01.)
     RayState sb = st;
     bool alive = true;
-    uint32_t sk = 0u;  // BH_SKIP_STICKY: the root-free test's state (step_bf)
     // TRIP_PAIRS ping-pong pairs per trip of the wave-uniform loop (1 / 2 / 3 pairs: 0.689 / 0.688
     // / 0.686 ms, A/B r01): fewer trip tests and their ballot materialisation per step.
     constexpr uint32_t TRIP_PAIRS = 3;
@@ -1475,13 +1382,13 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
 #pragma unroll
         for (uint32_t j = 0; j < TRIP_PAIRS; ++j) {
             if (alive) {
-                if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j, &sk)) {
+                if (march_step_io<SF, true>(a, f, st, sb, fate, it + 2u * j)) {
                     alive = false;
                     if (fate_before_rk(fate)) sb.n_rk = 0u;
                 }
             }
             if (alive) {
-                if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u, &sk)) {
+                if (march_step_io<SF, true>(a, f, sb, st, fate, it + 2u * j + 1u)) {
                     alive = false;
                     if (fate_before_rk(fate)) st.n_rk = 0u;
                 }
@@ -1504,25 +1411,11 @@ __device__ __forceinline__ void march_ray(const MarchArgs& a, const Frame& f, Ra
 // overlaps the others' bulk instead of ending the launch alone.  Only frame 0
 // records the tile costs for the next launch's order (the histogram must count each tile once).
 //
-// BH_DIAG_PHASES (diagnostic builds only, tools/probe_phases.py): a clock-probed wave also adds the shader
-// cycles of its phases to its XCD's accumulator slots 3..7: wave start -> tables staged, -> march start
-// (tile, pixel ray), -> march end, -> pixel written, -> wave end (cost bookkeeping).
-#ifndef BH_DIAG_PHASES
-#define BH_DIAG_PHASES 0
-#endif
-#if BH_DIAG_PHASES
-struct Phases { uint32_t t[6]; };
-#define BH_PHASE(i) (ph.t[i] = (uint32_t)__builtin_amdgcn_s_memtime())
-#define BH_PHASES_ARG , Phases& ph
-#else
-#define BH_PHASE(i) ((void)0)
-#define BH_PHASES_ARG
-#endif
 
 // One dispatch slot, marched by one wave.
 template <uint32_t FMT, uint32_t SF>
 __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, const float* lut,
-                                           uint32_t lane BH_PHASES_ARG) {
+                                           uint32_t lane) {
     const uint32_t nf = A.n_frames;
     uint32_t fi = 0, j = slot;
     if (nf > 1u) {
@@ -1556,7 +1449,6 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
     st.n_rk = 0;
     st.outside = 0u;
     uint32_t fate = 0xFFu, steps = 0;
-    BH_PHASE(2);
     if (valid) {
         // the camera outside the unit sphere (1.01 leaves room for any rounding of |ro0|^2 against the
         // step's own r^2 > 1 + 2^-23 at iteration 0) and |s| <= 2^30 on every lane: the step without the
@@ -1569,7 +1461,6 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
             march_ray<SF>(a, f, st, fate, steps, lane);
         }
     }
-    BH_PHASE(3);
     if (valid) {
         // the frame's output pointers are loaded here, from an opaque copy of the frame index: loaded
         // up front they would hold 10 SGPRs through the march loop, over the 80 that keep 8
@@ -1585,7 +1476,6 @@ __device__ __forceinline__ void march_slot(const MarchArgs& A, uint32_t slot, co
 #endif
         write_pixel<FMT>(a, lut, out_index(a, t, lane, px, py), col, st.n_rk, fate, steps);
     }
-    BH_PHASE(4);
     if (a.tile_cost) {
         // the next frame's cost and its bucket histogram (a no-return atomic: the wave does not wait);
         // the last bucket is the remainder and is not counted
@@ -1623,60 +1513,24 @@ __device__ __forceinline__ void clock_end(unsigned long long* acc, const ClockSt
     }
 }
 
-// One wave per dispatch slot (the grid covers every slot), BH_WG_WAVES waves per workgroup.
+// One wave per dispatch slot (the grid covers every slot), WG_WAVES waves per workgroup.
 template <uint32_t FMT, uint32_t SF>
-#ifndef BH_MARCH_WPE
-#define BH_MARCH_WPE 0
-#endif
-#if BH_MARCH_WPE
-#define BH_MARCH_WPE_ATTR __attribute__((amdgpu_waves_per_eu(BH_MARCH_WPE, BH_MARCH_WPE)))
-#else
-#define BH_MARCH_WPE_ATTR
-#endif
-// BH_MARCH_WPE (A/B only): ask the register allocator for that many waves per SIMD (§5 item 24)
-__global__ void __launch_bounds__(64 * BH_WG_WAVES) BH_MARCH_WPE_ATTR march_tile_kernel(MarchArgs A) {
+__global__ void __launch_bounds__(64 * WG_WAVES) march_tile_kernel(MarchArgs A) {
     __shared__ float lut[lds_tables<FMT>()];
-#if BH_DIAG_PHASES
-    Phases ph;
-#endif
-    BH_PHASE(0);
-    load_tables<FMT, 64u * BH_WG_WAVES>(A, lut);
+    load_tables<FMT, 64u * WG_WAVES>(A, lut);
     __syncthreads();
-    BH_PHASE(1);
-    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * BH_WG_WAVES + (threadIdx.x >> 6));
+    const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * WG_WAVES + (threadIdx.x >> 6));
     const uint32_t n_slots = A.n_tiles * A.n_frames;
-#if BH_SPW > 1
-    // A/B variant: BH_SPW dispatch slots per wave, one after the other (consecutive slots, or with
-    // BH_SPW_STRIDED slot w + k * waves): the wave start-up (tables, arguments) paid once per BH_SPW tiles
-    const uint32_t n_waves = (n_slots + BH_SPW - 1u) / BH_SPW;
-    for (uint32_t k = 0; k < BH_SPW; ++k) {
-        const uint32_t slot = BH_SPW_STRIDED ? w + k * n_waves : w * BH_SPW + k;
-        if (slot >= n_slots) return;  // wave-uniform
-        if (k != 0u) __builtin_amdgcn_s_setprio(0);
-#else
     {
         const uint32_t slot = w;
         if (slot >= n_slots) return;  // wave-uniform
-#endif
         // one slot in `stride`, rotated by slot / stride: the dispatcher deals workgroups to the 8 XCDs
         // round robin, so plain multiples of the stride would all land on one XCD
         const bool probe = A.clk && ((slot + (slot >> 8)) & A.clk_mask) == 0u;
         ClockStart c0{0u, 0u};
         if (probe) c0 = clock_start();
-#if BH_DIAG_PHASES
-        march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u, ph);
-        if (probe) clock_end(A.clk, c0);
-        BH_PHASE(5);
-        if (probe && (threadIdx.x & 63u) == 0u) {
-            const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
-            for (int i = 0; i < 5; ++i)
-                __hip_atomic_fetch_add(A.clk + 16u * x + 3u + i, (unsigned long long)(ph.t[i + 1] - ph.t[i]), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
-#else
         march_slot<FMT, SF>(A, slot, lut, threadIdx.x & 63u);
         if (probe) clock_end(A.clk, c0);
-#endif
     }
 }
 
@@ -1863,9 +1717,9 @@ __global__ void __launch_bounds__(256) march_pair_kernel(MarchArgs a) {
 // atomic on one word is serialised across the 8 XCDs at ~85 M claims/s)
 template <uint32_t FMT, uint32_t SF>
 inline void launch_tile_schedule(const MarchArgs& a, hipStream_t s) {
-    const uint32_t waves = (a.n_tiles * a.n_frames + (BH_SPW - 1u)) / BH_SPW;
-    const uint32_t blocks = (waves + (BH_WG_WAVES - 1u)) / BH_WG_WAVES;
-    hipLaunchKernelGGL((march_tile_kernel<FMT, SF>), dim3(blocks), dim3(64u * BH_WG_WAVES), 0, s, a);
+    const uint32_t waves = a.n_tiles * a.n_frames;
+    const uint32_t blocks = (waves + (WG_WAVES - 1u)) / WG_WAVES;
+    hipLaunchKernelGGL((march_tile_kernel<FMT, SF>), dim3(blocks), dim3(64u * WG_WAVES), 0, s, a);
 }
 
 }  // namespace BH_NS

@@ -152,15 +152,30 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
 BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
 
 
-@pytest.mark.parametrize("env", [{"BH_BLOOM_FIX2": "1"}, {"BH_BLOOM_NO_FIX": "1"}, {"BH_BLOOM_ORG_KEEP": "1"},
-                                 {"BH_BLOOM_NO_STRIPS": "1"}, {"BH_BLOOM_FIXUP_NOREC": "1"}],
-                         ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec"])
-def test_bloom_switches_stay_bitexact(torch_cuda, env):
-    """The chain's A/B switches, which the library reads once per process, in a child process each: the final
-    epilogue's in-block fix (off by default), no in-block fix, grid origins that keep the block count (1920: a
-    residual column), the final fix-up from the row-major textures instead of its column strips, and the fix-up
-    without its records (which also drops the strips) -- display sizes with opaque and with any alpha, a
-    residual list (1366)."""
+GENERAL_FRAMES = ["1080x1920", "1080x1920:any", "720x1280:any", "768x1366", "768x1366:any"]
+STANDARD_FRAMES = ["512x1024", "256x512:any", "2048x4096"]  # powers of two: the standard plans' kernels
+
+
+@pytest.mark.parametrize("env,frames", [
+    ({"BH_BLOOM_FIX2": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_FIX": "1"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_ORG_KEEP": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_STRIPS": "1"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_FIXUP_NOREC": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_FIXUP_SAMPLE": "1"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_NO_SEPQ": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_SEP": "1"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_SEPQ_RAW": "3"}, GENERAL_FRAMES), ({"BH_BLOOM_SEPQ_MIN_BLOCKS": "100000"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_CAP_PLAIN": "2", "BH_BLOOM_CAP_Y": "2", "BH_BLOOM_CAP_FINAL": "2"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_NO_STD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_UP2": "1"}, STANDARD_FRAMES),
+    ({"BH_BLOOM_NO_YQUAD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_DOWN2": "1"}, STANDARD_FRAMES),
+    ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES)],
+    ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec", "fixup_sample", "no_sepq", "no_sep", "sepq_raw",
+         "sepq_min_blocks", "cap", "no_std", "no_up2", "no_yquad", "no_down2", "persist"])
+def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
+    """Every run-time A/B switch of the chain (the library reads them once per process), in a child process each,
+    against the oracle bit for bit: on display sizes (the general fused chain: the final epilogue's in-block fix,
+    no in-block fix, grid origins that keep the block count, the final fix-up from the row-major textures instead
+    of its column strips, the fix-up without its records, its per-sample form, the one-pixel separable kernel,
+    the per-pixel sampler, raw tiles, quad passes capped in blocks per CU) and on powers of two (the standard
+    plans: off, the general up pass instead of the 2:1 form, the Y pass one pixel per lane, no fused double
+    downsample, the persistent blocks)."""
     import os
     import subprocess
     import sys
@@ -168,8 +183,8 @@ def test_bloom_switches_stay_bitexact(torch_cuda, env):
     root = Path(__file__).resolve().parent.parent
     e = dict(os.environ, **env)
     e["PYTHONPATH"] = str(root) + os.pathsep + e.get("PYTHONPATH", "")
-    r = subprocess.run([sys.executable, str(root / "tests" / "_bloom_env_check.py"), "1080x1920", "1080x1920:any",
-                        "720x1280:any", "768x1366", "768x1366:any"], env=e, capture_output=True, text=True, timeout=600)
+    r = subprocess.run([sys.executable, str(root / "tests" / "_bloom_env_check.py"), *frames], env=e,
+                       capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
 
 

@@ -526,3 +526,20 @@ def test_bgra8_srgb_output_is_encoded_exact_result(torch_cuda, sky_small, cam, s
     assert np.array_equal(col.cpu().numpy(), _bgra8_expected(o[0]))
     assert np.array_equal(bo.cpu().numpy(), _bgra8_expected(o[1]))
     scene.close()
+
+
+@pytest.mark.parametrize("env", [{"BH_NO_SDF_SKIP": "1"}, {"BH_ORDER_ALWAYS": "1"}], ids=["no_sdf_skip", "order_always"])
+def test_march_switches_stay_bitexact(torch_cuda, env):
+    """The march's two run-time A/B switches, which the library reads once per process, in a child process each:
+    every step evaluates its SDF roots (no root-free step), and the temporal order rebuilt on every launch (no
+    repeat skip) -- cameras A and E, three frames each, against the oracle bit for bit (tests/_march_env_check.py)."""
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parent.parent
+    e = dict(os.environ, **env)
+    e["PYTHONPATH"] = str(root) + os.pathsep + e.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, "-m", "tests._march_env_check"], cwd=str(root), env=e, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

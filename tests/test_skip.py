@@ -194,68 +194,5 @@ def test_far_field_implies_dt_equals_dtm_r(rs, dtm):
     assert not bad.any(), p[bad][:4]
 
 
-def term_radii(rs, dtm):
-    """mirror of bh_host.cpp sdf_term_radii: (ps_r2, mo_r2, mi_r2)"""
-    k = 1.1251 * dtm
-    out, m = 1.0 - k, 10.0 * np.sqrt(2.0)
-    ps, mo = np.inf, np.inf
-    if out > 0.01:
-        Rp, Rm = 1.01 * (1.5 * rs + 0.078) / out, 1.01 * (m + 0.503) / out
-        ps, mo = np.nextafter(f32(Rp * Rp), f32(np.inf)), np.nextafter(f32(Rm * Rm), f32(np.inf))
-    Ri = 0.99 * (m - 0.503) / (1.0 + k)
-    return ps, mo, np.nextafter(f32(Ri * Ri), f32(0))
-
-
-def step_terms_from_point(p, rs, dtm, cam, drop_m, drop_p):
-    """step_from_point with the marker / photon-sphere terms left out (+inf) where drop_m / drop_p"""
-    x, y, z = p[:, 0], p[:, 1], p[:, 2]
-    r2 = (x * x + y * y) + z * z
-    r = np.sqrt(r2)
-    dtr = f32(dtm) * r
-    rho = np.sqrt(x * x + z * z)
-    disc = np.fmax(np.fmax(rho - f32(6.0) * rs, -(rho - f32(3.0) * rs)), np.abs(y) - f32(0.02))
-    zz = (f32(-10.0) - z) ** 2
-    ty, tx = f32(10.0) - np.abs(y), f32(10.0) - np.abs(x)
-    qm = np.fmin((x * x + ty * ty) + zz, (tx * tx + y * y) + zz)
-    m = np.where(drop_m, f32(np.inf), np.sqrt(qm) - f32(0.5))
-    cps = (-cam / np.sqrt((cam * cam).sum()) * f32(1.5) * rs).astype(f32)
-    dc = cps - p
-    dps = np.where(drop_p, f32(np.inf), np.sqrt((dc[:, 0] * dc[:, 0] + dc[:, 1] * dc[:, 1]) + dc[:, 2] * dc[:, 2]) - f32(0.075))
-    ds = np.fmin(disc, m)
-    dt = np.fmin(np.fmin(ds, dps) * f32(0.9), dtr)
-    return dt, ds < f32(0.001)
-
-
-@pytest.mark.parametrize("rs,dtm", [(1.0, 0.5), (0.25, 0.5), (8.0, 0.5), (1.0, 0.1), (1.0, 0.6), (0.003, 0.3), (1.0, 2.0)])
-def test_term_radii_keep_dt_and_surface(rs, dtm):
-    """bh_march.hpp BH_SDF_RADII: a lane beyond the photon sphere's radius, or outside the markers' band, may
-    leave that term out of dist: dt and the surface test are the full step's, bit for bit -- on points packed
-    around each radius (every direction, the disc plane's and the markers' included) and spread over all r."""
-    rng = np.random.default_rng(int(rs * 1000 + dtm * 10) + 7)
-    ps, mo, mi = term_radii(rs, dtm)
-    rs = f32(rs)
-    n = 300_000
-    d = rng.normal(size=(n, 3))
-    d[: n // 4, 1] *= 1e-3
-    d[n // 4: n // 2] = [0.0, 1.0, -1.0] + 0.05 * rng.normal(size=(n // 4, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    radii = [np.sqrt(v) for v in (ps, mo, mi) if np.isfinite(v) and v > 0]
-    R = rng.choice(radii, n) * (1 + rng.uniform(-2e-3, 2e-3, n))
-    R = np.where(rng.random(n) < 0.3, np.exp(rng.uniform(0, 6, n)), R)
-    p = (d * R[:, None]).astype(f32)
-    cam = np.array([0.0, 0.0, -20.0], f32)
-    x, y, z = p[:, 0], p[:, 1], p[:, 2]
-    r2 = (x * x + y * y) + z * z
-    fin = r2 <= f32(np.finfo(np.float32).max)
-    drop_p = (r2 >= ps) & fin
-    drop_m = ((r2 >= mo) | (r2 <= mi)) & fin
-    dt, surface = step_terms_from_point(p, rs, dtm, cam, np.zeros(n, bool), np.zeros(n, bool))
-    dt2, surface2 = step_terms_from_point(p, rs, dtm, cam, drop_m, drop_p)
-    bad = (dt2.view(np.int32) != dt.view(np.int32)) | (surface2 != surface)
-    assert not bad.any(), p[bad][:4]
-    assert drop_m.sum() > n // 8  # the points do exercise the radii
-    assert drop_p.sum() > n // 4 or not np.isfinite(ps)
-
-
 def test_far_field_off_for_large_dtm():
     assert far_r2(1.0, 0.7) == np.inf

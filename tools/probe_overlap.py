@@ -31,6 +31,9 @@ p.add_argument("--max-iters", type=int, default=256)
 p.add_argument("--frames", type=int, default=64)
 p.add_argument("--ring", type=int, default=3)
 p.add_argument("--variants", default="all")
+p.add_argument("--camera", choices=["orbit", "A", "B"], default="orbit",
+               help="orbit: every frame a different camera on a circle of radius 20 looking at the origin")
+p.add_argument("--only-march", action="store_true", help="time the march alone (one frame per launch) and exit")
 args = p.parse_args()
 W, H, F, R = args.width, args.height, args.frames, args.ring
 
@@ -61,7 +64,12 @@ cams = []
 for i in range(F):
     a = 2 * math.pi * i / F
     c = bh.CameraUniform()
-    c.update(bh.Camera.look_at((20 * math.sin(a), 2.0, -20 * math.cos(a)), (0.0, 0.0, 0.0), W, H))
+    if args.camera == "orbit":
+        c.update(bh.Camera.look_at((20 * math.sin(a), 2.0, -20 * math.cos(a)), (0.0, 0.0, 0.0), W, H))
+    elif args.camera == "A":
+        c.update(bh.Camera.default(W, H))
+    else:
+        c.update(bh.Camera.look_at((0.0, 3.0, -20.0), (0.0, 0.0, 0.0), W, H))
     cams.append(c)
 col = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(R)]
 bo = [torch.empty_like(col[0]) for _ in range(R)]
@@ -126,6 +134,13 @@ def pipe(sm, sb):
 res = {"width": W, "height": H, "max_iters": args.max_iters, "frames": F, "ring": R, "n_cu": n_cu,
        "prio_range": [lo.value, hi.value]}
 res["march"] = timed(run_march)
+t0 = time.perf_counter()
+run_march(F)
+res["march_enqueue"] = (time.perf_counter() - t0) * 1e3 / F  # host time per frame to enqueue (no sync)
+torch.cuda.synchronize()
+if args.only_march:
+    print(json.dumps({k: (round(v, 5) if isinstance(v, float) else v) for k, v in res.items()}), flush=True)
+    sys.exit(0)
 res["bloom"] = timed(run_bloom)
 res["serial"] = timed(run_serial)
 variants = {
