@@ -9,7 +9,7 @@ from ._abi import (BH_BLOOM_AUTO, BH_BLOOM_LITERAL, BH_FATE_BLACKOUT, BH_FATE_CA
                    BH_OUT_RGBA32F, BH_SCENE_DEFAULT, BH_SCENE_DISC, BH_SCENE_MARKERS, BH_SCHED_FLAG_STATIC_ORDER, BH_SCHED_FLAG_ISSUE_ORDER, BH_SCHED_FLAG_LATENCY, BH_SCHED_PAIR, BH_SCHED_PERSISTENT, BH_SCHED_TILE,
                    BYTES_PER_PIXEL,
                    BhError, load)
-from .scene import (MAX_ITERATIONS, Camera, CameraController, CameraUniform, FrameBatch, Partition, Scene, Uniforms, bloom_check, bloom_plan_failures, clock_mhz, load_sky,
+from .scene import (MAX_ITERATIONS, Camera, CameraController, CameraUniform, FrameBatch, Partition, Presenter, Scene, Uniforms, bloom_check, bloom_plan_failures, clock_mhz, load_sky,
                     partition_map, shard_tile_count, srgb_encode_table, tiles_unpack_rgbm_partition,
                     synthetic_sky, tile_bytes, tiles_unpack, tiles_unpack_rgb, tiles_unpack_rgbm)
 

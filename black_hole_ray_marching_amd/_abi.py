@@ -71,6 +71,13 @@ class bh_render_desc(C.Structure):
                 ("dbg_steps", C.c_void_p), ("partition", C.c_void_p)]
 
 
+class bh_presenter_desc(C.Structure):
+    _fields_ = [(n, C.c_uint32) for n in ("width", "height", "max_iters", "scene_flags", "math", "levels", "batch",
+                                          "bloom_cus")]
+
+
+BH_PRESENT_BATCH_MAX = 32
+
 assert C.sizeof(bh_camera_uniform) == 112
 assert C.sizeof(bh_uniforms) == 32
 
@@ -115,6 +122,11 @@ SIGNATURES = {
                            C.c_void_p, C.c_void_p]),
     "bh_bloom_check": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.c_char_p,
                                  C.c_size_t]),
+    "bh_presenter_create": (C.c_int, [C.c_void_p, C.POINTER(bh_presenter_desc), C.POINTER(C.c_void_p)]),
+    "bh_presenter_destroy": (C.c_int, [C.c_void_p]),
+    "bh_present_frames": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(bh_camera_uniform), C.POINTER(bh_uniforms),
+                                    C.POINTER(C.c_void_p), C.c_void_p]),
+    "bh_present": (C.c_int, [C.c_void_p, C.POINTER(bh_camera_uniform), C.POINTER(bh_uniforms), C.c_void_p, C.c_void_p]),
     "bh_bloom_plan_failures": (C.c_int64, [C.c_char_p, C.c_size_t]),
     "bh_selftest_crmath": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_void_p, C.c_int]),
     "bh_set_clock_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

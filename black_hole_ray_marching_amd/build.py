@@ -55,6 +55,7 @@ TU_FLAGS = {
                      "-mllvm", "-pragma-unroll-threshold=200000"],  # the quad pass's 8 taps x 9 read forms
     "bh_selftest.hip": ["-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt"],
     "bh_host.cpp": ["-ffp-contract=off", "-x", "hip"],
+    "bh_present.cpp": ["-x", "hip"],
 }
 
 

@@ -314,6 +314,10 @@ extern "C" __attribute__((visibility("hidden"))) uint32_t bh_bloom_same_org(uint
                                                                           std::vector<uint32_t>* rows2);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_same_verify(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                          uint32_t nc, uint32_t nr, std::string* why);
+// bh_host.cpp for the other host translation units: the thread's last error, an argument failure, a ctx's device
+extern "C" __attribute__((visibility("hidden"))) void bh_set_last_error(const std::string& msg);
+extern "C" __attribute__((visibility("hidden"))) int bh_bad_arg(const char* fn, int line);
+extern "C" __attribute__((visibility("hidden"))) int bh_ctx_device(const bh_ctx* c);
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_records_verify(uint32_t w, uint32_t h, const uint32_t* plan,
                                                                             const uint32_t* list, uint32_t nc, uint32_t nr,
                                                                             const uint32_t* rec, const uint32_t* stc,

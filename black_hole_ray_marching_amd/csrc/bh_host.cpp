@@ -325,6 +325,14 @@ extern "C" {
 
 int bh_abi_version(void) { return BH_ABI_VERSION; }
 
+// for the other host translation units (bh_present.cpp)
+__attribute__((visibility("hidden"))) void bh_set_last_error(const std::string& msg) { g_last_error = msg; }
+__attribute__((visibility("hidden"))) int bh_bad_arg(const char* fn, int line) {
+    g_last_error = std::string(fn) + ": invalid argument (line " + std::to_string(line) + ")";
+    return BH_ERR_INVALID_ARG;
+}
+__attribute__((visibility("hidden"))) int bh_ctx_device(const bh_ctx* c) { return c->device; }
+
 const char* bh_status_string(int st) {
     switch (st) {
         case BH_OK: return "ok";

@@ -423,6 +423,56 @@ class Scene:
                                 levels, schedule, _ptr(out), _stream_handle(stream)), "bh_bloom")
 
 
+class Presenter:
+    """bh_presenter (include/bh_render.h): the frame the reference app presents per redraw -- State::render
+    (src/state.rs:270-286): Scene::render into the two Bgra8UnormSrgb targets, then Bloom::render to the
+    surface -- pipelined: a call's frames march while the previous call's are bloomed on a second stream.
+    Every surface equals scene.render(..., fmt=BH_OUT_BGRA8_SRGB) + scene.bloom(...) bytes."""
+
+    def __init__(self, scene: "Scene", width: int | None = None, height: int | None = None, *, levels: int = 3,
+                 batch: int = 1, bloom_cus: int = 0, max_iters: int | None = None, math: int | None = None) -> None:
+        self.scene = scene
+        self.width, self.height = width or scene.width, height or scene.height
+        self.batch = batch
+        d = _abi.bh_presenter_desc(self.width, self.height, max_iters or scene.max_iters, scene.scene_flags,
+                                   scene.math if math is None else math, levels, batch, bloom_cus)
+        h = C.c_void_p()
+        check(scene.lib.bh_presenter_create(scene._ctx, C.byref(d), C.byref(h)), "bh_presenter_create")
+        self.handle = h
+        self._cams = (_abi.bh_camera_uniform * batch)()
+        self._outs = (C.c_void_p * batch)()
+        self._keep = None
+
+    def present(self, surfaces, cameras=None, stream=None) -> None:
+        """Frames cameras[i] (CameraUniform; default: the scene's camera) -> surfaces[i] (width x height BGRA8
+        device images), len(surfaces) <= batch; asynchronous on `stream` (the stream then waits for them)."""
+        n = len(surfaces)
+        if not 1 <= n <= self.batch:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, f"present: 1..{self.batch} surfaces, got {n}")
+        if cameras is None:
+            cameras = [self.scene.camera_uniform] * n
+        elif len(cameras) != n:
+            raise BhError(_abi.BH_ERR_INVALID_ARG, "present: one camera per surface")
+        for i, (c, t) in enumerate(zip(cameras, surfaces)):
+            _check_size(t, self.width * self.height * 4, "surface", "present")
+            self._cams[i] = c.c
+            self._outs[i] = _ptr(t)
+        self._keep = surfaces  # referenced until the next call (the stream orders their later users)
+        check(self.scene.lib.bh_present_frames(self.handle, n, self._cams, C.byref(self.scene.uniforms.to_c()),
+                                               self._outs, _stream_handle(stream)), "bh_present_frames")
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            self.scene.lib.bh_presenter_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def clock_mhz(acc) -> dict:
     """The shader clock sampled by set_clock_probe: acc (128 u64 as an int64 array) -> per-XCD MHz and
     the clock over all sampled waves (100 MHz * shader ticks / reference ticks)."""
@@ -563,7 +613,7 @@ def tiles_unpack_rgbm_partition(packed, out_col, out_blackout, partition: "Parti
           "bh_tiles_unpack_rgbm_partition")
 
 
-__all__ = ["Camera", "Partition", "partition_map", "tiles_unpack_rgbm_partition", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
+__all__ = ["Camera", "Partition", "Presenter", "partition_map", "tiles_unpack_rgbm_partition", "CameraController", "CameraUniform", "Uniforms", "Scene", "synthetic_sky", "shard_tile_count", "tiles_unpack",
            "tiles_unpack_rgb", "tiles_unpack_rgbm", "tile_bytes", "BH_LAYOUT_TILES_RGBM", "BH_LAYOUT_TILES_RGBM14",
            "BH_UNPACK_RGBM14",
            "srgb_encode_table", "load_sky", "bloom_plan_failures", "BH_OUT_BGRA8_SRGB",

@@ -307,6 +307,39 @@ int bh_bloom_check(uint32_t width, uint32_t height, uint32_t levels, uint32_t sc
  * refusal's message.  0 for every frame size the tests name. */
 int64_t bh_bloom_plan_failures(char* out_last, size_t len);
 
+/* The frame the reference application presents per redraw, State::render (src/state.rs:270-286):
+ * Scene::render into the two Bgra8UnormSrgb targets, then Bloom::render from them to the surface -- as one
+ * pipelined path.  A presenter owns two banks of `batch` target pairs and two streams of `ctx`'s device:
+ * bh_present_frames marches its n frames (one bh_render_frames launch, BH_OUT_BGRA8_SRGB, both targets)
+ * into one bank while the previous call's frames are bloomed from the other, so the bloom of frame i fills
+ * the CUs the march of frame i + 1 leaves idle instead of adding to it.  Each surface holds exactly the
+ * bytes of bh_render + bh_bloom run one after the other.  Asynchronous: the blooms wait for the caller's
+ * stream as it is at the call (earlier users of the surfaces), and the caller's stream waits for the
+ * call's last bloom (later users see the finished surfaces); the host never blocks.  `bloom_cus` = 0: the
+ * bloom's stream shares every CU at the device's highest priority; k > 0: the bloom runs on k CUs (spread
+ * over the mask), the march on the others (hipExtStreamCreateWithCUMask).  The presenter's blooms share
+ * `ctx`'s bloom scratch: do not run bh_bloom of the same ctx concurrently with it.  The first call of a
+ * presenter allocates (order state, bloom scratch): do not capture it into a graph. */
+#define BH_PRESENT_BATCH_MAX 32
+typedef struct bh_presenter bh_presenter;
+typedef struct {
+    uint32_t width, height;   /* frame size (1..65536) */
+    uint32_t max_iters;       /* MAX_ITERATIONS, 1..65535 */
+    uint32_t scene_flags;     /* BH_SCENE_* */
+    uint32_t math;            /* bh_math_mode */
+    uint32_t levels;          /* the Bloom's levels (src/state.rs:125: 3), 1..12 */
+    uint32_t batch;           /* frames per bh_present_frames call, 1..BH_PRESENT_BATCH_MAX (1: one frame per redraw) */
+    uint32_t bloom_cus;       /* 0: shared CUs, high-priority bloom stream; else CUs given to the bloom */
+} bh_presenter_desc;
+int bh_presenter_create(bh_ctx* ctx, const bh_presenter_desc* desc, bh_presenter** out);
+int bh_presenter_destroy(bh_presenter* presenter);
+/* n (1..batch) frames: cameras[i] -> out_surfaces[i] (width x height BGRA8 device images, caller-owned). */
+int bh_present_frames(bh_presenter* presenter, uint32_t n, const bh_camera_uniform* cameras, const bh_uniforms* uniforms,
+                      void* const* out_surfaces, void* hip_stream);
+/* bh_present_frames of one frame: State::render. */
+int bh_present(bh_presenter* presenter, const bh_camera_uniform* camera, const bh_uniforms* uniforms, void* out_surface,
+               void* hip_stream);
+
 /* Graph contract (see the top of this file): unpin every order state and bloom scratch set that a
  * capture marked, so that LRU eviction may free them again.  Call it only after destroying every HIP
  * graph captured from this ctx (their kernels read and write those buffers). */

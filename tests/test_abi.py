@@ -33,7 +33,8 @@ def test_abi_version_and_status_strings():
     # the Python mirror's constants are the header's
     text = HEADER.read_text()
     for name, value in (("BH_ABI_VERSION", _abi.ABI_VERSION), ("BH_MAX_FRAMES", _abi.BH_MAX_FRAMES),
-                        ("BH_ORDER_STATES", _abi.BH_ORDER_STATES), ("BH_BLOOM_SETS", _abi.BH_BLOOM_SETS)):
+                        ("BH_ORDER_STATES", _abi.BH_ORDER_STATES), ("BH_BLOOM_SETS", _abi.BH_BLOOM_SETS),
+                        ("BH_PRESENT_BATCH_MAX", _abi.BH_PRESENT_BATCH_MAX)):
         assert re.search(rf"#define {name} {value}\b", text), name
     assert lib.bh_status_string(0) == b"ok"
     assert lib.bh_status_string(-1) == b"invalid argument"
