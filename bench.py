@@ -788,10 +788,14 @@ def main() -> int:
                             f"{'disc+markers+sky' if flags else 'sky only (no surfaces)'}, camera {args.camera}"
                             + (f" orbiting {args.orbit_deg} deg/frame" if args.camera_path == "orbit" else "") + ", "
                             f"{args.fmt} col+blackout, {args.math} math, {D} frames per step"
-                            + ("" if not sharded else f", 8x8 tiles (tx+3ty)%{n} per rank, RCCL gather of "
-                                                  f"{'RGBM14' if p14 else 'RGBM'} shards "
-                                                  "(RGB + blackout mask) to rank 0 overlapped with the next "
-                                                  "batch, rank 0 unpacks col and blackout_col"),
+                            + ("" if not sharded else
+                               ", 8x8 tiles dealt by a weighted tile-list partition (bh_partition: rank k owns "
+                               f"weights[k] of every sum(weights) residues of (tx+3ty), weights {weights or [20] * n}), "
+                               f"{dist.get_backend() if dist.is_initialized() else 'no'} "
+                               f"{'(RCCL) ' if dist.is_initialized() and dist.get_backend() == 'nccl' else ''}gather of "
+                               f"{'RGBM14' if p14 else 'RGBM'} shards (RGB + blackout mask) to rank 0 overlapped "
+                               "with the next batch, rank 0 unpacks col and blackout_col"
+                               + (" (REHEARSAL: every rank on cuda:0 over gloo)" if rehearsal else "")),
                 "baseline_config": args.config or None,
                 "width": W, "height": H, "max_iters": cap, "camera": args.camera, "camera_path": args.camera_path,
                 "math": args.math,

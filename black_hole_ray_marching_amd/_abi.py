@@ -73,10 +73,11 @@ class bh_render_desc(C.Structure):
 
 class bh_presenter_desc(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("width", "height", "max_iters", "scene_flags", "math", "levels", "batch",
-                                          "bloom_cus")]
+                                          "bloom_cus", "depth", "march_streams")]
 
 
 BH_PRESENT_BATCH_MAX = 32
+BH_PRESENT_DEPTH_MAX = 8
 
 assert C.sizeof(bh_camera_uniform) == 112
 assert C.sizeof(bh_uniforms) == 32

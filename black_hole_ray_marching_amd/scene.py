@@ -426,16 +426,18 @@ class Scene:
 class Presenter:
     """bh_presenter (include/bh_render.h): the frame the reference app presents per redraw -- State::render
     (src/state.rs:270-286): Scene::render into the two Bgra8UnormSrgb targets, then Bloom::render to the
-    surface -- pipelined: a call's frames march while the previous call's are bloomed on a second stream.
+    surface -- pipelined: a call's frames march while the previous call's are bloomed on a second stream, and
+    (march_streams 2) while the previous call's march tail still runs on the other march stream.
     Every surface equals scene.render(..., fmt=BH_OUT_BGRA8_SRGB) + scene.bloom(...) bytes."""
 
     def __init__(self, scene: "Scene", width: int | None = None, height: int | None = None, *, levels: int = 3,
-                 batch: int = 1, bloom_cus: int = 0, max_iters: int | None = None, math: int | None = None) -> None:
+                 batch: int = 1, bloom_cus: int = 0, depth: int = 0, march_streams: int = 0,
+                 max_iters: int | None = None, math: int | None = None) -> None:
         self.scene = scene
         self.width, self.height = width or scene.width, height or scene.height
         self.batch = batch
         d = _abi.bh_presenter_desc(self.width, self.height, max_iters or scene.max_iters, scene.scene_flags,
-                                   scene.math if math is None else math, levels, batch, bloom_cus)
+                                   scene.math if math is None else math, levels, batch, bloom_cus, depth, march_streams)
         h = C.c_void_p()
         check(scene.lib.bh_presenter_create(scene._ctx, C.byref(d), C.byref(h)), "bh_presenter_create")
         self.handle = h

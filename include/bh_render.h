@@ -309,10 +309,14 @@ int64_t bh_bloom_plan_failures(char* out_last, size_t len);
 
 /* The frame the reference application presents per redraw, State::render (src/state.rs:270-286):
  * Scene::render into the two Bgra8UnormSrgb targets, then Bloom::render from them to the surface -- as one
- * pipelined path.  A presenter owns two banks of `batch` target pairs and two streams of `ctx`'s device:
- * bh_present_frames marches its n frames (one bh_render_frames launch, BH_OUT_BGRA8_SRGB, both targets)
- * into one bank while the previous call's frames are bloomed from the other, so the bloom of frame i fills
- * the CUs the march of frame i + 1 leaves idle instead of adding to it.  Each surface holds exactly the
+ * pipelined path.  A presenter owns `depth` banks of `batch` target pairs, `march_streams` march streams and
+ * one bloom stream of `ctx`'s device: call c marches its n frames (one bh_render_frames launch,
+ * BH_OUT_BGRA8_SRGB, both targets) into bank c % depth on march stream c % march_streams, then blooms them on
+ * the bloom stream.  So the bloom of call c fills the CUs the march of call c + 1 leaves idle instead of
+ * adding to it, and (march_streams 2) the march of call c + 1 starts while the serial tail of call c's march
+ * -- the few rays that run to the cap -- still runs, as the frames of one multi-frame launch overlap each
+ * other's tails.  A call of 4 or more frames fills the GPU by itself (its frames overlap each other's tails in
+ * one launch): it runs its march and then its blooms on the caller's stream, in order.  Each surface holds exactly the
  * bytes of bh_render + bh_bloom run one after the other.  Asynchronous: the blooms wait for the caller's
  * stream as it is at the call (earlier users of the surfaces), and the caller's stream waits for the
  * call's last bloom (later users see the finished surfaces); the host never blocks.  `bloom_cus` = 0: the
@@ -321,6 +325,7 @@ int64_t bh_bloom_plan_failures(char* out_last, size_t len);
  * `ctx`'s bloom scratch: do not run bh_bloom of the same ctx concurrently with it.  The first call of a
  * presenter allocates (order state, bloom scratch): do not capture it into a graph. */
 #define BH_PRESENT_BATCH_MAX 32
+#define BH_PRESENT_DEPTH_MAX 8
 typedef struct bh_presenter bh_presenter;
 typedef struct {
     uint32_t width, height;   /* frame size (1..65536) */
@@ -330,6 +335,9 @@ typedef struct {
     uint32_t levels;          /* the Bloom's levels (src/state.rs:125: 3), 1..12 */
     uint32_t batch;           /* frames per bh_present_frames call, 1..BH_PRESENT_BATCH_MAX (1: one frame per redraw) */
     uint32_t bloom_cus;       /* 0: shared CUs, high-priority bloom stream; else CUs given to the bloom */
+    uint32_t depth;           /* calls in flight: target banks, 2..BH_PRESENT_DEPTH_MAX (0: 3) */
+    uint32_t march_streams;   /* 1 or 2, at most depth (0: 2 when the call's frames hold at most 64 tiles
+                                 per CU -- a march that leaves the GPU mostly idle -- else 1) */
 } bh_presenter_desc;
 int bh_presenter_create(bh_ctx* ctx, const bh_presenter_desc* desc, bh_presenter** out);
 int bh_presenter_destroy(bh_presenter* presenter);

@@ -47,7 +47,7 @@ def expected_bytes(fmt, x):
     return np.stack([e[..., 2], e[..., 1], e[..., 0], np.full(e.shape[:2], 255, np.uint8)], -1)
 
 
-def render_full(torch, scene, W, H, fmt, dbg=False):
+def render_full(torch, scene, W, H, fmt, dbg=False, schedule=0):
     dt = getattr(torch, DT[fmt])
     col = torch.zeros((H, W, 4), dtype=dt, device="cuda")
     bo = torch.zeros((H, W, 4), dtype=dt, device="cuda")
@@ -55,7 +55,7 @@ def render_full(torch, scene, W, H, fmt, dbg=False):
     if dbg:
         kw = dict(dbg_n_rk=torch.zeros((H, W), dtype=torch.int16, device="cuda"),
                   dbg_fate=torch.full((H, W), 0xFF, dtype=torch.uint8, device="cuda"))
-    scene.render(col, bo, fmt=fmt, **kw)
+    scene.render(col, bo, fmt=fmt, schedule=schedule, **kw)
     torch.cuda.synchronize()
     out = [col.cpu().numpy(), bo.cpu().numpy()]
     if dbg:
@@ -81,8 +81,11 @@ def test_full_frame_bitexact(torch_cuda, sky_full, cid, W, H, cap, cam, flags, f
     scene = bh.Scene(W, H, sky=sky_full, max_iters=cap, scene_flags=flags, math=bh.BH_MATH_EXACT)
     scene.camera_uniform = cu
     oc, ob, on, of = oracle.render_rows(cu.to_bytes(), bytes(U.to_c()), sky_full, W, H, cap, flags)
-    for frame in range(2):  # first frame (centre-out order) and second (learned cost order)
-        gc, gb, gn, gf = render_full(torch, scene, W, H, bh.BH_OUT_RGBA32F, dbg=True)
+    # first frame (centre-out order) and second (learned cost order); then both exact builds forced (camera B:
+    # photon-sphere rays whose tail steps take the tiny-dt form, bh_march.hpp step_bf TINY / step_tail)
+    scheds = [0, 0] + ([bh.BH_SCHED_FLAG_ISSUE_ORDER, bh.BH_SCHED_FLAG_LATENCY] if cam == "B" else [])
+    for frame, sched in enumerate(scheds):
+        gc, gb, gn, gf = render_full(torch, scene, W, H, bh.BH_OUT_RGBA32F, dbg=True, schedule=sched)
         assert np.array_equal(gf, of), f"{cid} frame {frame}: fate mismatch at {np.argwhere(gf != of)[:5]}"
         assert np.array_equal(gn, on), f"{cid} frame {frame}: n_rk mismatch at {np.argwhere(gn != on)[:5]}"
         bad = gc.view(np.uint32) != oc.view(np.uint32)

@@ -44,18 +44,20 @@ def _serial(torch, scene, cams, W, H):
     return [o.cpu().numpy() for o in out]
 
 
-@pytest.mark.parametrize("W,H,cap,batch,bloom_cus", [(320, 200, 256, 1, 0), (320, 200, 256, 1, 16),
-                                                     (256, 128, 512, 4, 0), (1280, 720, 256, 1, 0),
-                                                     (1920, 1080, 256, 2, 8)])
-def test_pipelined_frames_equal_serial(torch_cuda, sky_small, W, H, cap, batch, bloom_cus):
+@pytest.mark.parametrize("W,H,cap,batch,bloom_cus,depth,ms", [(320, 200, 256, 1, 0, 2, 1), (320, 200, 256, 1, 16, 2, 1),
+                                                              (256, 128, 512, 4, 0, 2, 2), (1280, 720, 256, 1, 0, 2, 2),
+                                                              (1920, 1080, 256, 2, 8, 2, 1), (640, 360, 512, 1, 0, 4, 2),
+                                                              (512, 256, 256, 3, 0, 3, 1)])
+def test_pipelined_frames_equal_serial(torch_cuda, sky_small, W, H, cap, batch, bloom_cus, depth, ms):
     """An orbiting camera (every frame its own), 3 calls per bank reuse: the pipelined surfaces, written while
-    other frames march, are the serial chain's bytes -- one frame per call, several, and with the CU split."""
+    other frames march, are the serial chain's bytes -- one frame per call, several, with the CU split, and with
+    several march streams in flight."""
     torch = torch_cuda
     scene = bh.Scene(W, H, sky=sky_small, max_iters=cap, math=bh.BH_MATH_EXACT)
-    n = 6 * batch
+    n = 3 * depth * batch
     cams = _orbit(n, W, H)
     want = _serial(torch, scene, cams, W, H)
-    p = bh.Presenter(scene, batch=batch, bloom_cus=bloom_cus)
+    p = bh.Presenter(scene, batch=batch, bloom_cus=bloom_cus, depth=depth, march_streams=ms)
     surf = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(n)]
     s = torch.cuda.Stream()
     for k in range(0, n, batch):
@@ -64,6 +66,28 @@ def test_pipelined_frames_equal_serial(torch_cuda, sky_small, W, H, cap, batch, 
     for i in range(n):
         got = surf[i].cpu().numpy()
         assert np.array_equal(got, want[i]), (i, np.argwhere(got != want[i])[:4])
+    p.close()
+    scene.close()
+
+
+def test_mixed_call_sizes_equal_serial(torch_cuda, sky_small):
+    """Calls of 4 frames (blooms after the march on its stream) between calls of 1 and 2 (blooms on the bloom
+    stream): the chains never overlap each other (shared scratch) and every surface is the serial bytes."""
+    torch = torch_cuda
+    W, H = 320, 160
+    scene = bh.Scene(W, H, sky=sky_small, max_iters=256, math=bh.BH_MATH_EXACT)
+    sizes = [4, 1, 2, 4, 1, 4, 2]
+    cams = _orbit(sum(sizes), W, H)
+    want = _serial(torch, scene, cams, W, H)
+    p = bh.Presenter(scene, batch=4, march_streams=2)
+    surf = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in cams]
+    k = 0
+    for n in sizes:
+        p.present(surf[k:k + n], cameras=cams[k:k + n])
+        k += n
+    torch.cuda.synchronize()
+    for i, t in enumerate(surf):
+        assert np.array_equal(t.cpu().numpy(), want[i]), i
     p.close()
     scene.close()
 
@@ -119,6 +143,12 @@ def test_presenter_invalid_arguments(torch_cuda, sky_small):
         bh.Presenter(scene, batch=bh._abi.BH_PRESENT_BATCH_MAX + 1)
     with pytest.raises(bh.BhError):
         bh.Presenter(scene, bloom_cus=100000)
+    with pytest.raises(bh.BhError):
+        bh.Presenter(scene, depth=1)
+    with pytest.raises(bh.BhError):
+        bh.Presenter(scene, depth=bh._abi.BH_PRESENT_DEPTH_MAX + 1)
+    with pytest.raises(bh.BhError):
+        bh.Presenter(scene, march_streams=3)
     p = bh.Presenter(scene, batch=2)
     t = torch.zeros((32, 64, 4), dtype=torch.uint8, device="cuda")
     with pytest.raises(bh.BhError):

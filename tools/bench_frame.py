@@ -4,7 +4,9 @@ targets) + Bloom::render (/root/reference/src/state.rs:270-286), per frame, on o
   bloom      bh_bloom alone
   serial     march then bloom on one stream, frame after frame
   pipelined  bh_presenter (include/bh_render.h): a call's frames march while the previous call's are bloomed on a
-             second stream; `pipelined_cus<k>`: the same with the bloom on k CUs and the march on the others
+             second stream (defaults: 3 calls in flight, march streams auto); variants: `pipelined_d<N>m<K>` N
+             calls in flight (target banks) and K march streams (K = 2: the next call's march also starts under this
+             one's tail), `pipelined_cus<k>` the bloom on k CUs and the march on the others
 `hidden` = (serial - pipelined) / bloom: the share of the bloom the pipeline hides.  HIP events on the caller's
 stream around `frames` frames (after a warm-up); the shader clock of the march launches (bh_set_clock_probe)
 during the pipelined run; `roofline`: the march's algorithmic FP32 work (the frames' executed-RK-step counts from
@@ -30,6 +32,11 @@ p.add_argument("--camera", choices=["orbit", "A", "B"], default="orbit")
 p.add_argument("--frames", type=int, default=64)
 p.add_argument("--batch", type=int, default=1)
 p.add_argument("--cus", default="8", help="comma list of bloom CU counts for the CU-split variant ('' = none)")
+p.add_argument("--variants", default="d2m1,d3m1,d3m2",
+               help="presenter variants beyond the default (depth 3, march streams auto): dNmK = depth N, K march streams")
+p.add_argument("--only-pipelined", action="store_true",
+               help="time the default presenter only (a rocprofv3 trace of the pipeline: tools/prof_overlap.py)")
+p.add_argument("--no-roofline", action="store_true", help="skip the debug renders that count the executed RK steps")
 args = p.parse_args()
 
 
@@ -72,7 +79,7 @@ for spec in args.sizes.split(","):
     col = [torch.empty((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(D)]
     bo = [torch.empty_like(col[0]) for _ in range(D)]
     total_steps = 0
-    for c in cams:
+    for c in ([] if args.no_roofline else cams):
         scene.camera_uniform = c
         scene.render(col[0], bo[0], fmt=bh.BH_OUT_BGRA8_SRGB, dbg_steps=steps)
         total_steps += int(steps.cpu().numpy().view(np.uint16).astype(np.int64).sum())
@@ -100,9 +107,16 @@ for spec in args.sizes.split(","):
                 pr.present(surf[k:k + D], cameras=cams[k:k + D], stream=st)
         return run
 
-    row = {"width": W, "height": H, "max_iters": cap, "camera": args.camera, "frames": F, "batch": D,
-           "march_ms": round(timed(march, s, F), 5), "bloom_ms": round(timed(bloom, s, F), 5),
-           "serial_ms": round(timed(serial, s, F), 5)}
+    row = {"width": W, "height": H, "max_iters": cap, "camera": args.camera, "frames": F, "batch": D}
+    if args.only_pipelined:
+        pr = bh.Presenter(scene, batch=D)
+        row["pipelined_ms"] = round(timed(piped(pr), s, F), 5)
+        pr.close()
+        print(json.dumps(row), flush=True)
+        scene.close()
+        continue
+    row.update(march_ms=round(timed(march, s, F), 5), bloom_ms=round(timed(bloom, s, F), 5),
+               serial_ms=round(timed(serial, s, F), 5))
     # verify: the pipelined surfaces equal the serial ones (the serial run just wrote surf)
     ref = [t.clone() for t in surf]
     pr = bh.Presenter(scene, batch=D)
@@ -114,6 +128,11 @@ for spec in args.sizes.split(","):
     row["pipelined_equals_serial"] = all(torch.equal(a, b) for a, b in zip(ref, surf))
     row["clock_mhz"] = bh.clock_mhz(acc.cpu().numpy())["mhz"]
     pr.close()
+    for v in filter(None, args.variants.split(",")):
+        dep, ms = (int(x) for x in v[1:].split("m"))
+        pr = bh.Presenter(scene, batch=D, depth=dep, march_streams=ms)
+        row[f"pipelined_{v}_ms"] = round(timed(piped(pr), s, F), 5)
+        pr.close()
     for k in filter(None, args.cus.split(",")):
         pr = bh.Presenter(scene, batch=D, bloom_cus=int(k))
         row[f"pipelined_cus{k}_ms"] = round(timed(piped(pr), s, F), 5)
@@ -121,6 +140,10 @@ for spec in args.sizes.split(","):
     best = min(v for kk, v in row.items() if kk.startswith("pipelined") and kk.endswith("_ms"))
     row["hidden"] = round((row["serial_ms"] - best) / row["bloom_ms"], 3)
     row["speedup_vs_serial"] = round(row["serial_ms"] / best, 3)
+    if args.no_roofline:
+        print(json.dumps(row), flush=True)
+        scene.close()
+        continue
     flop = total_steps / F * F_STEP
     row["roofline"] = {"bound": "valu", "achieved": round(flop / (best * 1e-3) / 1e12, 2), "peak": PEAK / 1e12,
                        "unit": "TFLOP/s", "frac": round(flop / (best * 1e-3) / PEAK, 4),

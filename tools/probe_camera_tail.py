@@ -32,7 +32,7 @@ bos = [torch.empty_like(outs[0]) for _ in range(D)]
 n_rk = torch.empty((H, W), dtype=torch.int16, device="cuda")
 steps = torch.empty_like(n_rk)
 fate = torch.empty((H, W), dtype=torch.uint8, device="cuda")
-builds = {"auto": 0, "issue_order": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY}
+builds = {"issue_order": bh.BH_SCHED_FLAG_ISSUE_ORDER, "latency": bh.BH_SCHED_FLAG_LATENCY, "auto": 0}
 for cam in args.cameras.split(","):
     pos, tgt = CAMERAS[cam]
     scene.update(bh.Camera.look_at(pos, tgt, W, H))

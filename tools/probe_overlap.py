@@ -54,7 +54,7 @@ def mk_stream(mask_bits=None, prio=None):
             words[b // 32] |= 1 << (b % 32)
         rc = hip.hipExtStreamCreateWithCUMask(C.byref(s), len(words), words)
     else:
-        rc = hip.hipStreamCreateWithPriority(C.byref(s), 0, hi.value if prio == "high" else 0)
+        rc = hip.hipStreamCreateWithPriority(C.byref(s), 0, {"high": hi.value, "low": lo.value}.get(prio, 0))
     assert rc == 0, rc
     return s.value
 
@@ -114,14 +114,17 @@ def run_serial(n):
 
 
 def pipe(sm, sb):
-    tm, tb = torch.cuda.ExternalStream(sm), torch.cuda.ExternalStream(sb)
+    """sm: one march stream or a list (frame i marches on sm[i % len])"""
+    sms = sm if isinstance(sm, list) else [sm]
+    tms, tb = [torch.cuda.ExternalStream(x) for x in sms], torch.cuda.ExternalStream(sb)
 
     def run(n):
         done = [None] * n
         for i in range(n):
+            tm, smi = tms[i % len(sms)], sms[i % len(sms)]
             if i >= R:
                 tm.wait_event(done[i - R])
-            render(i, sm)
+            render(i, smi)
             e = torch.cuda.Event()
             e.record(tm)
             tb.wait_event(e)
@@ -146,8 +149,14 @@ res["serial"] = timed(run_serial)
 variants = {
     "normal": lambda: (mk_stream(), mk_stream()),
     "bloom_high": lambda: (mk_stream(), mk_stream(prio="high")),
+    "bloom_low": lambda: (mk_stream(), mk_stream(prio="low")),
+    "march_high": lambda: (mk_stream(prio="high"), mk_stream()),
+    "2march_normal": lambda: ([mk_stream(), mk_stream()], mk_stream()),
+    "2march_bloom_high": lambda: ([mk_stream(), mk_stream()], mk_stream(prio="high")),
+    "2march_bloom_low": lambda: ([mk_stream(), mk_stream()], mk_stream(prio="low")),
+    "2march_march_high": lambda: ([mk_stream(prio="high"), mk_stream(prio="high")], mk_stream()),
 }
-for k in (8, 16, 32, 64):
+for k in (8, 16, 32, 64) if args.variants == "all" else ():
     # k CUs for the bloom: every (n_cu / k)-th CU, whatever the bit -> XCD mapping
     step = n_cu // k
     bl = [i * step for i in range(k)]

@@ -16,6 +16,25 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
 
 
+def masked_streams(torch, k):
+    """(render stream on every CU but k, unpack stream on those k: every (n_cu / k)-th mask bit), as torch streams"""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipExtStreamCreateWithCUMask.argtypes = [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_uint32)]
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (n_cu + 31) // 32
+    side = {i * (n_cu // k) for i in range(k)}
+    out = []
+    for bits in ([c for c in range(n_cu) if c not in side], sorted(side)):
+        m = (C.c_uint32 * words)()
+        for b in bits:
+            m[b // 32] |= 1 << (b % 32)
+        h = C.c_void_p()
+        assert hip.hipExtStreamCreateWithCUMask(C.byref(h), words, m) == 0
+        out.append(torch.cuda.ExternalStream(h.value))
+    return out
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--n", default="2,4,8")
@@ -28,6 +47,8 @@ def main():
     p.add_argument("--side-priority", default="0", help="comma list: the unpack stream's priority (0 normal, -1 high)")
     p.add_argument("--render-streams", type=int, default=1, help="launches alternate over this many streams")
     p.add_argument("--tag", default="", help="copied into every line (e.g. the A/B variant)")
+    p.add_argument("--cu-split", default="0", help="comma list: k > 0 runs the unpack on k CUs and the render on the "
+                                                   "others (hipExtStreamCreateWithCUMask), 0 = shared CUs")
     a = p.parse_args()
     import torch
     import black_hole_ray_marching_amd as bh
@@ -48,7 +69,8 @@ def main():
             counts = part.counts if part else [bh.shard_tile_count(W, H, k, n) for k in range(n)]
             stride = max(counts)
             kw = dict(layout=layout, shard_count=n, **({"partition": part} if part else {}))
-            for rows, sp in ((int(r), int(q)) for r in a.rows.split(",") for q in a.side_priority.split(",")):
+            for rows, sp, cus in ((int(r), int(q), int(c)) for r in a.rows.split(",") for q in a.side_priority.split(",")
+                                  for c in a.cu_split.split(",")):
                 scene = bh.Scene(W, H, sky=sky, device=0, max_iters=512, math=bh.BH_MATH_EXACT)
                 bufs = [torch.empty((D * stride, tb), dtype=torch.uint8, device=dev) for _ in range(2)]
                 K1 = 1 if n > 1 else 0  # n = 1: the whole frame in the packed layout (rank 1 := rank 0)
@@ -61,6 +83,9 @@ def main():
                 rs = torch.cuda.current_stream()
                 ss = torch.cuda.Stream(priority=sp)
                 rss = [rs] + [torch.cuda.Stream() for _ in range(a.render_streams - 1)]
+                if cus:
+                    rs, ss = masked_streams(torch, cus)
+                    rss = [rs]
                 nl = [0]
 
                 def render(k):
@@ -101,6 +126,7 @@ def main():
                 r1 = run(a.it, K1, True, False)
                 out = {"tag": a.tag, "n": n, "frame": f"{W}x{H}", "frames_per_launch": D, "unpack_rows_in_flight": rows,
                        "transport": a.transport, "tile_bytes": tb, "side_priority": sp, "render_streams": a.render_streams,
+                       "unpack_cus": cus or None,
                        "root_ratio": round(ratio, 4), "weights": weights if part else None, "tiles": (counts + counts)[:2],
                        "rank0_render_ms": round(run(a.it, 0, True, False), 4), "rank0_render_plus_unpack_ms": round(r0, 4),
                        "rank1_render_ms": round(r1, 4), "unpack_only_ms": round(run(a.it, 0, False, True), 4),
