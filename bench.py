@@ -592,7 +592,8 @@ def main() -> int:
     extra = not (args.no_extra or sharded or args.graph)
     n_orbit_frames = (args.warmup + args.steps) * D if args.camera_path == "orbit" else 0
     if extra:
-        n_orbit_frames = max(n_orbit_frames, 2 * EXTRA_ORBIT_LAUNCHES * D + D)  # _leg's two passes + the untimed one
+        # _leg's two passes + the untimed one (orbit), and the one-frame orbit leg's two passes
+        n_orbit_frames = max(n_orbit_frames, 2 * EXTRA_ORBIT_LAUNCHES * D + D, 2 * EXTRA_SINGLE_FRAMES + 1)
     if n_orbit_frames:
         if args.graph:
             raise SystemExit("--graph replays one launch's cameras: use --camera-path fixed")
@@ -640,7 +641,7 @@ def main() -> int:
     # millisecond costs the next launch ~10 % of its time while the clock ramps back up)
     K = args.steps
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    clk = torch.zeros((3, 128), dtype=torch.int64, device=dev)  # shader clock: timed region, extra legs
+    clk = torch.zeros((4, 128), dtype=torch.int64, device=dev)  # shader clock: timed region, extra legs
     for _ in range(args.warmup):
         render(D)
         exchange(D)
@@ -738,7 +739,23 @@ def main() -> int:
             frame_no[0] += D
         legs["orbit"] = _leg(orbit_launch, EXTRA_ORBIT_LAUNCHES, D, scene, clk[2], stream, dev, W, H, torch, bh)
         legs["single_frame"]["note"] = ("one bh_render_frames(n=1) per frame, fixed camera, back to back: the "
-                                        "reference's one Scene::render per redraw (src/state.rs:270-279)")
+                                        "reference's one Scene::render per redraw (src/state.rs:270-279); a "
+                                        "repeated frame skips the dispatch-order build (its costs are the ones "
+                                        "the order holds), so this is the static camera's best case: "
+                                        "single_frame_orbit moves the camera every frame")
+        frame_no[0] = 0
+        launch(1, path="orbit")  # untimed: the order learns the path's start
+        frame_no[0] = 1
+
+        def orbit_single():
+            launch(1, path="orbit")
+            frame_no[0] += 1
+        legs["single_frame_orbit"] = _leg(orbit_single, EXTRA_SINGLE_FRAMES, 1, scene, clk[3], stream, dev, W, H,
+                                          torch, bh)
+        legs["single_frame_orbit"].update(deg_per_frame=args.orbit_deg, note=(
+            f"one bh_render_frames(n=1) per frame, camera {args.camera} orbiting the hole at {args.orbit_deg} "
+            "deg/frame: the interactive redraw of a moving camera (every frame builds its dispatch order from the "
+            "previous frame's costs)"))
         legs["orbit"].update(deg_per_frame=args.orbit_deg, frames_per_launch=D,
                              note=f"camera {args.camera} orbiting the hole at {args.orbit_deg} deg/frame, {D} "
                                   "frames per launch each with its own camera (the dispatch order learned from "

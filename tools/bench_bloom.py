@@ -3,8 +3,10 @@ bloom + remix over a 4096x2048 BGRA8 frame (the march kernel's own two targets),
 stream, fused (AUTO) and literal schedules.  `roofline` (tools/bloom_roofline.py): the chain's
 algorithmic bytes (read col + blackout, write the surface: 12 B/pixel) against HBM, the reference's arithmetic
 in flop-equivalents as a rate against the FP32 VALU peak (an op count, not executed instructions), and -- when
-a committed rocprofv3 PMC summary of this frame size exists (profiles/r05/bloom_roof/roofline<W>.json) -- the
-hardware's executed VALU-issue, LDS and HBM busy fractions, time-weighted over the fused chain's kernels.
+a committed rocprofv3 PMC summary of this frame size exists (profiles/r*/bloom_roof/roofline<W>.json, the newest) --
+the hardware's executed VALU-issue, LDS and HBM busy fractions, time-weighted over the fused chain's kernels: as
+`hardware` when the summary's library_sha256 is the loaded library's, else as `profiled_build_hardware` (another
+build's counters, kept apart from this run's time).
     python tools/bench_bloom.py [--width 4096 --height 2048 --levels 3 --steps 100]"""
 import argparse
 import json
@@ -23,15 +25,20 @@ ROOT = Path(__file__).resolve().parent.parent
 
 
 def hardware_busy(W, H):
-    """Time-weighted VALU / LDS busy and HBM fraction of the fused chain's kernels from the committed PMC summary."""
-    f = ROOT / "profiles" / "r05" / "bloom_roof" / f"roofline{W}.json"
-    if not f.exists():
+    """Time-weighted VALU / LDS busy and HBM fraction of the fused chain's kernels from the newest committed PMC
+    summary of this frame size, with the build it profiled (library_sha256; absent in round 5's summaries):
+    (key, fields), key 'hardware' when that build is the loaded library, else 'profiled_build_hardware'."""
+    from tools.bloom_roofline import library_sha256
+    cands = sorted((ROOT / "profiles").glob(f"r*/bloom_roof/roofline{W}.json"))
+    if not cands:
         return None
+    f = cands[-1]
     d = json.loads(f.read_text())
     if d.get("height") != H or "kernels" not in d:
         return None
     t = sum(k["us"] * k["launches_per_chain"] for k in d["kernels"])
-    out = {"source": str(f.relative_to(ROOT)), "kernel_us_per_chain": round(t, 2)}
+    out = {"source": str(f.relative_to(ROOT)), "kernel_us_per_chain": round(t, 2),
+           "profiled_library_sha256": d.get("library_sha256"), "loaded_library_sha256": library_sha256()}
     for key in ("valu_busy", "lds_busy", "hbm_frac"):
         out[key] = round(sum(k.get(key, 0.0) * k["us"] * k["launches_per_chain"] for k in d["kernels"]) / t, 3)
     return out
@@ -76,5 +83,7 @@ for name, sched in (("auto", bh.BH_BLOOM_AUTO), ("literal", bh.BH_BLOOM_LITERAL)
         line["roofline"] = chain_roofline(W, H, args.levels, float(ms.mean()))
         hw = hardware_busy(W, H)
         if hw:
-            line["roofline"]["hardware"] = hw
+            # only the build that was profiled may report its counters as this run's
+            same = hw["profiled_library_sha256"] == hw["loaded_library_sha256"]
+            line["roofline"]["hardware" if same else "profiled_build_hardware"] = hw
     print(json.dumps(line))

@@ -154,15 +154,22 @@ def chain_roofline(W, H, L, chain_ms, ref=None, mini=None):
     t = chain_ms * 1e-3
     return {"bound": "latency (VALU, LDS and HBM all below their peaks; DESIGN.md §7b)",
             "reference_work": {"flop_eq_per_chain": mini, "rate_tops": round(mini / t / 1e12, 3),
-                               "ratio_to_valu_peak": round(mini / t / PEAK_VALU, 4),
+                               "reference_op_rate_over_valu_peak": round(mini / t / PEAK_VALU, 4),
                                "reference_chain_flop_eq": ref,
-                               "reference_chain_ratio_to_valu_peak": round(ref / t / PEAK_VALU, 4),
+                               "reference_chain_op_rate_over_valu_peak": round(ref / t / PEAK_VALU, 4),
                                "peak_tops": PEAK_VALU / 1e12,
                                "unit": "flop-eq (f32 op, texel decode, channel encode = 1 each)",
                                "note": "the reference's op count per chain time, not executed instructions (can "
                                        "exceed the peak); the executed fraction is hardware.valu_busy"},
             "hbm": {"achieved_gbs": round(12 * W * H / t / 1e9, 1), "peak_gbs": PEAK_HBM / 1e9,
                     "frac": round(12 * W * H / t / PEAK_HBM, 4), "algorithmic_bytes": 12 * W * H}}
+
+
+def library_sha256() -> str:
+    """sha256 (16 hex) of the libbh_render.so this process loads: ties a PMC summary to the build it profiled"""
+    import hashlib
+    from black_hole_ray_marching_amd import _abi
+    return hashlib.sha256(_abi.LIB_PATH.read_bytes()).hexdigest()[:16]
 
 
 def main():
@@ -178,7 +185,7 @@ def main():
     ref, passes = reference_ops(W, H, L)
     fused = bh.bloom_check(W, H, L, bh.BH_BLOOM_AUTO)
     mini = minimal_ops(fused)
-    out = {"width": W, "height": H, "levels": L, "reference_passes": passes,
+    out = {"width": W, "height": H, "levels": L, "library_sha256": library_sha256(), "reference_passes": passes,
            "reference_flop_eq_per_chain": ref, "reference_flop_eq_per_pixel": round(ref / (W * H), 1),
            "minimal_flop_eq_per_chain": mini, "minimal_flop_eq_per_pixel": round(mini / (W * H), 1),
            "algorithmic_bytes": 12 * W * H, "fused_launches": [" ".join(map(str, x)) for x in fused]}
