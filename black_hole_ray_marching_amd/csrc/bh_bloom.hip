@@ -1592,8 +1592,13 @@ __device__ __forceinline__ void yquad_tap(const float4* T, int32_t d1, int i, F4
             acc_scaled(s[b][a], q, HX + HY, i);
         }
 }
-template <int STD>
-__global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y) {
+// D2: the chain's next pass too, down2_kernel's two 2:1 downsamples of Y (bh_bloom_down2_fusable: frame sides
+// multiples of 32, every sample of both levels the 0.5 / 0.5 average of the 2x2 texels below it): a lane's quad
+// is the intermediate texel (x / 2, y / 2)'s four words, and four neighbouring lanes' intermediate words are the
+// output pixel (x / 4, y / 4)'s -- down_store's arithmetic on the same words in the same order, so the same bits,
+// and Y is not read back from memory.
+template <int STD, bool D2 = false>
+__global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y, Tex D2o) {
     __shared__ Lds L;
     __shared__ float4 tile[FP_YQ * FS_YQ + FP_YQ / 2 + 1];
     const uint32_t bx = xcd_block().x * 32u, by = xcd_block().y * 32u;
@@ -1632,6 +1637,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
     // inside the frame, and rows 8-byte aligned (even width; x is even); else one word per pixel
     auto finish = [&]() {
         const bool full = x + 1u < Y.w && y + 1u < Y.h && (Y.w & 1u) == 0u;
+        uint32_t q[4];  // the quad's words: (x, y), (x + 1, y), (x, y + 1), (x + 1, y + 1)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
             uint32_t c[2];
@@ -1640,6 +1646,7 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
                 const F4 b1 = quant(L, div12(s[b][a]));
                 const float4 v = tile[base + b * FS_YQ + a];  // the pixel's own texel (row m + b, b < 2: no shift)
                 c[a] = enc(L, remix({v.x, v.y, v.z, v.w}, b1));
+                q[2 * b + a] = c[a];
             }
             if (full) {
                 *reinterpret_cast<uint2*>(Y.px + (uint32_t)(y + b) * Y.w + x) = make_uint2(c[0], c[1]);
@@ -1648,6 +1655,15 @@ __global__ void BLOOM_BOUNDS bloom_yq_kernel(Tables tb, CTex X, TapPlan P, Tex Y
                 for (int a = 0; a < 2; ++a)
                     if (x + a < Y.w && y + b < Y.h) Y.px[(uint32_t)(y + b) * Y.w + x + a] = c[a];
             }
+        }
+        if constexpr (D2) {
+            // every lane of the block is inside the frame (sides multiples of 32): the lane exchanges are complete
+            const uint32_t mid = enc(L, down_value(L, q, 0.5f, 0.5f));  // the intermediate texel (x / 2, y / 2)
+            const int l = (int)(threadIdx.x & 63u);
+            const uint32_t w[4] = {mid, (uint32_t)__shfl_xor((int)mid, 1), (uint32_t)__shfl_xor((int)mid, 16),
+                                   (uint32_t)__shfl_xor((int)mid, 17)};
+            if ((l & 17) == 0)  // the lane of the 2x2 lane group's first quad: (x, y) multiples of 4
+                D2o.px[(y >> 2) * D2o.w + (x >> 2)] = enc(L, down_value(L, w, 0.5f, 0.5f));
         }
     };
     if constexpr (STD != 0) {
@@ -3036,15 +3052,34 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
     return (int)hipGetLastError();
 }
 
+extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_down2_fusable(uint32_t w, uint32_t h) {
+    // down2_kernel's sample arithmetic (down_at) on every pixel of both levels: texel 2 x' and 2 x' + 1, weight 0.5
+    auto axis = [](uint32_t n) {
+        if (n % 32u != 0u) return false;
+        for (uint32_t on = n / 2u, tn = n; on >= n / 4u; tn = on, on /= 2u)
+            for (uint32_t x = 0; x < on; ++x) {
+                const float t = h_sample_coord(h_texcoord(x, on), tn), f = floorf(t);
+                if (f != (float)(2u * x) || t - f != 0.5f || 2u * x + 1u > tn - 1u) return false;
+            }
+        return true;
+    };
+    return axis(w) && axis(h);
+}
+
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
                                                                       const uint8_t* buckets, const uint32_t* codes,
                                                                       const uint32_t* X, uint32_t* Y, uint32_t w,
-                                                                      uint32_t h, hipStream_t s) {
+                                                                      uint32_t h, uint32_t* d2out, bool* d2_done,
+                                                                      hipStream_t s) {
     const TapPlan P = tap_plan(w, h, w, h, w, h);
     static const bool no_quad = std::getenv("BH_BLOOM_NO_YQUAD") != nullptr;  // A/B: one pixel per lane
+    static const bool no_yd2 = std::getenv("BH_BLOOM_NO_YDOWN2") != nullptr;  // A/B: down2_kernel after the Y pass
     const bool quad = P.valid && !no_quad && P.hi_x - P.lo_x + 32 <= FP_YQ && P.hi_y - P.lo_y + 32 <= FP_YQ;
+    const bool d2 = quad && d2out && !no_yd2 && bh_bloom_down2_fusable(w, h);
+    if (d2_done) *d2_done = d2;
     if (g_dry) {  // the quad form's tile (row-pair shift) or with_source<FP_Y>
         note_launch(quad ? (std_tap_plan(P) == 12 ? "yq12" : "yq0") : "y1", w, h, w, h, w, h);
+        if (d2) note_launch("down2f", w / 4u, h / 4u, w, h, w / 2u, h / 2u);  // fused into the Y launch
         const bool ok = quad ? tile_ok(FP_YQ, FS_YQ, 2, FP_YQ * FS_YQ + FP_YQ / 2 + 1) &&
                                    tapplan_axis_ok(P, w, w, w, 0, 32u, FP_YQ) && tapplan_axis_ok(P, h, h, h, 1, 32u, FP_YQ)
                              : tile_ok(FP_Y, FP_Y, 0, FP_Y * FP_Y) && tapplan_axis_ok(P, w, w, w, 0, 16u, FP_Y) &&
@@ -3053,12 +3088,16 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const flo
     }
     if (quad) {
         const dim3 g((w + 31u) / 32u, (h + 31u) / 32u);
-        if (std_tap_plan(P) == 12)
-            hipLaunchKernelGGL(bloom_yq_kernel<12>, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P,
-                               Tex{Y, w, h});
+        const Tables tb{lut, enc, buckets, codes};
+        const Tex D{d2 ? d2out : Y, w / 4u, h / 4u};
+        if (std_tap_plan(P) == 12 && d2)
+            hipLaunchKernelGGL((bloom_yq_kernel<12, true>), g, dim3(256), 0, s, tb, CTex{X, w, h}, P, Tex{Y, w, h}, D);
+        else if (std_tap_plan(P) == 12)
+            hipLaunchKernelGGL((bloom_yq_kernel<12, false>), g, dim3(256), 0, s, tb, CTex{X, w, h}, P, Tex{Y, w, h}, D);
+        else if (d2)
+            hipLaunchKernelGGL((bloom_yq_kernel<0, true>), g, dim3(256), 0, s, tb, CTex{X, w, h}, P, Tex{Y, w, h}, D);
         else
-            hipLaunchKernelGGL(bloom_yq_kernel<0>, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{X, w, h}, P,
-                               Tex{Y, w, h});
+            hipLaunchKernelGGL((bloom_yq_kernel<0, false>), g, dim3(256), 0, s, tb, CTex{X, w, h}, P, Tex{Y, w, h}, D);
         return (int)hipGetLastError();
     }
     const uint32_t pm = P.valid ? 0u : bh_bloom_point_mask(w, h, w, h, w, h);

@@ -339,7 +339,8 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_y(const float* lut, const float* enc,
                                                                       const uint8_t* buckets, const uint32_t* codes,
                                                                       const uint32_t* X, uint32_t* Y, uint32_t w,
-                                                                      uint32_t h, hipStream_t s);
+                                                                      uint32_t h, uint32_t* d2out, bool* d2_done,
+                                                                      hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_final(const float* lut, const float* enc,
                                                                           const uint8_t* buckets, const uint32_t* codes,
                                                                           const uint32_t* col, const uint32_t* Y,

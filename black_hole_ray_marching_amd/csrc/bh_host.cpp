@@ -878,10 +878,11 @@ struct BloomRun {
     // the fused chains' blur downsamples src (res[0]) -> down[1] -> ... -> down[levels - 1]; returns the
     // last level.  An intermediate level is read by nothing but the next downsample, so pairs run as one
     // pass (bh_launch_bloom_down2, the intermediate not stored); BH_BLOOM_NO_DOWN2 runs them one by one (A/B)
-    const uint32_t* downs(const uint32_t* src, uint32_t levels, uint32_t** down, const BloomPlan& P) {
+    // first = 3: the Y pass already wrote down[2] (bh_launch_bloom_y's fused down2)
+    const uint32_t* downs(const uint32_t* src, uint32_t levels, uint32_t** down, const BloomPlan& P, uint32_t first = 1) {
         static const bool no_down2 = std::getenv("BH_BLOOM_NO_DOWN2") != nullptr;
-        const uint32_t* dn = src;
-        uint32_t l = 1;
+        const uint32_t* dn = first == 3 ? down[2] : src;
+        uint32_t l = first;
         for (; !no_down2 && l + 1 < levels && err == 0; l += 2) {
             err = bh_launch_bloom_down2(c->lut, c->enc, c->enc_b, c->enc_e, dn, P.res[l - 1][0], P.res[l - 1][1],
                                         P.res[l][0], P.res[l][1], down[l + 1], P.res[l + 1][0], P.res[l + 1][1], s);
@@ -925,11 +926,15 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
     if (fused) {
         // same-size passes are identities (same_size_identity): see bh_bloom.hip
         const uint32_t* S = X;
+        bool d2 = false;  // the Y pass also wrote the blur's first two downsamples (down[2])
         if (levels > 1) {
-            if (R.err == 0) R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H, s);
+            if (R.err == 0)
+                R.err = bh_launch_bloom_y(c->lut, c->enc, c->enc_b, c->enc_e, X, copy_in[1], W, H,
+                                          levels >= 3 ? down[2] : nullptr, &d2, s);
             S = copy_in[1];
         }
-        const uint32_t* u_src = R.downs(S, levels, down, P);  // down[0] == S; up[levels-1] == down[levels-1]
+        // down[0] == S; up[levels-1] == down[levels-1]
+        const uint32_t* u_src = R.downs(S, levels, down, P, d2 ? 3u : 1u);
         for (uint32_t l = 0; l + 1 < levels; ++l) {
             const uint32_t ti = levels - l - 2;
             R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],

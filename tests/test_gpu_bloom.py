@@ -165,9 +165,10 @@ STANDARD_FRAMES = ["512x1024", "256x512:any", "2048x4096"]  # powers of two: the
     ({"BH_BLOOM_CAP_PLAIN": "2", "BH_BLOOM_CAP_Y": "2", "BH_BLOOM_CAP_FINAL": "2"}, GENERAL_FRAMES),
     ({"BH_BLOOM_NO_STD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_UP2": "1"}, STANDARD_FRAMES),
     ({"BH_BLOOM_NO_YQUAD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_DOWN2": "1"}, STANDARD_FRAMES),
-    ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES)],
+    ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_YDOWN2": "1"}, STANDARD_FRAMES)],
     ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec", "fixup_sample", "no_sepq", "no_sep", "sepq_raw",
-         "sepq_min_blocks", "cap", "no_std", "no_up2", "no_yquad", "no_down2", "persist"])
+         "sepq_min_blocks", "cap", "no_std", "no_up2", "no_yquad", "no_down2", "persist",
+         "no_ydown2"])
 def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
     """Every run-time A/B switch of the chain (the library reads them once per process), in a child process each,
     against the oracle bit for bit: on display sizes (the general fused chain: the final epilogue's in-block fix,
@@ -175,7 +176,7 @@ def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
     of its column strips, the fix-up without its records, its per-sample form, the one-pixel separable kernel,
     the per-pixel sampler, raw tiles, quad passes capped in blocks per CU) and on powers of two (the standard
     plans: off, the general up pass instead of the 2:1 form, the Y pass one pixel per lane, no fused double
-    downsample, the persistent blocks)."""
+    downsample, the persistent blocks, the two downsamples in their own pass instead of the Y pass)."""
     import os
     import subprocess
     import sys

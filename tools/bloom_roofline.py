@@ -58,7 +58,7 @@ def minimal_ops(launches):
     for form, ow, oh, tw, th, rx, ry in launches:
         if form.startswith("sep"):
             kinds = {"0": ("up",), "1": ("up", "remix"), "2": ("up", "remix", "remix")}[form.split("/")[1][0]]
-        elif form == "down2":
+        elif form in ("down2", "down2f"):  # down2f: fused into the Y launch before it
             total += OPS["down"] * rx * ry  # the intermediate level (mw x mh)
             kinds = ("down",)
         else:
@@ -97,7 +97,9 @@ def form_of(name):
         return f"sep{int(a[0])}{'r' if a[2].strip() == 'true' else ''}/{int(a[1].strip().rstrip('u'))}"
     for k, f in (("fixup_gather_kernel<1u>", "fixup/1"), ("fixup_gather_kernel<2u>", "fixup/2"),
                  ("fixup_kernel<1u>", "fixup/1"), ("fixup_kernel<2u>", "fixup/2"), ("down2_kernel", "down2"),
-                 ("bloom_yq_kernel<12>", "yq12"), ("bloom_yq_kernel<0>", "yq0"), ("bloom_y_kernel", "y1"),
+                 ("bloom_yq_kernel<12>", "yq12"), ("bloom_yq_kernel<0>", "yq0"), ("bloom_yq_kernel<12, false>", "yq12"),
+                 ("bloom_yq_kernel<0, false>", "yq0"), ("bloom_yq_kernel<12, true>", "yq12"),
+                 ("bloom_yq_kernel<0, true>", "yq0"), ("bloom_y_kernel", "y1"),
                  ("bloom_final_kernel<48>", "final48"), ("bloom_final_kernel<0>", "final0"),
                  ("up2_kernel<12>", "up2_12"), ("up2_kernel<3>", "up2_3"), ("up2_kernel<0>", "up2_0"),
                  ("remix2_plan_kernel", "remix2_plan"), ("remix_plan_kernel", "remix_plan"),
