@@ -3053,7 +3053,9 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_pass(uint32
 }
 
 extern "C" __attribute__((visibility("hidden"))) bool bh_bloom_down2_fusable(uint32_t w, uint32_t h) {
-    // down2_kernel's sample arithmetic (down_at) on every pixel of both levels: texel 2 x' and 2 x' + 1, weight 0.5
+    // the sides multiples of 32 (the Y quad kernel's block: every lane inside the frame), and down2_kernel's
+    // sample arithmetic (down_at) on every pixel of both levels: texel 2 x' and 2 x' + 1, weight 0.5 -- which
+    // holds at powers of two, not at display sizes such as 1920 x 1080 (37 and 32 inexact samples per axis)
     auto axis = [](uint32_t n) {
         if (n % 32u != 0u) return false;
         for (uint32_t on = n / 2u, tn = n; on >= n / 4u; tn = on, on /= 2u)
