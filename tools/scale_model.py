@@ -56,9 +56,11 @@ def main():
     p.add_argument("--link-gbps", type=float, default=76.8)
     p.add_argument("--link-eff", type=float, default=1.0)
     p.add_argument("--rebalance", action="store_true")
+    p.add_argument("--unpack-ms", type=float, default=0.0365,
+                   help="frontier: rank 0's exposed unpack per frame (0: fully hidden under its render)")
     a = p.parse_args()
     if a.frontier:
-        frontier(a.one_gpu_ms, a.k)
+        frontier(a.one_gpu_ms, a.k, unpack_ms=a.unpack_ms)
         return
     rows = [json.loads(x) for x in open(a.probe) if x.startswith("{")]
     print(f"one GPU {a.one_gpu_ms} ms/frame, K = {a.k}, link {a.link_gbps} GB/s x {a.link_eff} per direction")
