@@ -904,13 +904,17 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
                 const void* blackout, uint32_t W, uint32_t H, uint32_t levels, uint32_t schedule, void* out,
                 hipStream_t s) {
     const BloomPlan P = bloom_plan(W, H, levels);
-    // AUTO: the fused chain when every same-size sample is exact (powers of two); the general fused chain
-    // when they are proven identities on stored texels (same_size_identity: the copies vanish, the remixes
-    // still sample through the same-size plan); else the literal pass list
+    // AUTO: the fused chain when every same-size sample is exact (powers of two); else the general fused chain
+    // (the remixes sample through the same-size plan; the same-size copies vanish where they are proven identities
+    // on stored texels, same_size_identity, and run as the reference's copy passes where not: 3840x2160, 3440x1440,
+    // ...); the literal pass list when a plan is refused (or BH_BLOOM_NO_GENERAL_COPIES and a copy is not an
+    // identity: the round-5 rule, A/B)
     const uint32_t wl = P.res[levels - 1][0], hl = P.res[levels - 1][1];
     const bool fused = schedule == BH_BLOOM_AUTO && same_size_exact(W) && same_size_exact(H) && same_size_exact(wl) &&
                        same_size_exact(hl);
-    const bool general = schedule == BH_BLOOM_AUTO && !fused && same_size_identity(W, H) && same_size_identity(wl, hl);
+    const bool id_full = same_size_identity(W, H), id_low = same_size_identity(wl, hl);
+    static const bool no_copies = std::getenv("BH_BLOOM_NO_GENERAL_COPIES") != nullptr;
+    const bool general = schedule == BH_BLOOM_AUTO && !fused && (!no_copies || (id_full && id_low));
     bh_ctx::SepPlan same;
     uint32_t** T = B->tex.data();
     uint32_t **copy_in = T, **remix_in0 = T + levels, **remix_in1 = T + 2 * levels;
@@ -996,12 +1000,30 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
                               : bh_launch_bloom_remix2_plan(c->lut, c->enc, c->enc_b, c->enc_e, own0, own1, aux, plan, dst,
                                                             W, H, s);
         };
+        // A copy that is not an identity (same_size_identity) runs as the literal chain's pass: X1 = copy(X) (the
+        // first loop's down[0] and remix_in0[0]), X2 = its same-size down (the blur of one level), S1 = copy(Y)
+        // (the last blur's down[0] and remix_in0[L]), and the same-size down at the blur's smallest level.
         const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
         if (levels > 1) {
-            fused_up(1u, X, W, H, full, remix_in1[0], X, nullptr, copy_in[1]);
+            const uint32_t *X1 = X, *X2 = X;
+            if (!id_full) {
+                R.pass(bh_bloom_shader_copy, X, W, H, nullptr, full, remix_in0[0], W, H);
+                R.pass(bh_bloom_shader_down, remix_in0[0], W, H, nullptr, P.res[0], blur_in, W, H);
+                X1 = remix_in0[0];
+                X2 = blur_in;
+            }
+            fused_up(1u, X2, W, H, full, remix_in1[0], X1, nullptr, copy_in[1]);
             S = copy_in[1];
         }
+        if (!id_full) {
+            R.pass(bh_bloom_shader_copy, S, W, H, nullptr, full, remix_in0[L], W, H);
+            S = remix_in0[L];
+        }
         const uint32_t* u_src = R.downs(S, levels, down, P);
+        if (!id_low) {
+            R.pass(bh_bloom_shader_down, u_src, wl, hl, nullptr, P.res[L], up[L], wl, hl);
+            u_src = up[L];
+        }
         for (uint32_t l = 0; l + 1 < levels; ++l) {
             const uint32_t ti = levels - l - 2;
             R.pass(bh_bloom_shader_up, u_src, P.res[ti + 1][0], P.res[ti + 1][1], nullptr, P.res[l], up[ti],

@@ -56,13 +56,16 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # common display widths the CPU sweep (1..2100) does not reach:
                                         # their strip tables and records
                                         (1440, 2560, 3), (2160, 3840, 3),
+                                        # sizes whose same-size copies are not identities (3840x2160, 3440x1440,
+                                        # 3840x1080, 1000x700): the general chain with the copies as passes
+                                        (1440, 3440, 3), (1080, 3840, 3), (2160, 3840, 1), (2160, 3840, 4), (700, 1000, 2),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
                                         (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
 def test_bloom_bitexact(torch_cuda, sky_small, H, W, levels, schedule):
-    """AUTO fuses the chain when its same-size passes are provably identities on stored texels (the
-    host's same_size_identity: every size here, powers of two trivially) and runs the literal pass list
-    otherwise; LITERAL always runs the pass list.  Both must give the oracle's bytes.  Power-of-two
+    """AUTO fuses the chain: its same-size copies vanish where they are provably identities on stored texels
+    (the host's same_size_identity; powers of two trivially) and run as the reference's copy passes where not
+    (3840x2160, 3440x1440, ...); LITERAL always runs the pass list.  Both must give the oracle's bytes.  Power-of-two
     sizes also take the 8-tap passes' TapPlan form (constant-offset taps) and the 2:1 up passes'
     Up2Plan form (per-parity offsets and weights), up to the full 4096x2048 frame."""
     rng = np.random.default_rng(W * 7 + H + levels)
@@ -165,10 +168,11 @@ STANDARD_FRAMES = ["512x1024", "256x512:any", "2048x4096"]  # powers of two: the
     ({"BH_BLOOM_CAP_PLAIN": "2", "BH_BLOOM_CAP_Y": "2", "BH_BLOOM_CAP_FINAL": "2"}, GENERAL_FRAMES),
     ({"BH_BLOOM_NO_STD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_UP2": "1"}, STANDARD_FRAMES),
     ({"BH_BLOOM_NO_YQUAD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_DOWN2": "1"}, STANDARD_FRAMES),
-    ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_YDOWN2": "1"}, STANDARD_FRAMES)],
+    ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_YDOWN2": "1"}, STANDARD_FRAMES),
+    ({"BH_BLOOM_NO_GENERAL_COPIES": "1"}, ["1080x3840", "700x1000:any"])],
     ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec", "fixup_sample", "no_sepq", "no_sep", "sepq_raw",
          "sepq_min_blocks", "cap", "no_std", "no_up2", "no_yquad", "no_down2", "persist",
-         "no_ydown2"])
+         "no_ydown2", "no_general_copies"])
 def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
     """Every run-time A/B switch of the chain (the library reads them once per process), in a child process each,
     against the oracle bit for bit: on display sizes (the general fused chain: the final epilogue's in-block fix,
@@ -176,7 +180,8 @@ def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
     of its column strips, the fix-up without its records, its per-sample form, the one-pixel separable kernel,
     the per-pixel sampler, raw tiles, quad passes capped in blocks per CU) and on powers of two (the standard
     plans: off, the general up pass instead of the 2:1 form, the Y pass one pixel per lane, no fused double
-    downsample, the persistent blocks, the two downsamples in their own pass instead of the Y pass)."""
+    downsample, the persistent blocks, the two downsamples in their own pass instead of the Y pass), and sizes whose
+    same-size copies are not identities through the literal pass list instead of the general chain."""
     import os
     import subprocess
     import sys
