@@ -1228,6 +1228,48 @@ __device__ __forceinline__ F4 finish_same(const Lds& L, const SameWords& s) {
     return lerp_plan(make_float4(a.r, a.g, a.b, a.a), make_float4(b.r, b.g, b.b, b.a), make_float4(c.r, c.g, c.b, c.a),
                      make_float4(d.r, d.g, d.b, d.a), s.fa, s.fb);
 }
+// The general chain's same-size copies where they are not identities (bh_host.cpp bloom_chain: the reference's
+// copy pass and the blur's same-size down, both the texel-centre sample, sample_same's arithmetic through the
+// same-size plan): out = q(S(src)).  An exact pixel's sample is its own texel, so only the inexact columns' and
+// rows' pixels gather and encode.
+// A block covers 64 x 32 pixels, 8 rows per thread: its table staging (3 KiB) is paid once per 2048 pixels.
+constexpr uint32_t SAME_COPY_ROWS = 8u;
+__global__ void __launch_bounds__(256) same_copy_kernel(Tables tb, CTex src, const uint2* __restrict__ plan, Tex out) {
+    __shared__ Lds L;
+    const uint32_t W = src.w, H = src.h;
+    const uint2 blk = xcd_block();
+    const uint32_t x = blk.x * 64u + (threadIdx.x & 63u), y0 = blk.y * (4u * SAME_COPY_ROWS) + (threadIdx.x >> 6);
+    const bool xin = x < W;
+    const uint2 cx = plan[xin ? x : 0u];
+    // every row's own word and plan entry first (independent loads: an exact pixel needs nothing else) ...
+    uint32_t own[SAME_COPY_ROWS];
+    uint2 cy[SAME_COPY_ROWS];
+#pragma unroll
+    for (uint32_t k = 0; k < SAME_COPY_ROWS; ++k) {
+        const uint32_t y = min(y0 + 4u * k, H - 1u);
+        cy[k] = plan[W + y];
+        own[k] = src.px[y * W + (xin ? x : 0u)];
+    }
+    // ... then the inexact pixels' sample words, all rows' at once
+    SameWords a[SAME_COPY_ROWS];
+#pragma unroll
+    for (uint32_t k = 0; k < SAME_COPY_ROWS; ++k) {
+        a[k] = SameWords{{own[k], 0u, 0u, 0u}, 0.0f, 0.0f};
+        if (cx.y != 0u || cy[k].y != 0u) a[k] = gather_same(src, cx, cy[k]);
+    }
+    load_tables(tb, L);
+    if (!xin) return;
+#pragma unroll
+    for (uint32_t k = 0; k < SAME_COPY_ROWS; ++k) {
+        const uint32_t y = y0 + 4u * k;
+        if (y >= H) break;
+        // an exact sample is its own texel, and q(dec(t)) == t for every stored word (the sRGB and alpha round
+        // trips, which same_size_identity's exact class checks too): the word itself
+        const bool exact = cx.y == 0u && cy[k].y == 0u;
+        out.px[y * W + x] = exact ? own[k] : enc(L, finish_same(L, a[k]));
+    }
+}
+
 // The gather form: the kernel's global reads in two dependent round trips (the list entry, then the
 // plan entries of the pixel's column and row and of their neighbours, then every texel word) with the
 // tables' staging overlapping them, instead of five (tables, list, plan, F's plan entries, texels).  A
@@ -2956,6 +2998,23 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(
     }
     hipLaunchKernelGGL(remix_plan_kernel, grid_for(w, h), dim3(256), 0, s, Tables{lut, enc, buckets, codes},
                        CTex{a, w, h}, CTex{b, w, h}, reinterpret_cast<const uint2*>(plan), Tex{out, w, h});
+    return (int)hipGetLastError();
+}
+// same_copy_kernel: out = the copy pass of src (and of the blur's same-size down: the same sample)
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_same_copy(const float* lut, const float* enc,
+                                                                              const uint8_t* buckets,
+                                                                              const uint32_t* codes, const uint32_t* src,
+                                                                              const uint32_t* plan, uint32_t* out,
+                                                                              uint32_t w, uint32_t h, hipStream_t s) {
+    if (g_dry) {  // the plan's texel indices (host copy)
+        note_launch("same_copy", w, h, w, h, w, h);
+        return chk(plan != nullptr, "same-size copy without a plan") && same_ok(w, h, plan, nullptr, 0u, 0u, false)
+                   ? 0
+                   : (int)hipErrorInvalidValue;
+    }
+    const dim3 g((w + 63u) / 64u, (h + 4u * SAME_COPY_ROWS - 1u) / (4u * SAME_COPY_ROWS));
+    hipLaunchKernelGGL(same_copy_kernel, g, dim3(256), 0, s, Tables{lut, enc, buckets, codes}, CTex{src, w, h},
+                       reinterpret_cast<const uint2*>(plan), Tex{out, w, h});
     return (int)hipGetLastError();
 }
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan(const float* lut, const float* enc,

@@ -291,6 +291,11 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix_plan(
                                                                                const uint32_t* b, const uint32_t* plan,
                                                                                uint32_t* out, uint32_t w, uint32_t h,
                                                                                hipStream_t s);
+extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_same_copy(const float* lut, const float* enc,
+                                                                              const uint8_t* buckets,
+                                                                              const uint32_t* codes, const uint32_t* src,
+                                                                              const uint32_t* plan, uint32_t* out,
+                                                                              uint32_t w, uint32_t h, hipStream_t s);
 extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_remix2_plan(const float* lut, const float* enc,
                                                                                 const uint8_t* buckets,
                                                                                 const uint32_t* codes,

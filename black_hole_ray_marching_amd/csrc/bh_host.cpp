@@ -906,7 +906,7 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
     const BloomPlan P = bloom_plan(W, H, levels);
     // AUTO: the fused chain when every same-size sample is exact (powers of two); else the general fused chain
     // (the remixes sample through the same-size plan; the same-size copies vanish where they are proven identities
-    // on stored texels, same_size_identity, and run as the reference's copy passes where not: 3840x2160, 3440x1440,
+    // on stored texels, same_size_identity, and run as same-size copy passes where not: 3840x2160, 3440x1440,
     // ...); the literal pass list when a plan is refused (or BH_BLOOM_NO_GENERAL_COPIES and a copy is not an
     // identity: the round-5 rule, A/B)
     const uint32_t wl = P.res[levels - 1][0], hl = P.res[levels - 1][1];
@@ -1006,9 +1006,11 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
         const uint32_t* S = X;  // levels 1: the loop never runs, the blur reads X itself
         if (levels > 1) {
             const uint32_t *X1 = X, *X2 = X;
-            if (!id_full) {
-                R.pass(bh_bloom_shader_copy, X, W, H, nullptr, full, remix_in0[0], W, H);
-                R.pass(bh_bloom_shader_down, remix_in0[0], W, H, nullptr, P.res[0], blur_in, W, H);
+            if (!id_full) {  // same_copy_kernel, twice
+                if (R.err == 0)
+                    R.err = bh_launch_bloom_same_copy(c->lut, c->enc, c->enc_b, c->enc_e, X, plan, remix_in0[0], W, H, s);
+                if (R.err == 0)
+                    R.err = bh_launch_bloom_same_copy(c->lut, c->enc, c->enc_b, c->enc_e, remix_in0[0], plan, blur_in, W, H, s);
                 X1 = remix_in0[0];
                 X2 = blur_in;
             }
@@ -1016,7 +1018,8 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
             S = copy_in[1];
         }
         if (!id_full) {
-            R.pass(bh_bloom_shader_copy, S, W, H, nullptr, full, remix_in0[L], W, H);
+            if (R.err == 0)
+                R.err = bh_launch_bloom_same_copy(c->lut, c->enc, c->enc_b, c->enc_e, S, plan, remix_in0[L], W, H, s);
             S = remix_in0[L];
         }
         const uint32_t* u_src = R.downs(S, levels, down, P);

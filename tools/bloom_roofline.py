@@ -46,6 +46,8 @@ FUSED_WORK = {  # bh_bloom_check form of the fused chain -> the reference passes
     "up2_12": ("up",), "up2_3": ("up",), "up2_0": ("up",), "pass_up": ("up",), "pass_up_tap": ("up",),
     "pass_down": ("down",), "pass_copy": ("copy",), "pass_remix": ("remix",), "remix_plan": ("remix",),
     "remix2_plan": ("remix", "remix"), "fixup/1": (), "fixup/1r": (), "fixup/2": (), "fixup/2r": (),
+    # the general chain's same-size copies where they are not identities (a copy pass or the blur's same-size down)
+    "same_copy": ("copy",),
 }
 
 
@@ -95,7 +97,7 @@ def form_of(name):
     if "up_sep_kernel<" in n:
         a = n.split("<")[1].rstrip(">").split(",")
         return f"sep{int(a[0])}{'r' if a[2].strip() == 'true' else ''}/{int(a[1].strip().rstrip('u'))}"
-    for k, f in (("fixup_gather_kernel<1u>", "fixup/1"), ("fixup_gather_kernel<2u>", "fixup/2"),
+    for k, f in (("same_copy_kernel", "same_copy"), ("fixup_gather_kernel<1u>", "fixup/1"), ("fixup_gather_kernel<2u>", "fixup/2"),
                  ("fixup_kernel<1u>", "fixup/1"), ("fixup_kernel<2u>", "fixup/2"), ("down2_kernel", "down2"),
                  ("bloom_yq_kernel<12>", "yq12"), ("bloom_yq_kernel<0>", "yq0"), ("bloom_yq_kernel<12, false>", "yq12"),
                  ("bloom_yq_kernel<0, false>", "yq0"), ("bloom_yq_kernel<12, true>", "yq12"),
