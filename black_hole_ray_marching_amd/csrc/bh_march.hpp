@@ -546,9 +546,8 @@ __device__ __forceinline__ float sdf_skip_slack(const SdfSlack& t) { return fmin
 
 // UNI: every active lane of the wave is at loop iteration `it` (n_rk == it: the ping-pong loop), so the
 // cap test is a wave-uniform (scalar) compare.
-// TINY (the tail's steps): a wave with a lane whose dt is tiny and nonzero (0 < |dt| < 2^-25) takes the RK
-// update in its "tiny" form (rk_update), whose ops are exact for any dt, instead of the core form whose guard
-// would send the whole step to the IEEE re-run.  The photon-sphere rays whose steps shrink below 2^-25 without
+// TINY (the tail's steps): rd + 0.5 k unfused -- the WGSL's own op order, exact for any dt -- where the fused
+// form's premise (|dt| >= 2^-25) would send a step with a tiny dt to the IEEE re-run.  The photon-sphere rays whose steps shrink below 2^-25 without
 // settling into an exact cycle take hundreds of such steps (camera B: 42 rays, ~210 tiny steps each).
 template <bool BRANCHY, class Ops, uint32_t SF = SF_DYN, bool UNI = false, bool TINY = false>
 __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, const RayState& in, RayState& out, Ops& X,
@@ -703,9 +702,10 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
     // |x| >= 2^-60, and these sums scale with dt); the rest -- the accelerations' divisions and roots, whose
     // operands do not scale with dt, and a + 2b (2b is exact at any scale) -- keeps the cores and their guards.
     v3 dro, drd;
-    auto rk_update = [&](auto TMc) {
-        constexpr bool TM = decltype(TMc)::value;
-        auto rd_half = [&](v3 v, v3 k) { return TM ? add(v, smul(0.5f, k)) : X.rd_half(v, k); };
+    // UNF (TINY): rd + 0.5 k as its two IEEE ops (XOps::rd_half's fma needs |dt| >= 2^-25)
+    auto rk_update = [&](auto UNFc) {
+        constexpr bool UNF = decltype(UNFc)::value;
+        auto rd_half = [&](v3 v, v3 k) { return UNF ? add(v, smul(0.5f, k)) : X.rd_half(v, k); };
         const v3 ro_k1 = smul(dt, rd);
         const v3 rd_k1 = smul(dt, X.template accel_qs<1>(ro, s, r2, r, y1));
         const v3 ro_k2 = smul(dt, rd_half(rd, rd_k1));
@@ -716,36 +716,25 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         const v3 rd_k4 = smul(dt, X.template accel<4>(add(ro, ro_k3), s));
         const v3 sro = add(X.add2(X.add2(ro_k1, ro_k2), ro_k3), ro_k4);
         const v3 srd = add(X.add2(X.add2(rd_k1, rd_k2), rd_k3), rd_k4);
-        if constexpr (TM) {
-            dro = mk(sro.x / 6.0f, sro.y / 6.0f, sro.z / 6.0f);
-            drd = mk(srd.x / 6.0f, srd.y / 6.0f, srd.z / 6.0f);
-        } else {
-            dro = X.template div6<0>(sro);
-            drd = X.template div6<1>(srd);
-        }
+        dro = X.template div6<0>(sro);
+        drd = X.template div6<1>(srd);
 #if !BH_FAST
         if constexpr (Ops::kCR) {
             // Domain of the division cores: every numerator is 0 or >= 2^-60 in magnitude, and
             // |s| <= 2^30, which with Q <= 2^60 (|p| <= 2^12) bounds every |s*p_i| <= 2^42.
             X.bad |= X.kmin < crm::KEY_ACC_MIN;
             X.bad |= !(X.amin >= crm::ACC_N_MIN);
-            if constexpr (!TM) {
-                X.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);  // rd_half's premise
-                X.bad |= !(X.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
-            }
+            if constexpr (!UNF) X.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);  // rd_half's premise
+            X.bad |= !(X.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
             if constexpr (!CO) X.bad |= !(fabsf(s) <= 0x1p30f);  // SF_CAM_OUT: checked once per wave
         }
 #endif
     };
-#if !BH_FAST
-    if constexpr (TINY && Ops::kCR) {
-        if (__builtin_amdgcn_ballot_w64((fabsf(dt) < 0x1p-25f) & (dt != 0.0f)) != 0ull) rk_update(std::true_type{});
-        else rk_update(std::false_type{});
-    } else
+#if BH_FAST
+    rk_update(std::false_type{});
+#else
+    rk_update(std::bool_constant<TINY && Ops::kCR>{});
 #endif
-    {
-        rk_update(std::false_type{});
-    }
     const v3 nro = add(ro, dro), nrd = add(rd, drd);                   // :315, :322
     const float ntr = travelled + dt;                                  // :324
     out.s = s;
@@ -896,36 +885,23 @@ __device__ __forceinline__ bool step_tail(const MarchArgs& a, const Frame& f, co
     G.bad |= crm::sqrt_bad(qps);
     const float dist = fminf(ds, dps);
     const float dt = fminf(dist * 0.9f, a.dtm * r);
-    // the tiny form of the RK update as step_bf's (TINY)
-    p3 dro, drd;
-    auto rk_update = [&](auto TMc) {
-        constexpr bool TM = decltype(TMc)::value;
-        auto rd_half = [&](p3 v, p3 k) { return TM ? padd(v, psmul(0.5f, k)) : pro_half(v, k); };
-        const p3 ro_k1 = psmul(dt, rd);
-        const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, sy1.y, G));
-        const p3 ro_k2 = psmul(dt, rd_half(rd, rd_k1));  // rd + 0.5 k: XOps::rd_half
-        const p3 rd_k2 = psmul(dt, paccel<2>(pro_half(ro, ro_k1), s, G));
-        const p3 ro_k3 = psmul(dt, rd_half(rd, rd_k2));
-        const p3 rd_k3 = psmul(dt, paccel<3>(pro_half(ro, ro_k2), s, G));
-        const p3 ro_k4 = psmul(dt, padd(rd, rd_k3));
-        const p3 rd_k4 = psmul(dt, paccel<4>(padd(ro, ro_k3), s, G));
-        const p3 sro = padd(padd2(padd2(ro_k1, ro_k2), ro_k3), ro_k4);
-        const p3 srd = padd(padd2(padd2(rd_k1, rd_k2), rd_k3), rd_k4);
-        if constexpr (TM) {
-            dro = {f2{sro.xy.x / 6.0f, sro.xy.y / 6.0f}, sro.z / 6.0f};
-            drd = {f2{srd.xy.x / 6.0f, srd.xy.y / 6.0f}, srd.z / 6.0f};
-        } else {
-            G.amin6 = XOps<true>::absmin3(XOps<true>::absmin3(sro.xy.x, sro.xy.y, sro.z), srd.xy.x, srd.xy.y, srd.z);
-            dro = pdiv6(sro);
-            drd = pdiv6(srd);
-            G.bad |= (fabsf(dt) < 0x1p-25f) & (dt != 0.0f);
-            G.bad |= !(G.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
-        }
-        G.bad |= G.kmin < crm::KEY_ACC_MIN;
-        G.bad |= !(G.amin >= crm::ACC_N_MIN);
-    };
-    if (__builtin_amdgcn_ballot_w64((fabsf(dt) < 0x1p-25f) & (dt != 0.0f)) != 0ull) rk_update(std::true_type{});
-    else rk_update(std::false_type{});
+    // the RK update in the tail's form (step_bf TINY): rd + 0.5 k unfused, exact for any dt
+    auto rd_half = [&](p3 v, p3 k) { return padd(v, psmul(0.5f, k)); };
+    const p3 ro_k1 = psmul(dt, rd);
+    const p3 rd_k1 = psmul(dt, paccel_qs<1>(ro, s, r2, r, sy1.y, G));
+    const p3 ro_k2 = psmul(dt, rd_half(rd, rd_k1));
+    const p3 rd_k2 = psmul(dt, paccel<2>(pro_half(ro, ro_k1), s, G));
+    const p3 ro_k3 = psmul(dt, rd_half(rd, rd_k2));
+    const p3 rd_k3 = psmul(dt, paccel<3>(pro_half(ro, ro_k2), s, G));
+    const p3 ro_k4 = psmul(dt, padd(rd, rd_k3));
+    const p3 rd_k4 = psmul(dt, paccel<4>(padd(ro, ro_k3), s, G));
+    const p3 sro = padd(padd2(padd2(ro_k1, ro_k2), ro_k3), ro_k4);
+    const p3 srd = padd(padd2(padd2(rd_k1, rd_k2), rd_k3), rd_k4);
+    G.amin6 = XOps<true>::absmin3(XOps<true>::absmin3(sro.xy.x, sro.xy.y, sro.z), srd.xy.x, srd.xy.y, srd.z);
+    const p3 dro = pdiv6(sro), drd = pdiv6(srd);
+    G.bad |= !(G.amin6 >= crm::DIV_N_MIN) & (dt != 0.0f);
+    G.bad |= G.kmin < crm::KEY_ACC_MIN;
+    G.bad |= !(G.amin >= crm::ACC_N_MIN);
     if constexpr (!CO) G.bad |= !(fabsf(s) <= 0x1p30f);
     const float ntr = travelled + dt;
     out.s = s;
