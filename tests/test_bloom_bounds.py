@@ -57,7 +57,9 @@ def _chunks(sizes, k=150):
 @pytest.mark.parametrize("schedule", [bh.BH_BLOOM_AUTO, bh.BH_BLOOM_LITERAL])
 @pytest.mark.parametrize("W,H", [(4096, 2048), (1920, 1080), (1280, 720), (8192, 4096), (2048, 1024), (7, 300),
                                  (300, 7), (1, 1), (1, 2100), (2100, 1), (53, 37),
-                                 (2560, 1440), (3840, 2160)])
+                                 (2560, 1440), (3840, 2160),
+                                 # wider than 2048: same-size copies that are not identities (same_copy passes)
+                                 (3440, 1440), (3840, 1080), (2795, 661), (2057, 890), (3121, 1017), (4000, 2200)])
 @pytest.mark.parametrize("levels", [1, 2, 3, 4, 5, 12])
 def test_reference_sizes_pass_every_bound_check(W, H, levels, schedule):
     st, n, msg = _check(W, H, levels, schedule)

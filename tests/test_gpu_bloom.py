@@ -59,6 +59,7 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # sizes whose same-size copies are not identities (3840x2160, 3440x1440,
                                         # 3840x1080, 1000x700): the general chain with the copies as passes
                                         (1440, 3440, 3), (1080, 3840, 3), (2160, 3840, 1), (2160, 3840, 4), (700, 1000, 2),
+                                        (661, 2795, 1), (890, 2057, 2), (615, 2685, 3), (1017, 3121, 4),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
                                         (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
