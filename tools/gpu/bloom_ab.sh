@@ -1,6 +1,7 @@
 #!/bin/bash
-# round 6: bloom parity, then an interleaved A/B of the chain (default vs the env arm given as $1, e.g.
-# BH_BLOOM_NO_YDOWN2=1) at the three display sizes; `notest` as $2 skips the parity tests
+# Bloom parity, then an interleaved A/B of the chain (default vs the env arm given as $1, e.g.
+# BH_BLOOM_NO_YDOWN2=1) at the three display sizes; `notest` as $2 skips the parity tests:
+#   bash tools/gpu/bloom_ab.sh ARM [notest]        -> gpurun_out/r06/bloom/<time>/
 set -u -o pipefail
 source tools/gpu/outdir.sh r06 bloom
 ARM=${1:-BH_BLOOM_NO_YDOWN2=1}

@@ -1,6 +1,7 @@
 #!/bin/bash
-# round 6: presenter parity, the app-frame bench (tools/bench_frame.py) at one frame and 16 frames per call, and a
-# rocprofv3 kernel trace of the default presenter at 1920x1080 (tools/prof_overlap.py)
+# The app's frame (bh_presenter): presenter parity, the app-frame bench (tools/bench_frame.py) at one frame and 16
+# frames per call, and rocprofv3 kernel traces of the default presenter with the march / bloom overlap they show
+# (tools/prof_overlap.py):   bash tools/gpu/frame.sh        -> gpurun_out/r06/frame/<time>/
 set -u -o pipefail
 source tools/gpu/outdir.sh r06 frame
 timeout -k 10 600 python -u -m pytest tests/test_gpu_present.py -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
