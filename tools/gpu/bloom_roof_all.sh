@@ -1,3 +1,7 @@
+#!/bin/bash
+# The bloom chain's per-kernel PMC roofline at the display sizes (tools/gpu/bloom_roofline.sh per size, then
+# tools/bloom_roofline.py with the chain time of a bench_bloom run):  bash tools/gpu/bloom_roof_all.sh
+#   -> gpurun_out/r06/bloom_roof/<W>/roofline.json (copied to profiles/r06/bloom_roof/roofline<W>.json)
 set -u -o pipefail
 for s in "1920 1080" "1280 720" "4096 2048" "3840 2160"; do
   set -- $s
