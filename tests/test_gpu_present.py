@@ -47,7 +47,9 @@ def _serial(torch, scene, cams, W, H):
 @pytest.mark.parametrize("W,H,cap,batch,bloom_cus,depth,ms", [(320, 200, 256, 1, 0, 2, 1), (320, 200, 256, 1, 16, 2, 1),
                                                               (256, 128, 512, 4, 0, 2, 2), (1280, 720, 256, 1, 0, 2, 2),
                                                               (1920, 1080, 256, 2, 8, 2, 1), (640, 360, 512, 1, 0, 4, 2),
-                                                              (512, 256, 256, 3, 0, 3, 1)])
+                                                              (512, 256, 256, 3, 0, 3, 1),
+                                                              # a width whose bloom copies run as passes
+                                                              (2795, 661, 64, 1, 0, 2, 2)])
 def test_pipelined_frames_equal_serial(torch_cuda, sky_small, W, H, cap, batch, bloom_cus, depth, ms):
     """An orbiting camera (every frame its own), 3 calls per bank reuse: the pipelined surfaces, written while
     other frames march, are the serial chain's bytes -- one frame per call, several, with the CU split, and with
