@@ -697,12 +697,10 @@ __device__ __forceinline__ bool step_bf(const MarchArgs& a, const Frame& f, cons
         dt = fminf(dist * 0.9f, dtr);                                      // :307-310
     }
     }
-    // get_delta_photon_rk4 (:134-151).  The tiny form (TM): rd + 0.5 k as the two IEEE ops (rd_half's fma is
-    // exact only for |dt| >= 2^-25) and the x/6 of the RK sums as IEEE divisions (their core's domain is
-    // |x| >= 2^-60, and these sums scale with dt); the rest -- the accelerations' divisions and roots, whose
-    // operands do not scale with dt, and a + 2b (2b is exact at any scale) -- keeps the cores and their guards.
+    // get_delta_photon_rk4 (:134-151).  UNF (the tail's steps, TINY): rd + 0.5 k as its two IEEE ops, the WGSL's
+    // order, exact for any dt (XOps::rd_half's fma equals it only for |dt| >= 2^-25); the rest keeps the cores
+    // and their guards (the x/6 core's domain, |x| >= 2^-60, is checked as always).
     v3 dro, drd;
-    // UNF (TINY): rd + 0.5 k as its two IEEE ops (XOps::rd_half's fma needs |dt| >= 2^-25)
     auto rk_update = [&](auto UNFc) {
         constexpr bool UNF = decltype(UNFc)::value;
         auto rd_half = [&](v3 v, v3 k) { return UNF ? add(v, smul(0.5f, k)) : X.rd_half(v, k); };
