@@ -2865,8 +2865,7 @@ extern "C" __attribute__((visibility("hidden"))) int bh_launch_bloom_sep(const f
     } while (0)
 #define BH_EPI(LAUNCH, ...)                                                    \
     do {                                                                       \
-        if (epi == EPI_Y && fix) LAUNCH(__VA_ARGS__, EPI_Y, true);             \
-        else if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                  \
+        if (epi == EPI_Y) LAUNCH(__VA_ARGS__, EPI_Y, _);                       \
         else if (epi == EPI_FINAL && fix) LAUNCH(__VA_ARGS__, EPI_FINAL, true); \
         else if (epi == EPI_FINAL) LAUNCH(__VA_ARGS__, EPI_FINAL, _);          \
         else LAUNCH(__VA_ARGS__, EPI_PLAIN, _);                                \

@@ -958,10 +958,9 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
         const uint32_t* list = plan ? plan + 2u * ((size_t)W + H) : nullptr;
         const uint32_t* residual = list ? list + same.nc + same.nr : nullptr;
         const uint32_t* residual2 = residual ? residual + same.nrc + same.nrr : nullptr;
-        // The Y epilogue's in-block fix is on (BH_BLOOM_NO_FIX: off, A/B); the final epilogue's (FIX2) only with
-        // BH_BLOOM_FIX2 -- measured slower than its fix-up pass (1920x1080 0.1237 -> 0.1256 ms: three block
-        // barriers in the chain's longest-lived waves; profiles/r05/bloom_fix2/)
-        static const bool no_fix = std::getenv("BH_BLOOM_NO_FIX") != nullptr;
+        // The final epilogue's in-block fix (FIX2) only with BH_BLOOM_FIX2 -- measured slower than its fix-up pass
+        // (1920x1080 0.1237 -> 0.1256 ms: three block barriers in the chain's longest-lived waves;
+        // profiles/r05/bloom_fix2/)
         static const bool fix2 = std::getenv("BH_BLOOM_FIX2") != nullptr;
         // an up pass at full size into `aux` with epilogue `epi` (own0, own1 its own-texel inputs), then the
         // fix-up of the inexact pixels -- or the plain pass and the remix kernel
@@ -969,9 +968,11 @@ int bloom_chain(bh_ctx* c, bh_ctx::BloomScratch* B, bool capturing, std::string*
                             uint32_t* aux, const uint32_t* own0, const uint32_t* own1, uint32_t* dst) {
             if (R.err != 0) return;
             bh_ctx::SepPlan sp{};
-            // the Y epilogue's in-block fix (quad kernel): its grid at the same-size plan's origin, and the fix-up
-            // pass over the residual list only
-            const bool fix = epi == 1u ? !no_fix : fix2;
+            // the epilogues' in-block fixes (quad kernel: the grid at the same-size plan's origin, the fix-up pass
+            // over the residual list only): the Y epilogue's was removed in round 6 -- it gave wrong bytes at frame
+            // sizes outside the test list (a seeded random-size sweep: e.g. 1846x1392, 177x1706) --, the final
+            // epilogue's (BH_BLOOM_FIX2) is an A/B arm; otherwise the fix-up pass covers every inexact column and row
+            const bool fix = epi == 2u && fix2;
             const uint32_t org = fix ? same.org : 0u;
             if (bh_bloom_up_uses_sep(W, H, sw, sh, res[0], res[1]))
                 sp = sep_plan(B, capturing, dry_fail, W, H, sw, sh, res[0], res[1], &R.err, org, fix);

@@ -153,6 +153,24 @@ def test_bloom_invalid_arguments(torch_cuda, sky_small):
     scene.close()
 
 
+# seeded random frame sizes (both sides 1..3300, levels 1..5): whatever fused form, plan, fix-up list and copy
+# pass the host picks for them, AUTO must give the oracle's bytes
+_RNG_SIZES = np.random.default_rng(20261018)
+RANDOM_SIZES = [(int(_RNG_SIZES.integers(1, 1300)), int(_RNG_SIZES.integers(1, 3300)), int(_RNG_SIZES.integers(1, 6)))
+                for _ in range(16)]
+
+
+@pytest.mark.parametrize("H,W,levels", RANDOM_SIZES, ids=[f"{h}x{w}L{l}" for h, w, l in RANDOM_SIZES])
+def test_bloom_bitexact_random_sizes(torch_cuda, sky_small, H, W, levels):
+    rng = np.random.default_rng(W * 31 + H * 7 + levels)
+    col, bo = _img(rng, H, W), _img(rng, H, W, sparse=True)
+    scene = bh.Scene(16, 16, sky=sky_small)
+    got = _gpu_bloom(torch_cuda, scene, col, bo, levels, bh.BH_BLOOM_AUTO)
+    want = oracle.bloom(col, bo, levels)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    scene.close()
+
+
 BLOOM_GOLDEN = sorted((__import__("pathlib").Path(__file__).parent / "golden").glob("bloom_*.npz"))
 
 
@@ -161,7 +179,7 @@ STANDARD_FRAMES = ["512x1024", "256x512:any", "2048x4096"]  # powers of two: the
 
 
 @pytest.mark.parametrize("env,frames", [
-    ({"BH_BLOOM_FIX2": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_FIX": "1"}, GENERAL_FRAMES),
+    ({"BH_BLOOM_FIX2": "1"}, GENERAL_FRAMES),
     ({"BH_BLOOM_ORG_KEEP": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_STRIPS": "1"}, GENERAL_FRAMES),
     ({"BH_BLOOM_FIXUP_NOREC": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_FIXUP_SAMPLE": "1"}, GENERAL_FRAMES),
     ({"BH_BLOOM_NO_SEPQ": "1"}, GENERAL_FRAMES), ({"BH_BLOOM_NO_SEP": "1"}, GENERAL_FRAMES),
@@ -171,13 +189,13 @@ STANDARD_FRAMES = ["512x1024", "256x512:any", "2048x4096"]  # powers of two: the
     ({"BH_BLOOM_NO_YQUAD": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_DOWN2": "1"}, STANDARD_FRAMES),
     ({"BH_BLOOM_PERSIST": "1"}, STANDARD_FRAMES), ({"BH_BLOOM_NO_YDOWN2": "1"}, STANDARD_FRAMES),
     ({"BH_BLOOM_NO_GENERAL_COPIES": "1"}, ["1080x3840", "700x1000:any"])],
-    ids=["fix2", "no_fix", "org_keep", "no_strips", "fixup_norec", "fixup_sample", "no_sepq", "no_sep", "sepq_raw",
+    ids=["fix2", "org_keep", "no_strips", "fixup_norec", "fixup_sample", "no_sepq", "no_sep", "sepq_raw",
          "sepq_min_blocks", "cap", "no_std", "no_up2", "no_yquad", "no_down2", "persist",
          "no_ydown2", "no_general_copies"])
 def test_bloom_switches_stay_bitexact(torch_cuda, env, frames):
     """Every run-time A/B switch of the chain (the library reads them once per process), in a child process each,
     against the oracle bit for bit: on display sizes (the general fused chain: the final epilogue's in-block fix,
-    no in-block fix, grid origins that keep the block count, the final fix-up from the row-major textures instead
+    grid origins that keep the block count, the final fix-up from the row-major textures instead
     of its column strips, the fix-up without its records, its per-sample form, the one-pixel separable kernel,
     the per-pixel sampler, raw tiles, quad passes capped in blocks per CU) and on powers of two (the standard
     plans: off, the general up pass instead of the 2:1 form, the Y pass one pixel per lane, no fused double
