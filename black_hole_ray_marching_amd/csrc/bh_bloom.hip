@@ -1336,7 +1336,11 @@ __global__ void __launch_bounds__(256) fixup_gather_kernel(Tables tb, CTex A, CT
         live = live && x < W && y < H;  // defensive: a list entry outside the frame
         cx = PX[1];
         cy = PY[1];
-        if (!live) { x = y = 0u; cx = plan[0]; cy = plan[W]; PX[0] = PX[2] = cx; PY[0] = PY[2] = cy; }
+        // a dead lane (past the list, or a row lane's defensive case) gathers at pixel (0, 0) with every neighbour
+        // entry its own: the record it read (entry 0 for a lane past the list, a column record) must not leave a
+        // column's entry among the row ones, whose texel indices would then index rows (round 6's memory fault
+        // at 3996 x 495: tools/bloom_fixup_addr.cpp)
+        if (!live) { x = y = 0u; cx = plan[0]; cy = plan[W]; PX[0] = PX[1] = PX[2] = cx; PY[0] = PY[1] = PY[2] = cy; }
     } else {
         if (i < nc) {
             x = list[i / H];

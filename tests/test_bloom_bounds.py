@@ -125,3 +125,22 @@ def test_the_checks_catch_a_footprint_that_overfills_its_tile():
     n, _, msg = r.stdout.strip().partition(" ")
     assert int(n) >= 1, r.stdout
     assert "tile" in msg or "footprint" in msg or "span" in msg, msg
+
+
+def test_fixup_lane_addresses_stay_inside(tmp_path):
+    """The final fix-up pass's global reads lane by lane (tools/bloom_fixup_addr.cpp, a host emulation of
+    fixup_gather_kernel<EPI_FINAL> with records and column strips, from the library's own plan builders in
+    its bh_bloom.o): every index inside its buffer -- the dead lanes past the list included, whose stale
+    column record indexed rows at 3996 x 495 (round 6's GPU memory fault)."""
+    obj = ROOT / "black_hole_ray_marching_amd" / "_build" / "bh_bloom.o"
+    hipcc = Path(os.environ.get("HIPCC", "/opt/rocm/bin/hipcc"))
+    if not obj.exists() or not hipcc.exists():
+        pytest.skip("needs the built bh_bloom.o and hipcc")
+    o, exe = tmp_path / "fa.o", tmp_path / "fa"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-c", str(ROOT / "tools" / "bloom_fixup_addr.cpp"), "-o", str(o)], check=True)
+    subprocess.run([str(hipcc), "--offload-arch=gfx950", str(o), str(obj), "-o", str(exe)], check=True)
+    named = ["3996", "495", "1868", "83", "3840", "2160", "1920", "1080", "1", "1", "4096", "1"]
+    r = subprocess.run([str(exe), *named], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-2000:]
+    r = subprocess.run([str(exe), "sweep", "150", "6", "4200", "2300"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]

@@ -1,7 +1,9 @@
 """One frame of the bloom chain (AUTO) against the oracle, for bisecting a mismatch over the library's run-time
 switches: the parent runs the frame once per switch set given, each in a child process (the library reads its
 switches once per process), with test_gpu_bloom's inputs (test_bloom_bitexact_random_sizes).
-    python tools/bloom_bisect.py H W LEVELS [ENV=1[,ENV2=1] ...]"""
+    python tools/bloom_bisect.py H W LEVELS [ENV=1[,ENV2=1] | default ...]
+Arms run in the order given (no arm: the default only); the first child that fails (a GPU fault, an exception)
+ends the run with its exit status -- nothing more runs on the GPU after a fault."""
 import json
 import os
 import subprocess
@@ -41,10 +43,15 @@ if __name__ == "__main__":
         child(*(int(v) for v in sys.argv[1:4]))
         sys.exit(0)
     H, W, L = sys.argv[1:4]
-    for arm in [""] + sys.argv[4:]:
+    for arm in sys.argv[4:] or ["default"]:
+        arm = "" if arm == "default" else arm
         env = dict(os.environ, BISECT_CHILD="1", BISECT_TAG=arm or "default", PYTHONPATH=str(ROOT))
         for kv in filter(None, arm.split(",")):
             k, v = kv.split("=")
             env[k] = v
+        print(json.dumps({"arm": arm or "default", "W": int(W), "H": int(H), "levels": int(L)}), flush=True)
         r = subprocess.run([sys.executable, __file__, H, W, L], env=env, capture_output=True, text=True, timeout=300)
         print(r.stdout.strip() or r.stderr[-1500:], flush=True)
+        if r.returncode != 0:
+            print(r.stderr[-1500:], flush=True)
+            sys.exit(r.returncode)
