@@ -60,6 +60,10 @@ def _gpu_bloom(torch, scene, col, bo, levels, schedule):
                                         # 3840x1080, 1000x700): the general chain with the copies as passes
                                         (1440, 3440, 3), (1080, 3840, 3), (2160, 3840, 1), (2160, 3840, 4), (700, 1000, 2),
                                         (661, 2795, 1), (890, 2057, 2), (615, 2685, 3), (1017, 3121, 4),
+                                        # round 6's random-size sweep: the fix-up's dead lanes read far past
+                                        # the texture at 3996x495 (a memory fault), harmlessly at 1868x83
+                                        # (DESIGN.md §7b); wrong bytes of the removed Y in-block fix at 1846x1392
+                                        (495, 3996, 1), (83, 1868, 1), (1392, 1846, 3), (656, 1261, 5),
                                         # the 65536 side limit (a refused plan must fall back to
                                         # the general kernel, not fail the call; tests/test_bloom_bounds.py)
                                         (8, 65536, 3), (65536, 8, 3), (6, 65535, 2)])
